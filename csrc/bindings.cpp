@@ -1,0 +1,489 @@
+// torch operator registrations (namespace `shai`) for the gfx950 HIP kernels.
+// Every op writes into caller-allocated outputs on the current HIP stream and
+// never allocates or synchronises, so the ops are hipGraph-capturable.
+// Shape/stride/alignment preconditions the kernels rely on are checked here,
+// on the host, before launch (a bad launch on the box can reset the node).
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include "kernels/launchers.h"
+
+using at::Tensor;
+using c10::optional;
+
+namespace {
+
+#define SHAI_CHECK(cond, ...) TORCH_CHECK(cond, "shai: ", __VA_ARGS__)
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+const shai::bf16_t* cptr(const Tensor& t) { return reinterpret_cast<const shai::bf16_t*>(t.data_ptr()); }
+shai::bf16_t* mptr(const Tensor& t) { return reinterpret_cast<shai::bf16_t*>(t.data_ptr()); }
+const shai::bf16_t* optr(const optional<Tensor>& t) { return t.has_value() ? cptr(*t) : nullptr; }
+
+void check_bf16(const Tensor& t, const char* name) {
+  SHAI_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  SHAI_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16, got ", t.scalar_type());
+  SHAI_CHECK(t.stride(-1) == 1, name, " last dim must be contiguous");
+  SHAI_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+void check_f32(const Tensor& t, const char* name) {
+  SHAI_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), name, " must be contiguous f32 GPU");
+}
+void check_i32(const Tensor& t, const char* name) {
+  SHAI_CHECK(t.is_cuda() && t.scalar_type() == at::kInt && t.is_contiguous(), name, " must be contiguous int32 GPU");
+}
+void check_rows(const Tensor& t, const char* name) {
+  check_bf16(t, name);
+  for (int d = 0; d + 1 < t.dim(); ++d) SHAI_CHECK(t.stride(d) % 8 == 0 || t.size(d) == 1, name, " stride not 16B aligned");
+}
+
+// ---------------------------------------------------------------- norms
+void rmsnorm(const Tensor& x, const optional<Tensor>& w, const Tensor& out, const optional<Tensor>& residual,
+             const optional<Tensor>& residual_out, double eps, double w_offset) {
+  check_rows(x, "x");
+  check_rows(out, "out");
+  const int D = x.size(-1);
+  SHAI_CHECK(D % 8 == 0 && D <= 8192, "rmsnorm D must be a multiple of 8 and <= 8192");
+  const long rows = x.numel() / D;
+  SHAI_CHECK(x.dim() == 2 || x.is_contiguous(), "rmsnorm x must be 2D strided or contiguous");
+  shai::RowNormArgs a{};
+  a.x = cptr(x);
+  a.w = optr(w);
+  a.out = mptr(out);
+  if (residual) {
+    SHAI_CHECK(residual->is_contiguous() && x.is_contiguous(), "residual path needs contiguous tensors");
+    a.residual = cptr(*residual);
+    a.residual_out = residual_out ? mptr(*residual_out) : nullptr;
+  }
+  a.rows = rows;
+  a.D = D;
+  a.x_stride = x.dim() == 2 ? x.stride(0) : D;
+  a.out_stride = out.dim() == 2 ? out.stride(0) : D;
+  a.eps = eps;
+  a.w_offset = w_offset;
+  shai::launch_rmsnorm(a, stream());
+}
+
+void layernorm(const Tensor& x, const optional<Tensor>& w, const optional<Tensor>& b, const Tensor& out,
+               const optional<Tensor>& residual, const optional<Tensor>& residual_out, double eps) {
+  check_rows(x, "x");
+  check_rows(out, "out");
+  const int D = x.size(-1);
+  SHAI_CHECK(D % 8 == 0 && D <= 8192, "layernorm D must be a multiple of 8 and <= 8192");
+  SHAI_CHECK(x.dim() == 2 || x.is_contiguous(), "layernorm x must be 2D strided or contiguous");
+  shai::RowNormArgs a{};
+  a.x = cptr(x);
+  a.w = optr(w);
+  a.b = optr(b);
+  a.out = mptr(out);
+  if (residual) {
+    SHAI_CHECK(residual->is_contiguous() && x.is_contiguous(), "residual path needs contiguous tensors");
+    a.residual = cptr(*residual);
+    a.residual_out = residual_out ? mptr(*residual_out) : nullptr;
+  }
+  a.rows = x.numel() / D;
+  a.D = D;
+  a.x_stride = x.dim() == 2 ? x.stride(0) : D;
+  a.out_stride = out.dim() == 2 ? out.stride(0) : D;
+  a.eps = eps;
+  a.w_offset = 0.f;
+  shai::launch_layernorm(a, stream());
+}
+
+void groupnorm_stats(const Tensor& x, const optional<Tensor>& gamma, const optional<Tensor>& beta,
+                     const Tensor& partials, const Tensor& scale, const Tensor& shift, int64_t G, double eps) {
+  check_bf16(x, "x");
+  SHAI_CHECK(x.is_contiguous() && x.dim() == 3, "groupnorm x must be contiguous [N, HW, C]");
+  check_f32(partials, "partials");
+  check_f32(scale, "scale");
+  check_f32(shift, "shift");
+  const int N = x.size(0), HW = x.size(1), C = x.size(2);
+  SHAI_CHECK(C % 8 == 0 && C % G == 0 && C <= 4096 && G <= 128, "groupnorm: bad C/G");
+  SHAI_CHECK(partials.numel() >= (long)N * shai::gn_num_blocks(HW) * G * 2, "partials too small");
+  SHAI_CHECK(scale.numel() >= (long)N * C && shift.numel() >= (long)N * C, "scale/shift too small");
+  shai::GroupNormArgs a{};
+  a.x = cptr(x);
+  a.gamma = optr(gamma);
+  a.beta = optr(beta);
+  a.partials = partials.data_ptr<float>();
+  a.scale = scale.data_ptr<float>();
+  a.shift = shift.data_ptr<float>();
+  a.N = N;
+  a.HW = HW;
+  a.C = C;
+  a.G = G;
+  a.eps = eps;
+  shai::launch_groupnorm_stats(a, stream());
+}
+
+void groupnorm_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const Tensor& out, bool silu) {
+  check_bf16(x, "x");
+  check_bf16(out, "out");
+  SHAI_CHECK(x.is_contiguous() && out.is_contiguous() && x.dim() == 3, "groupnorm_apply needs contiguous [N,HW,C]");
+  check_f32(scale, "scale");
+  check_f32(shift, "shift");
+  shai::GroupNormArgs a{};
+  a.x = cptr(x);
+  a.scale = scale.data_ptr<float>();
+  a.shift = shift.data_ptr<float>();
+  a.out = mptr(out);
+  a.N = x.size(0);
+  a.HW = x.size(1);
+  a.C = x.size(2);
+  SHAI_CHECK(a.C % 8 == 0, "C % 8");
+  a.silu = silu;
+  shai::launch_groupnorm_apply(a, stream());
+}
+
+// ---------------------------------------------------------------- GEMM
+// a: [M, K] or [B, M, K]; w: [N, K] or [B, N, K]; c: [M, N'] or [B, M, N'] (N' = N or N/2 for glu)
+void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tensor>& bias,
+          const optional<Tensor>& bias2d, int64_t rows_per_bias2d, const optional<Tensor>& residual, double alpha,
+          double res_alpha, int64_t act, bool glu) {
+  check_rows(a, "a");
+  check_rows(w, "w");
+  check_bf16(c, "c");
+  SHAI_CHECK(a.dim() == w.dim() || w.dim() == 2, "gemm rank mismatch");
+  const bool batched = a.dim() == 3;
+  shai::GemmArgs g{};
+  g.A = cptr(a);
+  g.W = cptr(w);
+  g.C = mptr(c);
+  g.M = a.size(-2);
+  g.K = a.size(-1);
+  g.N = w.size(-2);
+  SHAI_CHECK(w.size(-1) == g.K, "gemm K mismatch: a ", a.sizes(), " w ", w.sizes());
+  SHAI_CHECK(g.K % 8 == 0, "gemm K must be a multiple of 8");
+  SHAI_CHECK(c.size(-2) == g.M && c.size(-1) == (glu ? g.N / 2 : g.N), "gemm output shape mismatch ", c.sizes());
+  SHAI_CHECK(!glu || g.N % 4 == 0, "glu needs N % 4 == 0");
+  g.lda = a.stride(-2);
+  g.ldw = w.stride(-2);
+  g.ldc = c.stride(-2);
+  g.batch = batched ? a.size(0) : 1;
+  g.batch_a = batched ? a.stride(0) : 0;
+  g.batch_w = (batched && w.dim() == 3) ? w.stride(0) : 0;
+  g.batch_c = batched ? c.stride(0) : 0;
+  if (bias) {
+    check_bf16(*bias, "bias");
+    SHAI_CHECK(bias->numel() == g.N, "bias size");
+    g.bias = cptr(*bias);
+  }
+  if (bias2d) {
+    check_bf16(*bias2d, "bias2d");
+    SHAI_CHECK(bias2d->is_contiguous() && bias2d->size(-1) == g.N && rows_per_bias2d > 0, "bias2d shape");
+    g.bias2d = cptr(*bias2d);
+    g.rows_per_bias2d = rows_per_bias2d;
+  }
+  if (residual) {
+    check_bf16(*residual, "residual");
+    SHAI_CHECK(residual->size(-2) == g.M && residual->size(-1) == c.size(-1), "residual shape");
+    g.residual = cptr(*residual);
+    g.ldr = residual->stride(-2);
+    g.batch_r = batched ? residual->stride(0) : 0;
+  }
+  g.alpha = alpha;
+  g.res_alpha = res_alpha;
+  g.act = act;
+  g.glu = glu;
+  shai::launch_gemm(g, stream());
+}
+
+// x: [N, H, W, C1] NHWC; x2 optional [N, H, W, C2]; w: [Cout, KH*KW*Cin]; out: [N, OH, OW, Cout]
+void conv2d(const Tensor& x, const optional<Tensor>& x2, const Tensor& w, const Tensor& out,
+            const optional<Tensor>& bias, const optional<Tensor>& bias2d, const optional<Tensor>& residual,
+            const optional<Tensor>& in_scale, const optional<Tensor>& in_shift, int64_t in_act, int64_t kh,
+            int64_t kw, int64_t stride, int64_t pad, bool upsample, int64_t act, double res_alpha) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_bf16(out, "out");
+  SHAI_CHECK(x.is_contiguous() && out.is_contiguous() && w.is_contiguous(), "conv2d needs contiguous tensors");
+  SHAI_CHECK(x.dim() == 4 && out.dim() == 4, "conv2d needs NHWC 4D tensors");
+  shai::GemmArgs g{};
+  g.conv = 1;
+  g.Nimg = x.size(0);
+  g.H = x.size(1);
+  g.Wd = x.size(2);
+  g.Cin1 = x.size(3);
+  g.Cin = g.Cin1;
+  if (x2) {
+    check_bf16(*x2, "x2");
+    SHAI_CHECK(x2->is_contiguous() && x2->size(0) == g.Nimg && x2->size(1) == g.H && x2->size(2) == g.Wd, "x2 shape");
+    g.A2 = cptr(*x2);
+    g.Cin += x2->size(3);
+  }
+  SHAI_CHECK(g.Cin % 8 == 0 && g.Cin1 % 8 == 0, "conv2d: input channels must be multiples of 8");
+  g.KH = kh;
+  g.KW = kw;
+  g.stride = stride;
+  g.pad = pad;
+  g.upsample = upsample;
+  const int IH = upsample ? 2 * g.H : g.H, IW = upsample ? 2 * g.Wd : g.Wd;
+  SHAI_CHECK(!upsample || stride == 1, "upsample requires stride 1");
+  g.OH = (IH + 2 * pad - kh) / stride + 1;
+  g.OW = (IW + 2 * pad - kw) / stride + 1;
+  SHAI_CHECK(out.size(0) == g.Nimg && out.size(1) == g.OH && out.size(2) == g.OW, "conv2d out shape ", out.sizes(),
+             " expected spatial ", g.OH, "x", g.OW);
+  g.N = out.size(3);
+  g.K = kh * kw * g.Cin;
+  SHAI_CHECK(w.size(0) == g.N && w.numel() == (long)g.N * g.K, "conv2d weight must be [Cout, KH*KW*Cin]");
+  g.M = g.Nimg * g.OH * g.OW;
+  g.A = cptr(x);
+  g.W = cptr(w);
+  g.C = mptr(out);
+  g.lda = g.K;
+  g.ldw = g.K;
+  g.ldc = g.N;
+  g.batch = 1;
+  g.alpha = 1.f;
+  g.res_alpha = res_alpha;
+  g.act = act;
+  if (bias) {
+    check_bf16(*bias, "bias");
+    g.bias = cptr(*bias);
+  }
+  if (bias2d) {
+    check_bf16(*bias2d, "bias2d");
+    SHAI_CHECK(bias2d->is_contiguous() && bias2d->size(0) == g.Nimg && bias2d->size(-1) == g.N, "bias2d [N, Cout]");
+    g.bias2d = cptr(*bias2d);
+    g.rows_per_bias2d = g.OH * g.OW;
+  }
+  if (residual) {
+    check_bf16(*residual, "residual");
+    SHAI_CHECK(residual->is_contiguous() && residual->numel() == (long)g.M * g.N, "residual shape");
+    g.residual = cptr(*residual);
+    g.ldr = g.N;
+  }
+  if (in_scale) {
+    SHAI_CHECK(in_shift.has_value(), "in_scale requires in_shift");
+    check_f32(*in_scale, "in_scale");
+    check_f32(*in_shift, "in_shift");
+    SHAI_CHECK(in_scale->numel() == (long)g.Nimg * g.Cin, "in_scale must be [N, Cin]");
+    g.in_scale = in_scale->data_ptr<float>();
+    g.in_shift = in_shift->data_ptr<float>();
+    g.in_act = in_act;
+  }
+  shai::launch_gemm(g, stream());
+}
+
+// ---------------------------------------------------------------- attention
+void flash_attn(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, double scale, bool causal,
+                int64_t causal_offset, const optional<Tensor>& kv_lens, const optional<Tensor>& q_lens,
+                const optional<Tensor>& bias, const optional<Tensor>& block_table) {
+  check_rows(q, "q");
+  check_rows(k, "k");
+  check_rows(v, "v");
+  check_rows(o, "o");
+  SHAI_CHECK(q.dim() == 4 && o.dim() == 4, "q/o must be [B, S, H, D]");
+  shai::AttnArgs a{};
+  a.B = q.size(0);
+  a.Sq = q.size(1);
+  a.Hq = q.size(2);
+  a.D = q.size(3);
+  SHAI_CHECK(a.D == 64 || a.D == 128, "flash_attn supports head dim 64 / 128, got ", a.D);
+  SHAI_CHECK(q.stride(2) == a.D && o.stride(2) == a.D, "heads must be packed (head stride == D)");
+  if (block_table) {
+    // k/v are caches [num_blocks, Hkv, 64, D]
+    SHAI_CHECK(k.dim() == 4 && k.size(2) == 64 && k.size(3) == a.D && k.is_contiguous() && v.is_contiguous(),
+               "paged k/v must be [blocks, Hkv, 64, D]");
+    check_i32(*block_table, "block_table");
+    SHAI_CHECK(kv_lens.has_value(), "paged attention needs kv_lens");
+    a.Hkv = k.size(1);
+    a.block_table = block_table->data_ptr<int>();
+    a.max_blocks = block_table->size(1);
+    a.kc_bs = k.stride(0);
+    a.kc_hs = k.stride(1);
+    a.Skv = a.max_blocks * 64;
+  } else {
+    SHAI_CHECK(k.dim() == 4 && v.dim() == 4 && k.size(3) == a.D && k.stride(2) == a.D && v.stride(2) == a.D,
+               "k/v must be [B, S, Hkv, D] with packed heads");
+    a.Hkv = k.size(2);
+    a.Skv = k.size(1);
+    a.k_bs = k.size(0) == 1 ? 0 : k.stride(0);
+    a.k_ts = k.stride(1);
+    a.v_bs = v.size(0) == 1 ? 0 : v.stride(0);
+    a.v_ts = v.stride(1);
+  }
+  SHAI_CHECK(a.Hq % a.Hkv == 0, "Hq must be a multiple of Hkv");
+  a.q = cptr(q);
+  a.k = cptr(k);
+  a.v = cptr(v);
+  a.o = mptr(o);
+  a.q_bs = q.stride(0);
+  a.q_ts = q.stride(1);
+  a.o_bs = o.stride(0);
+  a.o_ts = o.stride(1);
+  a.scale = scale;
+  a.causal = causal;
+  a.causal_offset = causal_offset;
+  if (kv_lens) {
+    check_i32(*kv_lens, "kv_lens");
+    a.kv_lens = kv_lens->data_ptr<int>();
+  }
+  if (q_lens) {
+    check_i32(*q_lens, "q_lens");
+    a.q_lens = q_lens->data_ptr<int>();
+  }
+  if (bias) {
+    check_bf16(*bias, "bias");
+    SHAI_CHECK(bias->is_contiguous() && bias->numel() == (long)a.Hq * a.Sq * a.Skv, "bias must be [Hq, Sq, Skv]");
+    a.bias = cptr(*bias);
+  }
+  shai::launch_flash_attn(a, stream());
+}
+
+void decode_attn(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& o,
+                 const Tensor& block_table, const Tensor& ctx_lens, const Tensor& ws, int64_t num_splits,
+                 double scale) {
+  check_rows(q, "q");
+  check_rows(o, "o");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_i32(block_table, "block_table");
+  check_i32(ctx_lens, "ctx_lens");
+  check_f32(ws, "ws");
+  SHAI_CHECK(q.dim() == 3 && k_cache.dim() == 4 && k_cache.size(2) == 64, "decode_attn shapes");
+  shai::DecodeAttnArgs a{};
+  a.B = q.size(0);
+  a.Hq = q.size(1);
+  a.D = q.size(2);
+  a.Hkv = k_cache.size(1);
+  SHAI_CHECK(a.D == 64 || a.D == 128, "decode_attn head dim 64/128");
+  SHAI_CHECK(a.Hq % a.Hkv == 0 && a.Hq / a.Hkv <= 8, "decode_attn GQA group must be <= 8");
+  SHAI_CHECK(q.stride(1) == a.D && o.stride(1) == a.D, "packed heads");
+  a.q = cptr(q);
+  a.o = mptr(o);
+  a.k_cache = cptr(k_cache);
+  a.v_cache = cptr(v_cache);
+  a.block_table = block_table.data_ptr<int>();
+  a.ctx_lens = ctx_lens.data_ptr<int>();
+  a.max_blocks = block_table.size(1);
+  a.num_splits = num_splits;
+  a.ws = ws.data_ptr<float>();
+  SHAI_CHECK(ws.numel() * 4 >= (long)shai::decode_attn_workspace(a.B, a.Hq, a.D, num_splits), "ws too small");
+  a.q_bs = q.stride(0);
+  a.o_bs = o.stride(0);
+  a.scale = scale;
+  shai::launch_decode_attn(a, stream());
+}
+
+void kv_write(const Tensor& k, const Tensor& v, const Tensor& k_cache, const Tensor& v_cache, const Tensor& slots) {
+  check_rows(k, "k");
+  check_rows(v, "v");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_i32(slots, "slots");
+  SHAI_CHECK(k.dim() == 3 && k_cache.dim() == 4, "k [T, Hkv, D], cache [blocks, Hkv, 64, D]");
+  SHAI_CHECK(k.stride(1) == k.size(2) && v.stride(1) == v.size(2), "packed heads");
+  shai::launch_kv_write(cptr(k), cptr(v), mptr(k_cache), mptr(v_cache), slots.data_ptr<int>(), k.size(0), k.size(1),
+                        k.size(2), k.stride(0), v.stride(0), stream());
+}
+
+// ---------------------------------------------------------------- elementwise
+void gated_act(const Tensor& x, const Tensor& out, int64_t act, bool gate_first) {
+  check_rows(x, "x");
+  check_bf16(out, "out");
+  SHAI_CHECK(out.is_contiguous(), "out contiguous");
+  const int F = out.size(-1);
+  SHAI_CHECK(x.size(-1) == 2 * F && F % 8 == 0, "gated_act: x last dim must be 2*F, F % 8 == 0");
+  const long rows = out.numel() / F;
+  const long xs = x.dim() >= 2 ? x.stride(-2) : 2 * F;
+  SHAI_CHECK(x.dim() == 2 || x.is_contiguous(), "gated_act x must be 2D strided or contiguous");
+  shai::launch_gated_act(cptr(x), mptr(out), rows, F, xs, act, gate_first, stream());
+}
+
+void bias_act(const Tensor& x, const optional<Tensor>& bias, const optional<Tensor>& residual, const Tensor& out,
+              int64_t act, double alpha) {
+  check_bf16(x, "x");
+  check_bf16(out, "out");
+  SHAI_CHECK(x.is_contiguous() && out.is_contiguous(), "bias_act contiguous");
+  const int D = x.size(-1);
+  SHAI_CHECK(D % 8 == 0, "D % 8");
+  if (residual) SHAI_CHECK(residual->is_contiguous() && residual->numel() == x.numel(), "residual");
+  shai::launch_bias_act(cptr(x), optr(bias), optr(residual), mptr(out), x.numel() / D, D, act, alpha, stream());
+}
+
+void rope(const Tensor& x, const Tensor& positions, const Tensor& cos, const Tensor& sin, int64_t rot_dim, bool neox) {
+  check_bf16(x, "x");
+  check_i32(positions, "positions");
+  check_f32(cos, "cos");
+  check_f32(sin, "sin");
+  SHAI_CHECK(x.dim() == 3 && x.stride(1) == x.size(2), "rope x must be [T, H, Dh] with packed heads");
+  shai::launch_rope(mptr(x), positions.data_ptr<int>(), cos.data_ptr<float>(), sin.data_ptr<float>(), x.size(0),
+                    x.size(1), x.size(2), rot_dim, x.stride(0), neox, stream());
+}
+
+void rope_pairs(const Tensor& x, const Tensor& cos, const Tensor& sin) {
+  check_bf16(x, "x");
+  check_f32(cos, "cos");
+  check_f32(sin, "sin");
+  SHAI_CHECK(x.dim() == 4 && x.stride(2) == x.size(3) && x.size(3) % 8 == 0, "rope_pairs x [B, T, H, Dh]");
+  SHAI_CHECK(cos.numel() == x.size(1) * x.size(3) / 2, "cos/sin must be [T, Dh/2]");
+  shai::launch_rope_pairs(mptr(x), cos.data_ptr<float>(), sin.data_ptr<float>(), x.size(0), x.size(1), x.size(2),
+                          x.size(3), x.stride(0), x.stride(1), stream());
+}
+
+void sched_step(const Tensor& model_out, const Tensor& latents, bool cfg, double guidance, int64_t pred_type,
+                double a_t, double a_prev, double dt) {
+  check_bf16(model_out, "model_out");
+  check_bf16(latents, "latents");
+  SHAI_CHECK(model_out.is_contiguous() && latents.is_contiguous(), "sched_step contiguous");
+  const long n = latents.numel();
+  SHAI_CHECK(n % 8 == 0 && model_out.numel() == (cfg ? 2 * n : n), "sched_step sizes");
+  shai::launch_sched_step(cptr(model_out), mptr(latents), n, cfg, guidance, pred_type, a_t, a_prev, dt, stream());
+}
+
+void softmax_(const Tensor& x, double scale) {
+  check_bf16(x, "x");
+  SHAI_CHECK(x.is_contiguous() && x.size(-1) % 8 == 0, "softmax contiguous, D % 8");
+  shai::launch_softmax(mptr(x), x.numel() / x.size(-1), x.size(-1), scale, stream());
+}
+
+void embedding(const Tensor& ids, const Tensor& table, const Tensor& out) {
+  check_i32(ids, "ids");
+  check_bf16(table, "table");
+  check_bf16(out, "out");
+  SHAI_CHECK(table.is_contiguous() && out.is_contiguous() && table.size(1) % 8 == 0, "embedding shapes");
+  shai::launch_embedding(ids.data_ptr<int>(), cptr(table), mptr(out), ids.numel(), table.size(1), stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(shai, m) {
+  m.def("rmsnorm(Tensor x, Tensor? w, Tensor(a!) out, Tensor? residual, Tensor(b!)? residual_out, float eps, float w_offset) -> ()");
+  m.def("layernorm(Tensor x, Tensor? w, Tensor? b, Tensor(a!) out, Tensor? residual, Tensor(b!)? residual_out, float eps) -> ()");
+  m.def("groupnorm_stats(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!) partials, Tensor(b!) scale, Tensor(c!) shift, int G, float eps) -> ()");
+  m.def("groupnorm_apply(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, bool silu) -> ()");
+  m.def("gemm(Tensor a, Tensor w, Tensor(a!) c, Tensor? bias, Tensor? bias2d, int rows_per_bias2d, Tensor? residual, float alpha, float res_alpha, int act, bool glu) -> ()");
+  m.def("conv2d(Tensor x, Tensor? x2, Tensor w, Tensor(a!) out, Tensor? bias, Tensor? bias2d, Tensor? residual, Tensor? in_scale, Tensor? in_shift, int in_act, int kh, int kw, int stride, int pad, bool upsample, int act, float res_alpha) -> ()");
+  m.def("flash_attn(Tensor q, Tensor k, Tensor v, Tensor(a!) o, float scale, bool causal, int causal_offset, Tensor? kv_lens, Tensor? q_lens, Tensor? bias, Tensor? block_table) -> ()");
+  m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor(a!) o, Tensor block_table, Tensor ctx_lens, Tensor(b!) ws, int num_splits, float scale) -> ()");
+  m.def("kv_write(Tensor k, Tensor v, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slots) -> ()");
+  m.def("gated_act(Tensor x, Tensor(a!) out, int act, bool gate_first) -> ()");
+  m.def("bias_act(Tensor x, Tensor? bias, Tensor? residual, Tensor(a!) out, int act, float alpha) -> ()");
+  m.def("rope(Tensor(a!) x, Tensor positions, Tensor cos, Tensor sin, int rot_dim, bool neox) -> ()");
+  m.def("rope_pairs(Tensor(a!) x, Tensor cos, Tensor sin) -> ()");
+  m.def("sched_step(Tensor model_out, Tensor(a!) latents, bool cfg, float guidance, int pred_type, float a_t, float a_prev, float dt) -> ()");
+  m.def("softmax_(Tensor(a!) x, float scale) -> ()");
+  m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(shai, CUDA, m) {
+  m.impl("rmsnorm", &rmsnorm);
+  m.impl("layernorm", &layernorm);
+  m.impl("groupnorm_stats", &groupnorm_stats);
+  m.impl("groupnorm_apply", &groupnorm_apply);
+  m.impl("gemm", &gemm);
+  m.impl("conv2d", &conv2d);
+  m.impl("flash_attn", &flash_attn);
+  m.impl("decode_attn", &decode_attn);
+  m.impl("kv_write", &kv_write);
+  m.impl("gated_act", &gated_act);
+  m.impl("bias_act", &bias_act);
+  m.impl("rope", &rope);
+  m.impl("rope_pairs", &rope_pairs);
+  m.impl("sched_step", &sched_step);
+  m.impl("softmax_", &softmax_);
+  m.impl("embedding", &embedding);
+}

@@ -1,0 +1,147 @@
+#!/usr/bin/env python3
+"""Native build for the gfx950 kernels and the C++ runtime pieces.
+
+Generates a ninja file and builds, in-tree (so the .so files travel to the GPU
+box with the repo snapshot):
+
+  * ``<pkg>/_native/libshai_kernels.so`` -- HIP kernels (hipcc --offload-arch=gfx950)
+    plus the torch operator registrations (``torch.ops.shai.*``).
+  * ``<pkg>/_native/libshai_runtime.so`` -- host C++ runtime (paged-KV block
+    manager, batching scheduler helpers) exposed through a C ABI (ctypes).
+  * ``<pkg>/_native/libshai_comm.so`` -- xGMI peer-to-peer all-reduce (HIP IPC).
+
+Kernel translation units include no torch headers, so editing a kernel
+recompiles in seconds; only ``bindings.cpp`` pulls in ATen.
+
+Usage: python csrc/build.py [--clean] [-j N]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+PKG = os.path.join(ROOT, "scalable-hw-agnostic-inference_amd")
+OUT = os.path.join(PKG, "_native")
+BUILD = os.path.join(ROOT, "build", "native")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+KERNEL_SRCS = ["kernels/norm.hip", "kernels/gemm.hip", "kernels/attention.hip", "kernels/elementwise.hip",
+               "kernels/sampling.hip", "kernels/gemv.hip"]
+BINDING_SRCS = ["bindings.cpp"]
+RUNTIME_SRCS = ["runtime/block_manager.cpp", "runtime/scheduler.cpp"]
+COMM_SRCS = ["comm/p2p_allreduce.hip"]
+
+
+def torch_paths():
+    import torch  # noqa: F401  (only for include/lib dirs)
+    from torch.utils import cpp_extension as ce
+    inc = ce.include_paths(device_type="cuda") if "device_type" in ce.include_paths.__code__.co_varnames else ce.include_paths(True)
+    lib = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def write_ninja(path: str) -> dict:
+    inc, tlib, abi = torch_paths()
+    hipcc = os.path.join(ROCM, "bin", "hipcc")
+    kflags = f"--offload-arch={ARCH} -O3 -std=c++17 -fPIC -ffp-contract=fast -Wno-unused-result -I{CSRC}"
+    incs = " ".join(f"-isystem {p}" for p in inc)
+    bflags = (f"-O2 -std=c++17 -fPIC -D_GLIBCXX_USE_CXX11_ABI={abi} -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 "
+              f"-I{CSRC} {incs} -isystem {ROCM}/include -Wno-deprecated-declarations")
+    rflags = f"-O3 -std=c++17 -fPIC -Wall -I{CSRC}"
+    lines = [
+        "ninja_required_version = 1.3",
+        f"hipcc = {hipcc}",
+        f"kflags = {kflags}",
+        f"bflags = {bflags}",
+        f"rflags = {rflags}",
+        "rule hip",
+        "  command = $hipcc $kflags -c $in -o $out",
+        "  description = HIP $in",
+        "rule cxx",
+        "  command = c++ $bflags -c $in -o $out",
+        "  description = CXX $in",
+        "rule rcxx",
+        "  command = c++ $rflags -c $in -o $out",
+        "  description = CXX $in",
+        "rule link_kernels",
+        f"  command = $hipcc --offload-arch={ARCH} -shared -fPIC $in -o $out -L{tlib} -Wl,-rpath,{tlib} "
+        f"-lc10 -lc10_hip -ltorch_cpu -ltorch_hip -L{ROCM}/lib -lamdhip64",
+        "  description = LINK $out",
+        "rule link_hip",
+        f"  command = $hipcc --offload-arch={ARCH} -shared -fPIC $in -o $out -L{ROCM}/lib -lamdhip64",
+        "  description = LINK $out",
+        "rule link_cxx",
+        "  command = c++ -shared -fPIC $in -o $out -lpthread",
+        "  description = LINK $out",
+    ]
+    targets = {}
+
+    def objs(srcs, rule):
+        out = []
+        for s in srcs:
+            if not os.path.exists(os.path.join(CSRC, s)):
+                continue
+            o = os.path.join(BUILD, s.replace("/", "_") + ".o")
+            lines.append(f"build {o}: {rule} {os.path.join(CSRC, s)} | {os.path.join(CSRC, 'kernels', 'common.h')} "
+                         f"{os.path.join(CSRC, 'kernels', 'launchers.h')}")
+            out.append(o)
+        return out
+
+    k = objs(KERNEL_SRCS, "hip") + objs(BINDING_SRCS, "cxx")
+    targets["kernels"] = os.path.join(OUT, "libshai_kernels.so")
+    lines.append(f"build {targets['kernels']}: link_kernels {' '.join(k)}")
+    r = objs(RUNTIME_SRCS, "rcxx")
+    if r:
+        targets["runtime"] = os.path.join(OUT, "libshai_runtime.so")
+        lines.append(f"build {targets['runtime']}: link_cxx {' '.join(r)}")
+    c = objs(COMM_SRCS, "hip")
+    if c:
+        targets["comm"] = os.path.join(OUT, "libshai_comm.so")
+        lines.append(f"build {targets['comm']}: link_hip {' '.join(c)}")
+    lines.append("default " + " ".join(targets.values()))
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return targets
+
+
+def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -> dict:
+    if clean and os.path.isdir(BUILD):
+        shutil.rmtree(BUILD)
+    os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(OUT, exist_ok=True)
+    ninja_file = os.path.join(BUILD, "build.ninja")
+    targets = write_ninja(ninja_file)
+    ninja = shutil.which("ninja")
+    if ninja is None:
+        import ninja as _nj  # pip package ships the binary
+        ninja = os.path.join(_nj.BIN_DIR, "ninja")
+    cmd = [ninja, "-f", ninja_file]
+    if jobs:
+        cmd += ["-j", str(jobs)]
+    if verbose:
+        cmd.append("-v")
+    subprocess.run(cmd, check=True, cwd=BUILD)
+    return targets
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("-j", type=int, default=min(16, os.cpu_count() or 8))
+    ap.add_argument("-v", action="store_true")
+    a = ap.parse_args()
+    t = build(a.clean, a.j, a.v)
+    for k, v in t.items():
+        print(f"{k}: {v}")
+
+
+if __name__ == "__main__":
+    sys.exit(main())

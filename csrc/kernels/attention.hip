@@ -1,0 +1,396 @@
+// Attention kernels for gfx950.
+//
+// flash_attn_fwd: fused QK^T -> online softmax -> PV on MFMA (no S x S matrix
+//   in HBM; replaces the reference's attention slicing / NEURON_FUSE_SOFTMAX
+//   paths, app/run-sd.py:135, app/compile-sd2.py:2).  One workgroup = 4 waves
+//   = 128 query rows; each wave owns 32 queries.  Scores are computed swapped
+//   (S^T = K Q^T, v_mfma_f32_32x32x16_bf16) so every lane holds one query's
+//   scores: the row max / row sum are in-lane plus one cross-half shuffle.
+//   P stays in registers and feeds O^T = V^T P^T directly as the B operand
+//   (accumulator-as-operand); V^T fragments come from ds_read_b64_tr_b16
+//   transposed LDS reads of the row-major V tile.  K/V tiles (64 keys) are
+//   register-staged one tile ahead and double-buffered in XOR-swizzled LDS.
+//   Supports D in {64,128}, GQA, causal (with offset for chunked prefill),
+//   per-batch q/kv lengths (padding masks), additive bias (T5 relative
+//   position bias) and a paged K/V source (64-token blocks).
+//
+// decode_attn: one query token per sequence against the paged KV cache,
+//   split-K over 64-token blocks (memory-bound; VALU dot products, K/V
+//   staged through LDS), followed by a split combine.
+#include "common.h"
+#include "launchers.h"
+
+namespace shai {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+template <int D>
+__device__ __forceinline__ int k_swz(int row, int ch) {
+  if constexpr (D == 128) return row * 128 + ((ch ^ (row & 15)) << 3);
+  else return row * 64 + ((ch ^ ((row >> 1) & 7)) << 3);
+}
+template <int D>
+__device__ __forceinline__ int v_swz(int row, int ch) {
+  if constexpr (D == 128) return row * 128 + ((ch ^ ((row & 3) << 2)) << 3);
+  else return row * 64 + ((ch ^ (((row >> 1) & 1) << 2)) << 3);
+}
+
+template <int D>
+__global__ void __launch_bounds__(256, 2) flash_fwd_kernel(const AttnArgs p) {
+  constexpr int KT = 64;                 // keys per tile
+  constexpr int CPR = D / 8;             // 16-byte chunks per row
+  constexpr int NST = KT * CPR / 256;    // chunks per thread per operand
+  constexpr int NS = D / 16;             // k-steps for QK^T
+  constexpr int ND = D / 32;             // 32-wide d blocks of O
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  bf16_t* sK = smem;                     // [2][64*D]
+  bf16_t* sV = smem + 2 * KT * D;        // [2][64*D]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 31, fh = lane >> 5;
+  const int b = blockIdx.z, hq = blockIdx.y;
+  const int hk = hq / (p.Hq / p.Hkv);
+  const int q_len = p.q_lens ? p.q_lens[b] : p.Sq;
+  const int kv_len = p.kv_lens ? p.kv_lens[b] : p.Skv;
+  const int c_off = p.q_lens ? kv_len - q_len : p.causal_offset;
+  if ((int)blockIdx.x * 128 >= q_len) return;
+  const int q0 = blockIdx.x * 128;
+  const int qi = q0 + wid * 32 + fr;  // this lane's query
+
+  // ---- Q fragments (B operand of S^T = K Q^T): Q[qi][16 s + 8 fh .. +7]
+  bf16x8 qf[NS];
+  {
+    const bf16_t* qp = p.q + (long)b * p.q_bs + (long)min(qi, q_len - 1) * p.q_ts + (long)hq * D;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      uint4_ v = *reinterpret_cast<const uint4_*>(qp + 16 * s + 8 * fh);
+      if (qi >= q_len) v = uint4_{0u, 0u, 0u, 0u};
+      qf[s] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+
+  // ---- number of key tiles this block needs
+  int kv_end = kv_len;
+  if (p.causal) kv_end = min(kv_end, q0 + 127 + c_off + 1);
+  const int ntiles = kv_end > 0 ? (kv_end + KT - 1) / KT : 0;
+
+  const bf16_t* kbase = p.k + (long)b * p.k_bs + (long)hk * D;
+  const bf16_t* vbase = p.v + (long)b * p.v_bs + (long)hk * D;
+
+  uint4_ rk[NST], rv[NST];
+  auto load_tile = [&](int t) {
+    const int key0 = t * KT;
+    const bf16_t* kb = kbase;
+    const bf16_t* vb = vbase;
+    long ts_k = p.k_ts, ts_v = p.v_ts;
+    int kbase_row = key0;
+    if (p.block_table) {
+      const int phys = p.block_table[(long)b * p.max_blocks + t];
+      kb = p.k + (long)phys * p.kc_bs + (long)hk * p.kc_hs;
+      vb = p.v + (long)phys * p.kc_bs + (long)hk * p.kc_hs;
+      ts_k = ts_v = D;
+      kbase_row = 0;
+    }
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int id = tid + 256 * i;
+      const int row = id / CPR, ch = id % CPR;
+      const bool ok = key0 + row < kv_len;
+      rk[i] = ok ? *reinterpret_cast<const uint4_*>(kb + (long)(kbase_row + row) * ts_k + ch * 8) : uint4_{0u, 0u, 0u, 0u};
+      rv[i] = ok ? *reinterpret_cast<const uint4_*>(vb + (long)(kbase_row + row) * ts_v + ch * 8) : uint4_{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store_tile = [&](int stage) {
+    bf16_t* ks = sK + stage * KT * D;
+    bf16_t* vs = sV + stage * KT * D;
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int id = tid + 256 * i;
+      const int row = id / CPR, ch = id % CPR;
+      *reinterpret_cast<uint4_*>(ks + k_swz<D>(row, ch)) = rk[i];
+      *reinterpret_cast<uint4_*>(vs + v_swz<D>(row, ch)) = rv[i];
+    }
+  };
+
+  float16_ o[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+  const float sl2 = p.scale * kLog2e;
+  const bf16_t* bias_row = p.bias ? p.bias + ((long)hq * p.Sq + min(qi, q_len - 1)) * p.Skv : nullptr;
+
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+
+  // lane roles for the transposed V reads
+  const int g16 = lane >> 4, i16 = lane & 15;
+  const int tq = i16 >> 2, tp = i16 & 3;
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < ntiles) load_tile(t + 1);
+    const bf16_t* ks = sK + cur * KT * D;
+    const bf16_t* vs = sV + cur * KT * D;
+
+    // ---- S^T = K Q^T for two 32-key blocks
+    float16_ sacc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[kb][r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + k_swz<D>(kb * 32 + fr, 2 * s + fh));
+        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kb], 0, 0, 0);
+      }
+    }
+    // ---- scale, bias, mask (log2 domain)
+    const int key0 = t * KT;
+    const bool need_mask = (key0 + KT > kv_len) || (p.causal && key0 + KT - 1 > q0 + c_off);
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        float sv = sacc[kb][r] * sl2;
+        if (bias_row) sv += (key < p.Skv ? bf2f(bias_row[key]) : 0.f) * kLog2e;
+        if (need_mask) {
+          const bool bad = key >= kv_len || (p.causal && key > qi + c_off);
+          sv = bad ? -INFINITY : sv;
+        }
+        sacc[kb][r] = sv;
+        mloc = fmaxf(mloc, sv);
+      }
+    }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float m_new = fmaxf(m_run, mloc);
+    const float m_use = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = exp2f(m_run - m_use);
+    m_run = m_new;
+    float lsum = 0.f;
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = exp2f(sacc[kb][r] - m_use);
+        sacc[kb][r] = e;
+        lsum += e;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (__bf16)sacc[kb][8 * s + j];
+        pf[kb][s] = v;
+      }
+    }
+    l_run = l_run * alpha + lsum;
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+
+    // ---- O^T += V^T P^T
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int r0 = kb * 32 + 16 * s + 4 * fh + tq;
+          const int col = d * 32 + 16 * (g16 & 1) + 4 * tp;
+          const int ch = col >> 3, half = (col >> 2) & 1;
+          const bf16_t* a0 = vs + v_swz<D>(r0, ch) + 4 * half;
+          const bf16_t* a1 = vs + v_swz<D>(r0 + 8, ch) + 4 * half;
+          const s4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(a0));
+          const s4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(a1));
+          short8 vv;
+          vv[0] = t0[0]; vv[1] = t0[1]; vv[2] = t0[2]; vv[3] = t0[3];
+          vv[4] = t1[0]; vv[5] = t1[1]; vv[6] = t1[2]; vv[7] = t1[3];
+          o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vv), pf[kb][s], o[d], 0, 0, 0);
+        }
+      }
+    }
+    if (t + 1 < ntiles) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (qi < q_len) {
+    bf16_t* op = p.o + (long)b * p.o_bs + (long)qi * p.o_ts + (long)hq * D;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int dd = d * 32 + 8 * g + 4 * fh;
+        uint2_ w;
+        w[0] = pack2(o[d][4 * g] * inv, o[d][4 * g + 1] * inv);
+        w[1] = pack2(o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv);
+        *reinterpret_cast<uint2_*>(op + dd) = w;
+      }
+    }
+  }
+}
+
+void launch_flash_attn(const AttnArgs& a, hipStream_t s) {
+  dim3 grid((a.Sq + 127) / 128, a.Hq, a.B);
+  const size_t lds = (size_t)4 * 64 * a.D * sizeof(bf16_t);
+  if (a.D == 128) flash_fwd_kernel<128><<<grid, 256, lds, s>>>(a);
+  else flash_fwd_kernel<64><<<grid, 256, lds, s>>>(a);
+}
+
+// ----------------------------------------------------------------------------
+// Paged decode attention (one query token per sequence).
+// grid (B, Hkv, splits); block = G waves (G = Hq/Hkv <= 8), wave w = head hk*G+w.
+// ----------------------------------------------------------------------------
+template <int D>
+__global__ void decode_attn_kernel(const DecodeAttnArgs p) {
+  constexpr int CPR = D / 8;
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  bf16_t* sK = reinterpret_cast<bf16_t*>(dsm);           // [64][D] swizzled
+  bf16_t* sV = sK + 64 * D;                              // [64][D] linear
+  float* sQ = reinterpret_cast<float*>(sV + 64 * D);     // [G][D]
+  float* sP = sQ + 8 * D;                                // [G][64]
+  const int G = p.Hq / p.Hkv;
+  const int nthr = G * 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x, hk = blockIdx.y, split = blockIdx.z;
+  const int hq = hk * G + w;
+  const int ctx = p.ctx_lens[b];
+  const int nblk = (ctx + 63) / 64;
+  const int per = (nblk + p.num_splits - 1) / p.num_splits;
+  const int blk0 = split * per, blk1 = min(nblk, blk0 + per);
+
+  for (int i = lane; i < D; i += 64) sQ[w * D + i] = bf2f(p.q[(long)b * p.q_bs + (long)hq * D + i]) * p.scale * kLog2e;
+  float m_run = -INFINITY, l_run = 0.f;
+  float o0 = 0.f, o1 = 0.f;  // this lane's d = lane, lane + 64 (D=128) or d = lane (D=64)
+  __syncthreads();
+  for (int bi = blk0; bi < blk1; ++bi) {
+    const int phys = p.block_table[(long)b * p.max_blocks + bi];
+    const bf16_t* kc = p.k_cache + ((long)phys * p.Hkv + hk) * 64 * D;
+    const bf16_t* vc = p.v_cache + ((long)phys * p.Hkv + hk) * 64 * D;
+    for (int id = tid; id < 64 * CPR; id += nthr) {
+      const int row = id / CPR, ch = id % CPR;
+      const uint4_ kv = *reinterpret_cast<const uint4_*>(kc + row * D + ch * 8);
+      const uint4_ vv = *reinterpret_cast<const uint4_*>(vc + row * D + ch * 8);
+      *reinterpret_cast<uint4_*>(sK + row * D + ((ch ^ (row & (CPR - 1))) << 3)) = kv;
+      *reinterpret_cast<uint4_*>(sV + row * D + ch * 8) = vv;
+    }
+    __syncthreads();
+    // lane = key
+    const int key = bi * 64 + lane;
+    float sc = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < CPR; ++ch) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4_*>(sK + lane * D + ((ch ^ (lane & (CPR - 1))) << 3)), f);
+      const float4_ qa = *reinterpret_cast<const float4_*>(sQ + w * D + ch * 8);
+      const float4_ qb = *reinterpret_cast<const float4_*>(sQ + w * D + ch * 8 + 4);
+      sc += f[0] * qa[0] + f[1] * qa[1] + f[2] * qa[2] + f[3] * qa[3] + f[4] * qb[0] + f[5] * qb[1] + f[6] * qb[2] +
+            f[7] * qb[3];
+    }
+    if (key >= ctx) sc = -INFINITY;
+    const float mt = wave_max(sc);
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = exp2f(m_run - m_new);
+    const float e = key < ctx ? exp2f(sc - m_new) : 0.f;
+    l_run = l_run * alpha + wave_sum(e);
+    m_run = m_new;
+    sP[w * 64 + lane] = e;
+    o0 *= alpha;
+    o1 *= alpha;
+    __syncthreads();  // sP visible (same wave, but keeps K/V reuse simple)
+    for (int k = 0; k < 64; ++k) {
+      const float pk = sP[w * 64 + k];
+      o0 += pk * bf2f(sV[k * D + lane]);
+      if (D == 128) o1 += pk * bf2f(sV[k * D + 64 + lane]);
+    }
+    __syncthreads();
+  }
+  // partial results: ws[b][hq][split] = {m, l, o[D]}
+  float* dst = p.ws + (((long)b * p.Hq + hq) * p.num_splits + split) * (D + 2);
+  if (lane == 0) {
+    dst[0] = m_run;
+    dst[1] = l_run;
+  }
+  dst[2 + lane] = o0;
+  if (D == 128) dst[2 + 64 + lane] = o1;
+}
+
+__global__ void decode_combine_kernel(const DecodeAttnArgs p) {
+  const int b = blockIdx.x, hq = blockIdx.y;
+  const int D = p.D;
+  const float* src = p.ws + ((long)b * p.Hq + hq) * p.num_splits * (D + 2);
+  float m = -INFINITY;
+  for (int s = 0; s < p.num_splits; ++s) m = fmaxf(m, src[s * (D + 2)]);
+  float l = 0.f;
+  for (int s = 0; s < p.num_splits; ++s) {
+    const float ms = src[s * (D + 2)];
+    if (ms != -INFINITY) l += src[s * (D + 2) + 1] * exp2f(ms - m);
+  }
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float acc = 0.f;
+    for (int s = 0; s < p.num_splits; ++s) {
+      const float ms = src[s * (D + 2)];
+      if (ms != -INFINITY) acc += src[s * (D + 2) + 2 + d] * exp2f(ms - m);
+    }
+    p.o[(long)b * p.o_bs + (long)hq * D + d] = f2bf(acc * inv);
+  }
+}
+
+size_t decode_attn_workspace(int B, int Hq, int D, int num_splits) {
+  return (size_t)B * Hq * num_splits * (D + 2) * sizeof(float);
+}
+
+void launch_decode_attn(const DecodeAttnArgs& a, hipStream_t s) {
+  const int G = a.Hq / a.Hkv;
+  dim3 grid(a.B, a.Hkv, a.num_splits);
+  const size_t lds = (size_t)2 * 64 * a.D * sizeof(bf16_t) + (size_t)8 * a.D * 4 + 8 * 64 * 4;
+  if (a.D == 128) decode_attn_kernel<128><<<grid, G * 64, lds, s>>>(a);
+  else decode_attn_kernel<64><<<grid, G * 64, lds, s>>>(a);
+  decode_combine_kernel<<<dim3(a.B, a.Hq), 128, 0, s>>>(a);
+}
+
+// ----------------------------------------------------------------------------
+// KV cache write: cache layout [num_blocks, Hkv, 64, D]; slot = block*64 + off
+// ----------------------------------------------------------------------------
+__global__ void kv_write_kernel(const bf16_t* __restrict__ k, const bf16_t* __restrict__ v, bf16_t* __restrict__ kc,
+                                bf16_t* __restrict__ vc, const int* __restrict__ slots, int T, int Hkv, int D,
+                                long k_ts, long v_ts) {
+  const int CPR = D / 8;
+  const long total = (long)T * Hkv * CPR;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % CPR);
+    const int h = (int)((i / CPR) % Hkv);
+    const int t = (int)(i / ((long)CPR * Hkv));
+    const int slot = slots[t];
+    if (slot < 0) continue;
+    const long dst = (((long)(slot >> 6) * Hkv + h) * 64 + (slot & 63)) * D + ch * 8;
+    *reinterpret_cast<uint4_*>(kc + dst) = *reinterpret_cast<const uint4_*>(k + (long)t * k_ts + (long)h * D + ch * 8);
+    *reinterpret_cast<uint4_*>(vc + dst) = *reinterpret_cast<const uint4_*>(v + (long)t * v_ts + (long)h * D + ch * 8);
+  }
+}
+
+void launch_kv_write(const bf16_t* k, const bf16_t* v, bf16_t* k_cache, bf16_t* v_cache, const int* slot_mapping, int T,
+                     int Hkv, int D, long k_ts, long v_ts, hipStream_t s) {
+  const long total = (long)T * Hkv * (D / 8);
+  long blocks = (total + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  kv_write_kernel<<<(int)blocks, 256, 0, s>>>(k, v, k_cache, v_cache, slot_mapping, T, Hkv, D, k_ts, v_ts);
+}
+
+}  // namespace shai

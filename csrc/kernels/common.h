@@ -1,0 +1,103 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels.
+//
+// Conventions used by every kernel in csrc/kernels:
+//   * bf16 tensors travel as raw `uint16_t` bit patterns; math is fp32.
+//   * wave = 64 lanes (hard-coded, never warpSize-32 idioms).
+//   * global loads of bf16 are 16-byte vectors (8 elements) wherever the
+//     shape allows (MI355X guide, Guideline 13).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace shai {
+
+constexpr int kWave = 64;
+
+typedef uint16_t bf16_t;
+typedef short short8 __attribute__((ext_vector_type(8)));
+typedef short short4 __attribute__((ext_vector_type(4)));
+typedef float float4_ __attribute__((ext_vector_type(4)));
+typedef float float16_ __attribute__((ext_vector_type(16)));
+typedef uint32_t uint4_ __attribute__((ext_vector_type(4)));
+typedef uint32_t uint2_ __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float bf2f(uint32_t x) { return __uint_as_float(x << 16); }
+
+// Round-to-nearest-even fp32 -> bf16 (plain cast lowers to v_cvt_pk_bf16_f32
+// on gfx950 and keeps NaNs NaN).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// Unpack 8 bf16 held in a uint4 into fp32.
+__device__ __forceinline__ void unpack8(const uint4_ v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(v[i] << 16);
+    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint4_ pack8(const float* f) {
+  uint4_ v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = pack2(f[2 * i], f[2 * i + 1]);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+
+__device__ __forceinline__ float gelu_erf_f(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+__device__ __forceinline__ float gelu_tanh_f(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.0f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+__device__ __forceinline__ float quick_gelu_f(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+
+enum Act : int { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_GELU_TANH = 3, ACT_QUICK_GELU = 4, ACT_RELU = 5 };
+
+template <int ACT>
+__device__ __forceinline__ float apply_act(float x) {
+  if constexpr (ACT == ACT_SILU) return silu_f(x);
+  else if constexpr (ACT == ACT_GELU) return gelu_erf_f(x);
+  else if constexpr (ACT == ACT_GELU_TANH) return gelu_tanh_f(x);
+  else if constexpr (ACT == ACT_QUICK_GELU) return quick_gelu_f(x);
+  else if constexpr (ACT == ACT_RELU) return fmaxf(x, 0.f);
+  else return x;
+}
+
+__device__ __forceinline__ float apply_act_rt(int act, float x) {
+  switch (act) {
+    case ACT_SILU: return silu_f(x);
+    case ACT_GELU: return gelu_erf_f(x);
+    case ACT_GELU_TANH: return gelu_tanh_f(x);
+    case ACT_QUICK_GELU: return quick_gelu_f(x);
+    case ACT_RELU: return fmaxf(x, 0.f);
+    default: return x;
+  }
+}
+
+}  // namespace shai
+
+#define SHAI_CHECK_LAUNCH() (void)hipGetLastError()

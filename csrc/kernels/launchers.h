@@ -1,0 +1,142 @@
+// Host-side launcher interface of the HIP kernels.  Kernel translation units
+// include only this header and <hip/hip_runtime.h> (no torch headers), which
+// keeps their hipcc compile fast; csrc/bindings.cpp adapts torch tensors.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace shai {
+typedef uint16_t bf16_t;
+
+// ---------------------------------------------------------------- norms
+struct RowNormArgs {
+  const bf16_t* x;
+  const bf16_t* residual;   // optional: x + residual is normalised
+  const bf16_t* w;          // optional weight [D]
+  const bf16_t* b;          // optional bias [D] (LayerNorm only)
+  bf16_t* out;
+  bf16_t* residual_out;     // optional: receives x + residual
+  int rows, D;
+  long x_stride, out_stride;  // row strides in elements
+  float eps;
+  float w_offset;           // y = norm(x) * (w + w_offset) + b
+};
+void launch_rmsnorm(const RowNormArgs& a, hipStream_t s);
+void launch_layernorm(const RowNormArgs& a, hipStream_t s);
+
+struct GroupNormArgs {
+  const bf16_t* x;   // [N, HW, C] channels-last
+  const bf16_t* gamma;
+  const bf16_t* beta;
+  float* partials;   // [N, 256, G, 2] workspace
+  float* scale;      // [N, C]
+  float* shift;      // [N, C]
+  bf16_t* out;       // apply output (optional)
+  int N, HW, C, G;
+  float eps;
+  int silu;
+};
+int gn_num_blocks(int HW);
+void launch_groupnorm_stats(const GroupNormArgs& a, hipStream_t s);
+void launch_groupnorm_apply(const GroupNormArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- elementwise
+// out[t, i] = act(x[t, i]) * x[t, F + i]   (gated MLP, unfused fallback), F = D/2
+void launch_gated_act(const bf16_t* x, bf16_t* out, long rows, int F, long x_stride, int act, int gate_first,
+                      hipStream_t s);
+// out = act(x * alpha + bias) (+ residual)  over [rows, D]
+void launch_bias_act(const bf16_t* x, const bf16_t* bias, const bf16_t* residual, bf16_t* out, long rows, int D,
+                     int act, float alpha, hipStream_t s);
+// Rotary embedding in-place on q/k heads: x [T, H, Dh] (token stride given),
+// cos/sin tables [max_pos, rot_dim/2] fp32, positions [T] int32.
+void launch_rope(bf16_t* x, const int* positions, const float* cos, const float* sin, int T, int H, int Dh,
+                 int rot_dim, long tok_stride, int neox, hipStream_t s);
+// Flux 3-axis rope with precomputed per-token (cos, sin) pairs [T, Dh/2].
+void launch_rope_pairs(bf16_t* x, const float* cos, const float* sin, int B, int T, int H, int Dh, long batch_stride,
+                       long tok_stride, hipStream_t s);
+// Scheduler step fused with classifier-free guidance (all fp32 math):
+//   eps = eu + g * (ec - eu)  (model_out holds [uncond; cond] halves when cfg)
+//   DDIM (eta=0):  x0 = (x - sqrt(1-a) eps)/sqrt(a) ; x' = sqrt(ap) x0 + sqrt(1-ap) eps
+//   v-prediction variants handled by pred_type (0 eps, 1 v, 2 flow (x' = x + dt * v))
+void launch_sched_step(const bf16_t* model_out, bf16_t* latents, long n, int cfg, float guidance, int pred_type,
+                       float a_t, float a_prev, float dt, hipStream_t s);
+// Row softmax in-place (fp32 math), bf16 rows of length D
+void launch_softmax(bf16_t* x, long rows, int D, float scale, hipStream_t s);
+// Embedding gather: out[t] = table[ids[t]]
+void launch_embedding(const int* ids, const bf16_t* table, bf16_t* out, long T, int D, hipStream_t s);
+
+// ---------------------------------------------------------------- GEMM / conv
+struct GemmArgs {
+  // C[b, m, n] = act(alpha * sum_k A[b, m, k] * W[b, n, k] + bias[n] + bias2d[m/rows_per_bias2d, n]) + residual[b, m, n]
+  const bf16_t* A;
+  const bf16_t* W;
+  bf16_t* C;
+  const bf16_t* bias;      // [N] optional
+  const bf16_t* bias2d;    // [M / rows_per_bias2d, N] optional (e.g. time-embedding per image)
+  const bf16_t* residual;  // [M, N] optional (same layout as C)
+  int M, N, K;
+  long lda, ldw, ldc, ldr;  // row strides (elements)
+  long batch_a, batch_w, batch_c, batch_r;  // batch strides (elements)
+  int batch;
+  int rows_per_bias2d;
+  float alpha;
+  float res_alpha;          // C = epi + res_alpha * residual
+  int act;                  // Act enum
+  int glu;                  // 1: gated output, weights interleaved (a,g) pairs -> C has N/2 cols: act(g) * a
+  // implicit-GEMM convolution (A is an NHWC activation, K = KH*KW*Cin)
+  int conv;                 // 0 = plain GEMM
+  int Nimg, H, Wd, Cin, OH, OW, KH, KW, stride, pad, upsample;  // upsample: nearest-2x fused into gather
+  const bf16_t* A2;         // optional second source: channels [Cin1, Cin) come from A2 (fused concat)
+  int Cin1;
+  // fused GroupNorm apply on the gathered A operand: a = act(x * scale[n,c] + shift[n,c])
+  const float* in_scale;
+  const float* in_shift;
+  int in_act;
+};
+void launch_gemm(const GemmArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- attention
+struct AttnArgs {
+  const bf16_t* q;  // [B, Sq, Hq, D] with strides
+  const bf16_t* k;  // [B, Skv, Hkv, D]
+  const bf16_t* v;
+  bf16_t* o;        // [B, Sq, Hq, D] with strides
+  int B, Sq, Skv, Hq, Hkv, D;
+  long q_bs, q_ts, k_bs, k_ts, v_bs, v_ts, o_bs, o_ts;  // batch / token strides (elements); head stride = D
+  float scale;
+  int causal;
+  int causal_offset;        // query i sees keys <= i + causal_offset
+  const int* kv_lens;       // optional [B] valid key count per batch
+  const int* q_lens;        // optional [B] valid query count; causal offset becomes kv_len - q_len
+  const bf16_t* bias;       // optional additive bias [Hq, Sq, Skv] (bf16), broadcast over batch
+  // paged K/V (LLM prefill over cached context): block tables of 64-token blocks
+  const int* block_table;   // optional [B, max_blocks]
+  int max_blocks;
+  long kc_bs, kc_hs;        // cache strides: block stride, head stride (elements); token stride = D
+};
+void launch_flash_attn(const AttnArgs& a, hipStream_t s);
+
+struct DecodeAttnArgs {
+  const bf16_t* q;          // [B, Hq, D]
+  const bf16_t* k_cache;    // [num_blocks, Hkv, 64, D]
+  const bf16_t* v_cache;
+  bf16_t* o;                // [B, Hq, D]
+  const int* block_table;   // [B, max_blocks]
+  const int* ctx_lens;      // [B]
+  float* ws;                // split-K workspace
+  int B, Hq, Hkv, D, max_blocks, num_splits;
+  long q_bs, o_bs;
+  float scale;
+};
+void launch_decode_attn(const DecodeAttnArgs& a, hipStream_t s);
+size_t decode_attn_workspace(int B, int Hq, int D, int num_splits);
+
+// Write new K/V tokens into the paged cache.
+void launch_kv_write(const bf16_t* k, const bf16_t* v, bf16_t* k_cache, bf16_t* v_cache, const int* slot_mapping,
+                     int T, int Hkv, int D, long k_ts, long v_ts, hipStream_t s);
+
+// ---------------------------------------------------------------- sampling
+// Per-row temperature / top-k / top-p sampling from fp32 or bf16 logits.
+void launch_sample(const float* logits, int rows, int V, const float* temperature, const int* top_k,
+                   const float* top_p, const float* uniform, int* out, float* ws, hipStream_t s);
+}  // namespace shai

@@ -1,0 +1,286 @@
+// Normalisation kernels for gfx950: RMSNorm, LayerNorm (both with optional
+// fused residual add) and channels-last GroupNorm (stats / finalize / apply).
+//
+// Row norms: one 64-lane wave owns one row, the row is held in registers as
+// packed bf16 (16-byte vectors), so x is read once from HBM and written once.
+// GroupNorm is split into a partial-statistics pass and a tiny finalize pass
+// that emits per-(sample, channel) fp32 scale/shift.  The apply step is
+// usually NOT a separate kernel: the implicit-GEMM conv kernel (conv.hip)
+// applies scale/shift (+SiLU) while it gathers its A tile, so the normalised
+// activation is never materialised (replaces the diffusers GroupNorm+SiLU
+// pair the reference runs eagerly / via Inductor, app/run-sd.py:107-134).
+#include "common.h"
+#include "launchers.h"
+
+namespace shai {
+
+// ----------------------------------------------------------------------------
+// RMSNorm / LayerNorm, one wave per row.
+// ----------------------------------------------------------------------------
+template <int MAXC, bool LAYERNORM>
+__global__ void __launch_bounds__(256) row_norm_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ residual, const bf16_t* __restrict__ w,
+    const bf16_t* __restrict__ b, bf16_t* __restrict__ out, bf16_t* __restrict__ residual_out, int rows,
+    int D, long x_stride, long out_stride, float eps, float w_offset) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const bf16_t* xr = x + (long)row * x_stride;
+  uint4_ v[MAXC];
+  float sum = 0.f, sumsq = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < D) {
+      v[c] = *reinterpret_cast<const uint4_*>(xr + col);
+      if (residual) {
+        const uint4_ r = *reinterpret_cast<const uint4_*>(residual + (long)row * D + col);
+        float f[8], g[8];
+        unpack8(v[c], f);
+        unpack8(r, g);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) f[i] += g[i];
+        v[c] = pack8(f);
+        if (residual_out) *reinterpret_cast<uint4_*>(residual_out + (long)row * D + col) = v[c];
+      }
+      float f[8];
+      unpack8(v[c], f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        sum += f[i];
+        sumsq += f[i] * f[i];
+      }
+    }
+  }
+  float mean = 0.f, rstd;
+  if (LAYERNORM) {
+    mean = wave_sum(sum) / D;
+    float var = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      if (col < D) {
+        float f[8];
+        unpack8(v[c], f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float d = f[i] - mean;
+          var += d * d;
+        }
+      }
+    }
+    rstd = rsqrtf(wave_sum(var) / D + eps);
+  } else {
+    rstd = rsqrtf(wave_sum(sumsq) / D + eps);
+  }
+  bf16_t* orow = out + (long)row * out_stride;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < D) {
+      float f[8], wf[8], bf[8];
+      unpack8(v[c], f);
+      if (w) unpack8(*reinterpret_cast<const uint4_*>(w + col), wf);
+      else
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wf[i] = 1.f;
+      if (LAYERNORM && b) unpack8(*reinterpret_cast<const uint4_*>(b + col), bf);
+      else
+#pragma unroll
+        for (int i = 0; i < 8; ++i) bf[i] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = (f[i] - mean) * rstd * (wf[i] + w_offset) + bf[i];
+      *reinterpret_cast<uint4_*>(orow + col) = pack8(f);
+    }
+  }
+}
+
+template <bool LN>
+static void launch_row_norm(const RowNormArgs& a, hipStream_t s) {
+  dim3 grid((a.rows + 3) / 4), block(256);
+  const int chunks = (a.D + 511) / 512;
+#define SHAI_RN(C)                                                                                       \
+  row_norm_kernel<C, LN><<<grid, block, 0, s>>>(a.x, a.residual, a.w, a.b, a.out, a.residual_out, a.rows, \
+                                                a.D, a.x_stride, a.out_stride, a.eps, a.w_offset)
+  if (chunks <= 1) SHAI_RN(1);
+  else if (chunks <= 2) SHAI_RN(2);
+  else if (chunks <= 4) SHAI_RN(4);
+  else if (chunks <= 8) SHAI_RN(8);
+  else SHAI_RN(16);
+#undef SHAI_RN
+}
+
+void launch_rmsnorm(const RowNormArgs& a, hipStream_t s) { launch_row_norm<false>(a, s); }
+void launch_layernorm(const RowNormArgs& a, hipStream_t s) { launch_row_norm<true>(a, s); }
+
+// ----------------------------------------------------------------------------
+// GroupNorm over channels-last [N, HW, C] (C % 8 == 0, C <= 4096).
+// Pass 1: grid (N, NB); each block reduces a contiguous pixel range into
+//         per-group (sum, sumsq) partials  -> part[N][NB][G][2].
+// Pass 2: grid (N); reduce partials, emit scale/shift [N][C] (fp32) such that
+//         y = x * scale + shift  ==  (x - mean) * rstd * gamma + beta.
+// Pass 3 (optional): apply (+ SiLU) elementwise.
+// ----------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict__ x, float* __restrict__ part,
+                                                       int HW, int C, int G, int NB, int ppb) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [P][C] sums then [P][C] sumsq
+  const int n = blockIdx.y, blk = blockIdx.x;
+  const int C8 = C >> 3;
+  const int t = threadIdx.x;
+  const int P = C8 <= 256 ? 256 / C8 : 1;
+  const int p0 = blk * ppb;
+  const int p1 = min(HW, p0 + ppb);
+  const bf16_t* xn = x + (long)n * HW * C;
+  // each thread: pixel lane pl, channel vectors cv0 (and cv0+256 when C8>256)
+  const int pl = C8 <= 256 ? t / C8 : 0;
+  const int cv0 = C8 <= 256 ? t % C8 : t;
+  const bool active = C8 <= 256 ? (t < P * C8) : (t < C8);
+  const bool second = C8 > 256 && (t + 256) < C8;
+  float s0[8], q0[8], s1[8], q1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s0[i] = q0[i] = s1[i] = q1[i] = 0.f;
+  if (active) {
+    for (int p = p0 + pl; p < p1; p += P) {
+      const bf16_t* xp = xn + (long)p * C;
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4_*>(xp + cv0 * 8), f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        s0[i] += f[i];
+        q0[i] += f[i] * f[i];
+      }
+      if (second) {
+        unpack8(*reinterpret_cast<const uint4_*>(xp + (cv0 + 256) * 8), f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          s1[i] += f[i];
+          q1[i] += f[i] * f[i];
+        }
+      }
+    }
+  }
+  float* ls = lds;
+  float* lq = lds + P * C;
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      ls[pl * C + cv0 * 8 + i] = s0[i];
+      lq[pl * C + cv0 * 8 + i] = q0[i];
+    }
+    if (second) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        ls[(cv0 + 256) * 8 + i] = s1[i];
+        lq[(cv0 + 256) * 8 + i] = q1[i];
+      }
+    }
+  }
+  __syncthreads();
+  // reduce over pixel lanes into row 0
+  for (int c = t; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int p = 0; p < P; ++p) {
+      a += ls[p * C + c];
+      b += lq[p * C + c];
+    }
+    ls[c] = a;
+    lq[c] = b;
+  }
+  __syncthreads();
+  const int Cg = C / G;
+  for (int g = t; g < G; g += 256) {
+    float a = 0.f, b = 0.f;
+    for (int c = 0; c < Cg; ++c) {
+      a += ls[g * Cg + c];
+      b += lq[g * Cg + c];
+    }
+    float* o = part + (((long)n * NB + blk) * G + g) * 2;
+    o[0] = a;
+    o[1] = b;
+  }
+}
+
+__global__ void __launch_bounds__(256) gn_finalize_kernel(const float* __restrict__ part, const bf16_t* __restrict__ gamma,
+                                                          const bf16_t* __restrict__ beta, float* __restrict__ scale,
+                                                          float* __restrict__ shift, int HW, int C, int G, int NB,
+                                                          float eps) {
+  __shared__ float mean_s[128], rstd_s[128];
+  const int n = blockIdx.x;
+  const int Cg = C / G;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < NB; ++k) {
+      const float* p = part + (((long)n * NB + k) * G + g) * 2;
+      a += p[0];
+      b += p[1];
+    }
+    const double cnt = (double)HW * Cg;
+    const double mean = a / cnt;
+    double var = b / cnt - mean * mean;
+    if (var < 0) var = 0;
+    mean_s[g] = (float)mean;
+    rstd_s[g] = (float)(1.0 / sqrt(var + (double)eps));
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int g = c / Cg;
+    const float ga = gamma ? bf2f(gamma[c]) : 1.f;
+    const float be = beta ? bf2f(beta[c]) : 0.f;
+    const float sc = rstd_s[g] * ga;
+    scale[(long)n * C + c] = sc;
+    shift[(long)n * C + c] = be - mean_s[g] * sc;
+  }
+}
+
+__global__ void __launch_bounds__(256) gn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, bf16_t* __restrict__ out,
+                                                       long total8, int HW, int C, int silu) {
+  const int C8 = C >> 3;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total8; i += (long)gridDim.x * blockDim.x) {
+    const long pix = i / C8;
+    const int cv = (int)(i - pix * C8);
+    const int n = (int)(pix / HW);
+    float f[8];
+    unpack8(reinterpret_cast<const uint4_*>(x)[i], f);
+    const float* sc = scale + (long)n * C + cv * 8;
+    const float* sh = shift + (long)n * C + cv * 8;
+    const float4_ a0 = *reinterpret_cast<const float4_*>(sc), a1 = *reinterpret_cast<const float4_*>(sc + 4);
+    const float4_ b0 = *reinterpret_cast<const float4_*>(sh), b1 = *reinterpret_cast<const float4_*>(sh + 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[k] = f[k] * a0[k] + b0[k];
+      f[k + 4] = f[k + 4] * a1[k] + b1[k];
+    }
+    if (silu)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = silu_f(f[k]);
+    reinterpret_cast<uint4_*>(out)[i] = pack8(f);
+  }
+}
+
+int gn_num_blocks(int HW) {
+  // ~512 pixels per block, at most 256 partial slots per sample
+  int nb = (HW + 511) / 512;
+  if (nb > 256) nb = 256;
+  if (nb < 1) nb = 1;
+  return nb;
+}
+
+void launch_groupnorm_stats(const GroupNormArgs& a, hipStream_t s) {
+  const int NB = gn_num_blocks(a.HW);
+  const int ppb = (a.HW + NB - 1) / NB;
+  const int C8 = a.C / 8;
+  const int P = C8 <= 256 ? 256 / C8 : 1;
+  const size_t lds = (size_t)2 * P * a.C * sizeof(float);
+  gn_stats_kernel<<<dim3(NB, a.N), 256, lds, s>>>(a.x, a.partials, a.HW, a.C, a.G, NB, ppb);
+  gn_finalize_kernel<<<a.N, 256, 0, s>>>(a.partials, a.gamma, a.beta, a.scale, a.shift, a.HW, a.C, a.G, NB, a.eps);
+}
+
+void launch_groupnorm_apply(const GroupNormArgs& a, hipStream_t s) {
+  const long total8 = (long)a.N * a.HW * a.C / 8;
+  long blocks = (total8 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  gn_apply_kernel<<<(int)blocks, 256, 0, s>>>(a.x, a.scale, a.shift, a.out, total8, a.HW, a.C, a.silu);
+}
+
+}  // namespace shai

@@ -1,0 +1,278 @@
+"""Operator layer: thin wrappers over the gfx950 HIP kernels (``torch.ops.shai``).
+
+GPU tensors always go to the native kernels (raising if the library is not
+built -- no silent eager fallback).  CPU tensors use the fp32 references in
+:mod:`shai_amd.ops.reference` (tests / CPU plumbing config).
+
+All wrappers allocate their outputs with torch (graph-pool aware), launch on
+the current stream and never synchronise, so whole model steps can be
+captured into HIP graphs (``torch.cuda.CUDAGraph`` is hipGraph on ROCm).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+
+from .. import native
+from . import reference as ref
+from .reference import (ACT_GELU, ACT_GELU_TANH, ACT_NONE, ACT_QUICK_GELU, ACT_RELU, ACT_SILU, act_id,
+                        pack_conv_weight, unpack_conv_weight)
+
+__all__ = [
+    "rmsnorm", "layernorm", "groupnorm_stats", "groupnorm_apply", "groupnorm", "linear", "conv2d", "attention",
+    "paged_attention", "decode_attention", "kv_write", "rope", "rope_pairs", "gated_act", "bias_act", "sched_step",
+    "softmax_", "embedding", "pack_conv_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
+    "ACT_GELU_TANH", "ACT_QUICK_GELU", "ACT_RELU", "decode_splits",
+]
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def _K():
+    return native.ops()
+
+
+def _i32(t: Optional[torch.Tensor]):
+    if t is None:
+        return None
+    return t if t.dtype == torch.int32 else t.to(torch.int32)
+
+
+# ----------------------------------------------------------------------------- norms
+def rmsnorm(x: torch.Tensor, w: Optional[torch.Tensor], eps: float = 1e-6, residual: Optional[torch.Tensor] = None,
+            w_offset: float = 0.0, out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """y = rmsnorm(x (+ residual)) * (w + w_offset); returns (y, x + residual or None)."""
+    if not _gpu(x):
+        return ref.rmsnorm(x, w, eps, residual, w_offset)
+    shape = x.shape
+    x2 = x if x.dim() == 2 else x.reshape(-1, shape[-1])
+    res2 = residual.reshape(-1, shape[-1]) if residual is not None else None
+    y = out if out is not None else torch.empty(x2.shape, dtype=x.dtype, device=x.device)
+    new_res = torch.empty(x2.shape, dtype=x.dtype, device=x.device) if residual is not None else None
+    _K().rmsnorm(x2, w, y, res2, new_res, float(eps), float(w_offset))
+    return y.view(shape), (new_res.view(shape) if new_res is not None else None)
+
+
+def layernorm(x: torch.Tensor, w: Optional[torch.Tensor], b: Optional[torch.Tensor], eps: float = 1e-5,
+              residual: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    if not _gpu(x):
+        return ref.layernorm(x, w, b, eps, residual)
+    shape = x.shape
+    x2 = x if x.dim() == 2 else x.reshape(-1, shape[-1])
+    res2 = residual.reshape(-1, shape[-1]) if residual is not None else None
+    y = torch.empty(x2.shape, dtype=x.dtype, device=x.device)
+    new_res = torch.empty(x2.shape, dtype=x.dtype, device=x.device) if residual is not None else None
+    _K().layernorm(x2, w, b, y, res2, new_res, float(eps))
+    return y.view(shape), (new_res.view(shape) if new_res is not None else None)
+
+
+def groupnorm_stats(x: torch.Tensor, gamma, beta, groups: int, eps: float):
+    """Channels-last GroupNorm statistics. x [N, ..., C] -> (scale, shift) fp32 [N, C]."""
+    N, C = x.shape[0], x.shape[-1]
+    x3 = x.reshape(N, -1, C)
+    if not _gpu(x):
+        return ref.groupnorm_stats(x3, gamma, beta, groups, eps)
+    HW = x3.shape[1]
+    nb = min(256, max(1, (HW + 511) // 512))
+    part = torch.empty(N * nb * groups * 2, dtype=torch.float32, device=x.device)
+    scale = torch.empty(N, C, dtype=torch.float32, device=x.device)
+    shift = torch.empty(N, C, dtype=torch.float32, device=x.device)
+    _K().groupnorm_stats(x3, gamma, beta, part, scale, shift, int(groups), float(eps))
+    return scale, shift
+
+
+def groupnorm_apply(x: torch.Tensor, scale, shift, silu: bool = False) -> torch.Tensor:
+    if not _gpu(x):
+        return ref.groupnorm_apply(x, scale, shift, silu)
+    N, C = x.shape[0], x.shape[-1]
+    out = torch.empty_like(x)
+    _K().groupnorm_apply(x.reshape(N, -1, C), scale, shift, out.view(N, -1, C), bool(silu))
+    return out
+
+
+def groupnorm(x, gamma, beta, groups, eps, silu=False):
+    scale, shift = groupnorm_stats(x, gamma, beta, groups, eps)
+    return groupnorm_apply(x, scale, shift, silu)
+
+
+# ----------------------------------------------------------------------------- GEMM / conv
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act=None,
+           residual: Optional[torch.Tensor] = None, glu: bool = False, alpha: float = 1.0,
+           res_alpha: float = 1.0) -> torch.Tensor:
+    """y = act(alpha * x @ w^T + bias) (+ res_alpha * residual).
+
+    glu=True: ``w`` rows are interleaved (value_i, gate_i) pairs and the output
+    has N/2 columns: value * act(gate) (SwiGLU / GEGLU fused in the epilogue).
+    """
+    if not _gpu(x):
+        return ref.linear(x, w, bias, act, residual, glu, alpha, res_alpha)
+    K = x.shape[-1]
+    N = w.shape[0]
+    lead = x.shape[:-1]
+    if x.dim() == 2 or x.is_contiguous():
+        x2 = x.reshape(-1, K)
+    else:
+        x2 = x.contiguous().reshape(-1, K)
+    Nout = N // 2 if glu else N
+    y = torch.empty(x2.shape[0], Nout, dtype=x.dtype, device=x.device)
+    r2 = residual.reshape(-1, Nout) if residual is not None else None
+    _K().gemm(x2, w, y, bias, None, 1, r2, float(alpha), float(res_alpha), act_id(act), bool(glu))
+    return y.view(*lead, Nout)
+
+
+def bmm(a: torch.Tensor, w: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
+    """Batched C[b] = alpha * a[b] @ w[b]^T (a [B,M,K], w [B,N,K])."""
+    if not _gpu(a):
+        return (torch.matmul(a.float(), w.float().transpose(-1, -2)) * alpha).to(a.dtype)
+    B, M, K = a.shape
+    N = w.shape[-2]
+    y = torch.empty(B, M, N, dtype=a.dtype, device=a.device)
+    _K().gemm(a, w, y, None, None, 1, None, float(alpha), 1.0, ACT_NONE, False)
+    return y
+
+
+def conv2d(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], kh: int, kw: int, stride: int = 1,
+           pad: int = 0, upsample: bool = False, x2: Optional[torch.Tensor] = None, norm=None,
+           temb: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None, act=None,
+           res_alpha: float = 1.0) -> torch.Tensor:
+    """NHWC implicit-GEMM convolution with fused prologue/epilogue.
+
+    norm = (scale [N,Cin] f32, shift [N,Cin] f32, act) applies GroupNorm(+act) to
+    the gathered input; x2 is concatenated on channels; upsample reads a
+    nearest-2x view; temb [N, Cout] is a per-image bias; residual is added last.
+    """
+    if not _gpu(x):
+        return ref.conv2d(x, w_packed, bias, kh, kw, stride, pad, upsample, x2, norm, temb, residual, act, res_alpha)
+    N, H, W, _ = x.shape
+    IH, IW = (2 * H, 2 * W) if upsample else (H, W)
+    OH = (IH + 2 * pad - kh) // stride + 1
+    OW = (IW + 2 * pad - kw) // stride + 1
+    cout = w_packed.shape[0]
+    out = torch.empty(N, OH, OW, cout, dtype=x.dtype, device=x.device)
+    sc, sh, nact = (norm if norm is not None else (None, None, None))
+    _K().conv2d(x, x2, w_packed, out, bias, temb, residual, sc, sh, act_id(nact), kh, kw, stride, pad, bool(upsample),
+                act_id(act), float(res_alpha))
+    return out
+
+
+# ----------------------------------------------------------------------------- attention
+def attention(q, k, v, scale: Optional[float] = None, causal: bool = False, causal_offset: int = 0, kv_lens=None,
+              q_lens=None, bias=None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fused flash attention. q [B,Sq,Hq,D] (packed heads), k/v [B,Skv,Hkv,D]."""
+    D = q.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if not _gpu(q):
+        return ref.attention(q, k, v, scale, causal, causal_offset, kv_lens, q_lens, bias)
+    o = out if out is not None else torch.empty(q.shape, dtype=q.dtype, device=q.device)
+    _K().flash_attn(q, k, v, o, float(scale), bool(causal), int(causal_offset), _i32(kv_lens), _i32(q_lens), bias,
+                    None)
+    return o
+
+
+def paged_attention(q, k_cache, v_cache, block_table, kv_lens, q_lens, scale=None, causal=True):
+    """Prefill attention over a paged KV cache (64-token blocks)."""
+    D = q.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if not _gpu(q):
+        return ref.paged_attention(q, k_cache, v_cache, block_table, kv_lens, q_lens, scale, causal)
+    o = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+    _K().flash_attn(q, k_cache, v_cache, o, float(scale), bool(causal), 0, _i32(kv_lens), _i32(q_lens), None,
+                    _i32(block_table))
+    return o
+
+
+def decode_splits(batch: int, hkv: int, max_ctx: int) -> int:
+    nblk = max(1, (max_ctx + 63) // 64)
+    want = max(1, 512 // max(1, batch * hkv))
+    return int(min(nblk, want, 64))
+
+
+def decode_attention(q, k_cache, v_cache, block_table, ctx_lens, scale=None, num_splits: Optional[int] = None,
+                     max_ctx: Optional[int] = None, out=None):
+    """Paged single-token decode attention. q [B,Hq,D]."""
+    D = q.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if not _gpu(q):
+        return ref.decode_attention(q, k_cache, v_cache, block_table, ctx_lens, scale)
+    B, Hq, _ = q.shape
+    if num_splits is None:
+        mc = max_ctx if max_ctx is not None else block_table.shape[1] * 64
+        num_splits = decode_splits(B, k_cache.shape[1], mc)
+    ws = torch.empty(B * Hq * num_splits * (D + 2), dtype=torch.float32, device=q.device)
+    o = out if out is not None else torch.empty(q.shape, dtype=q.dtype, device=q.device)
+    _K().decode_attn(q, k_cache, v_cache, o, _i32(block_table), _i32(ctx_lens), ws, int(num_splits), float(scale))
+    return o
+
+
+def kv_write(k, v, k_cache, v_cache, slots):
+    if not _gpu(k):
+        return ref.kv_write(k, v, k_cache, v_cache, slots)
+    _K().kv_write(k, v, k_cache, v_cache, _i32(slots))
+
+
+# ----------------------------------------------------------------------------- elementwise
+def rope(x, positions, cos, sin, rot_dim: Optional[int] = None, neox: bool = True):
+    """In-place rotary embedding on x [T, H, Dh] (token stride may be > H*Dh)."""
+    rot = rot_dim if rot_dim is not None else x.shape[-1]
+    if not _gpu(x):
+        return ref.rope(x, positions, cos, sin, rot, neox)
+    _K().rope(x, _i32(positions), cos, sin, int(rot), bool(neox))
+    return x
+
+
+def rope_pairs(x, cos, sin):
+    """In-place Flux RoPE on x [B, T, H, Dh] with cos/sin [T, Dh/2]."""
+    if not _gpu(x):
+        return ref.rope_pairs(x, cos, sin)
+    _K().rope_pairs(x, cos, sin)
+    return x
+
+
+def gated_act(x, act="silu", gate_first: bool = False):
+    """[.., 2F] -> [.., F]: a*act(g) (gate_first: act(a)*g)."""
+    if not _gpu(x):
+        return ref.gated_act(x, act, gate_first)
+    F_ = x.shape[-1] // 2
+    out = torch.empty(*x.shape[:-1], F_, dtype=x.dtype, device=x.device)
+    x2 = x if x.dim() == 2 else x.reshape(-1, x.shape[-1])
+    _K().gated_act(x2, out.view(-1, F_), act_id(act), bool(gate_first))
+    return out
+
+
+def bias_act(x, bias=None, residual=None, act=None, alpha: float = 1.0):
+    if not _gpu(x):
+        return ref.bias_act(x, bias, residual, act, alpha)
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    _K().bias_act(x, bias, residual.contiguous() if residual is not None else None, out, act_id(act), float(alpha))
+    return out
+
+
+def sched_step(model_out, latents, cfg: bool, guidance: float, pred_type: int, a_t: float, a_prev: float,
+               dt: float = 0.0):
+    """Fused CFG + scheduler update, in place on latents."""
+    if not _gpu(latents):
+        return ref.sched_step(model_out, latents, cfg, guidance, pred_type, a_t, a_prev, dt)
+    _K().sched_step(model_out, latents, bool(cfg), float(guidance), int(pred_type), float(a_t), float(a_prev),
+                    float(dt))
+    return latents
+
+
+def softmax_(x, scale: float = 1.0):
+    if not _gpu(x):
+        x.copy_(torch.softmax(x.float() * scale, dim=-1).to(x.dtype))
+        return x
+    _K().softmax_(x, float(scale))
+    return x
+
+
+def embedding(ids, table):
+    if not _gpu(table):
+        return table[ids.long()]
+    out = torch.empty(*ids.shape, table.shape[1], dtype=table.dtype, device=table.device)
+    _K().embedding(_i32(ids).contiguous(), table, out)
+    return out

@@ -1,0 +1,282 @@
+"""Plain-PyTorch fp32 reference implementations of every native op.
+
+Used (a) as the numerics oracle in tests (HIP kernel vs fp32 torch on the same
+inputs) and (b) as the CPU execution path (tests without a GPU, and the CPU
+DistilBERT "plumbing" config of BASELINE.json).  They compute in fp32 and
+return the input dtype, mirroring the kernels' bf16-in / fp32-math / bf16-out.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+ACT_NONE, ACT_SILU, ACT_GELU, ACT_GELU_TANH, ACT_QUICK_GELU, ACT_RELU = range(6)
+ACT_IDS = {"none": ACT_NONE, None: ACT_NONE, "silu": ACT_SILU, "gelu": ACT_GELU, "gelu_tanh": ACT_GELU_TANH,
+           "gelu_pytorch_tanh": ACT_GELU_TANH, "gelu_new": ACT_GELU_TANH, "quick_gelu": ACT_QUICK_GELU,
+           "relu": ACT_RELU, "swish": ACT_SILU}
+
+
+def act_id(act) -> int:
+    if isinstance(act, int):
+        return act
+    return ACT_IDS[act]
+
+
+def apply_act(x: torch.Tensor, act) -> torch.Tensor:
+    a = act_id(act)
+    if a == ACT_SILU:
+        return F.silu(x)
+    if a == ACT_GELU:
+        return F.gelu(x)
+    if a == ACT_GELU_TANH:
+        return F.gelu(x, approximate="tanh")
+    if a == ACT_QUICK_GELU:
+        return x * torch.sigmoid(1.702 * x)
+    if a == ACT_RELU:
+        return F.relu(x)
+    return x
+
+
+def rmsnorm(x, w, eps, residual=None, w_offset=0.0):
+    xf = x.float()
+    if residual is not None:
+        xf = xf + residual.float()
+    new_res = xf.to(x.dtype) if residual is not None else None
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    if w is not None:
+        y = y * (w.float() + w_offset)
+    return y.to(x.dtype), new_res
+
+
+def layernorm(x, w, b, eps, residual=None):
+    xf = x.float()
+    if residual is not None:
+        xf = xf + residual.float()
+    new_res = xf.to(x.dtype) if residual is not None else None
+    y = F.layer_norm(xf, (x.shape[-1],), w.float() if w is not None else None, b.float() if b is not None else None,
+                     eps)
+    return y.to(x.dtype), new_res
+
+
+def groupnorm_stats(x, gamma, beta, groups, eps):
+    """x [N, HW, C] -> (scale, shift) fp32 [N, C] with y = x*scale + shift."""
+    N, HW, C = x.shape
+    xf = x.float().reshape(N, HW, groups, C // groups)
+    mean = xf.mean(dim=(1, 3))  # [N, G]
+    var = xf.var(dim=(1, 3), unbiased=False)
+    rstd = torch.rsqrt(var + eps)
+    g = gamma.float() if gamma is not None else torch.ones(C, device=x.device)
+    b = beta.float() if beta is not None else torch.zeros(C, device=x.device)
+    rstd_c = rstd.repeat_interleave(C // groups, dim=1)
+    mean_c = mean.repeat_interleave(C // groups, dim=1)
+    scale = rstd_c * g
+    shift = b - mean_c * scale
+    return scale, shift
+
+
+def groupnorm_apply(x, scale, shift, silu):
+    N = x.shape[0]
+    C = x.shape[-1]
+    y = x.float() * scale.view(N, *([1] * (x.dim() - 2)), C) + shift.view(N, *([1] * (x.dim() - 2)), C)
+    if silu:
+        y = F.silu(y)
+    return y.to(x.dtype)
+
+
+def linear(x, w, bias=None, act=None, residual=None, glu=False, alpha=1.0, res_alpha=1.0):
+    y = torch.matmul(x.float(), w.float().t()) * alpha
+    if bias is not None:
+        y = y + bias.float()
+    if glu:
+        val, gate = y[..., 0::2], y[..., 1::2]
+        y = val * apply_act(gate, act)
+    else:
+        y = apply_act(y, act)
+    if residual is not None:
+        y = y + res_alpha * residual.float()
+    return y.to(x.dtype)
+
+
+def unpack_conv_weight(w_packed, cin, kh, kw):
+    cout = w_packed.shape[0]
+    return w_packed.reshape(cout, kh, kw, cin).permute(0, 3, 1, 2).contiguous()
+
+
+def pack_conv_weight(w):
+    """torch conv weight [Cout, Cin, KH, KW] -> [Cout, KH*KW*Cin] (k ordered (kh, kw, c))."""
+    cout = w.shape[0]
+    return w.permute(0, 2, 3, 1).reshape(cout, -1).contiguous()
+
+
+def conv2d(x, w_packed, bias, kh, kw, stride=1, pad=0, upsample=False, x2=None, norm=None, temb=None,
+           residual=None, act=None, res_alpha=1.0):
+    """x NHWC [N,H,W,C1] (+x2 [N,H,W,C2] concatenated on C) -> NHWC output."""
+    xin = x.float() if x2 is None else torch.cat([x.float(), x2.float()], dim=-1)
+    if norm is not None:
+        scale, shift, nact = norm
+        N, C = xin.shape[0], xin.shape[-1]
+        xin = xin * scale.view(N, 1, 1, C) + shift.view(N, 1, 1, C)
+        xin = apply_act(xin, nact)
+    xin = xin.to(x.dtype).float()  # the kernel rounds the gathered operand to bf16
+    if upsample:
+        xin = xin.repeat_interleave(2, dim=1).repeat_interleave(2, dim=2)
+    cin = xin.shape[-1]
+    w = unpack_conv_weight(w_packed.float(), cin, kh, kw)
+    y = F.conv2d(xin.permute(0, 3, 1, 2), w, None, stride=stride, padding=pad).permute(0, 2, 3, 1)
+    if bias is not None:
+        y = y + bias.float()
+    if temb is not None:
+        y = y + temb.float()[:, None, None, :]
+    y = apply_act(y, act)
+    if residual is not None:
+        y = y + res_alpha * residual.float().reshape(y.shape)
+    return y.to(x.dtype)
+
+
+def attention(q, k, v, scale=None, causal=False, causal_offset=0, kv_lens=None, q_lens=None, bias=None):
+    """q [B,Sq,Hq,D], k/v [B,Skv,Hkv,D] -> [B,Sq,Hq,D]."""
+    B, Sq, Hq, D = q.shape
+    Skv, Hkv = k.shape[1], k.shape[2]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    qf = q.float().permute(0, 2, 1, 3)
+    kf = k.float().permute(0, 2, 1, 3).repeat_interleave(Hq // Hkv, dim=1)
+    vf = v.float().permute(0, 2, 1, 3).repeat_interleave(Hq // Hkv, dim=1)
+    if kf.shape[0] == 1 and B > 1:
+        kf = kf.expand(B, -1, -1, -1)
+        vf = vf.expand(B, -1, -1, -1)
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if bias is not None:
+        s = s + bias.float()[None]
+    qi = torch.arange(Sq, device=q.device).view(1, 1, Sq, 1)
+    ki = torch.arange(Skv, device=q.device).view(1, 1, 1, Skv)
+    mask = torch.zeros(B, 1, Sq, Skv, dtype=torch.bool, device=q.device)
+    kvl = kv_lens.view(B, 1, 1, 1).to(q.device) if kv_lens is not None else torch.full((B, 1, 1, 1), Skv,
+                                                                                          device=q.device)
+    mask |= ki >= kvl
+    if causal:
+        if q_lens is not None:
+            off = kvl - q_lens.view(B, 1, 1, 1).to(q.device)
+        else:
+            off = causal_offset
+        mask |= ki > qi + off
+    s = s.masked_fill(mask, float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    p = torch.nan_to_num(p, nan=0.0)
+    o = torch.matmul(p, vf).permute(0, 2, 1, 3)
+    if q_lens is not None:
+        valid = (torch.arange(Sq, device=q.device).view(1, Sq) < q_lens.view(B, 1).to(q.device))
+        o = o * valid.view(B, Sq, 1, 1)
+    return o.to(q.dtype)
+
+
+def gather_paged(cache, block_table, length):
+    """cache [blocks, H, 64, D], table row -> [length, H, D]"""
+    nb = (length + 63) // 64
+    blocks = cache[block_table[:nb].long()]  # [nb, H, 64, D]
+    return blocks.permute(0, 2, 1, 3).reshape(nb * 64, cache.shape[1], cache.shape[3])[:length]
+
+
+def paged_attention(q, k_cache, v_cache, block_table, kv_lens, q_lens, scale=None, causal=True):
+    B, Sq, Hq, D = q.shape
+    out = torch.zeros_like(q)
+    for b in range(B):
+        L = int(kv_lens[b])
+        ql = int(q_lens[b]) if q_lens is not None else Sq
+        k = gather_paged(k_cache, block_table[b], L)[None]
+        v = gather_paged(v_cache, block_table[b], L)[None]
+        o = attention(q[b:b + 1, :ql], k, v, scale=scale, causal=causal, causal_offset=L - ql)
+        out[b, :ql] = o[0]
+    return out
+
+
+def decode_attention(q, k_cache, v_cache, block_table, ctx_lens, scale=None):
+    B, Hq, D = q.shape
+    out = torch.empty_like(q)
+    for b in range(B):
+        L = int(ctx_lens[b])
+        k = gather_paged(k_cache, block_table[b], L)[None]
+        v = gather_paged(v_cache, block_table[b], L)[None]
+        out[b] = attention(q[b:b + 1, None], k, v, scale=scale)[0, 0]
+    return out
+
+
+def kv_write(k, v, k_cache, v_cache, slots):
+    for t in range(k.shape[0]):
+        s = int(slots[t])
+        if s < 0:
+            continue
+        k_cache[s // 64, :, s % 64] = k[t]
+        v_cache[s // 64, :, s % 64] = v[t]
+
+
+def rope(x, positions, cos, sin, rot_dim, neox=True):
+    """in-place rotary on x [T, H, Dh]"""
+    half = rot_dim // 2
+    c = cos[positions.long()].unsqueeze(1)  # [T,1,half]
+    s = sin[positions.long()].unsqueeze(1)
+    xf = x.float()
+    if neox:
+        a, b = xf[..., :half], xf[..., half:rot_dim]
+    else:
+        a, b = xf[..., 0:rot_dim:2], xf[..., 1:rot_dim:2]
+    ra = a * c - b * s
+    rb = b * c + a * s
+    if neox:
+        x[..., :half] = ra.to(x.dtype)
+        x[..., half:rot_dim] = rb.to(x.dtype)
+    else:
+        x[..., 0:rot_dim:2] = ra.to(x.dtype)
+        x[..., 1:rot_dim:2] = rb.to(x.dtype)
+    return x
+
+
+def rope_pairs(x, cos, sin):
+    """in-place Flux rope: x [B,T,H,Dh], cos/sin [T, Dh/2] applied to pairs (2j, 2j+1)."""
+    xf = x.float()
+    a, b = xf[..., 0::2], xf[..., 1::2]
+    c = cos.view(1, cos.shape[0], 1, -1)
+    s = sin.view(1, sin.shape[0], 1, -1)
+    x[..., 0::2] = (a * c - b * s).to(x.dtype)
+    x[..., 1::2] = (b * c + a * s).to(x.dtype)
+    return x
+
+
+def gated_act(x, act, gate_first=False):
+    F_ = x.shape[-1] // 2
+    a, g = x[..., :F_].float(), x[..., F_:].float()
+    y = apply_act(a, act) * g if gate_first else a * apply_act(g, act)
+    return y.to(x.dtype)
+
+
+def bias_act(x, bias=None, residual=None, act=None, alpha=1.0):
+    y = x.float() * alpha
+    if bias is not None:
+        y = y + bias.float()
+    y = apply_act(y, act)
+    if residual is not None:
+        y = y + residual.float()
+    return y.to(x.dtype)
+
+
+def sched_step(model_out, latents, cfg, guidance, pred_type, a_t, a_prev, dt):
+    n = latents.numel()
+    e = model_out.float().reshape(-1)
+    if cfg:
+        eu, ec = e[:n], e[n:]
+        e = eu + guidance * (ec - eu)
+    x = latents.float().reshape(-1)
+    if pred_type == 2:
+        x = x + dt * e
+    else:
+        sa, s1a = math.sqrt(a_t), math.sqrt(1 - a_t)
+        if pred_type == 0:
+            eps = e
+            x0 = (x - s1a * eps) / sa
+        else:
+            x0 = sa * x - s1a * e
+            eps = sa * e + s1a * x
+        x = math.sqrt(a_prev) * x0 + math.sqrt(1 - a_prev) * eps
+    latents.copy_(x.view_as(latents).to(latents.dtype))
+    return latents

@@ -1,0 +1,281 @@
+"""HIP kernel numerics vs plain-PyTorch fp32 references (same random inputs).
+
+Each test runs the native gfx950 kernel (torch.ops.shai.*) and the fp32 torch
+reference from shai_amd.ops.reference and compares with bf16 tolerances.
+"""
+import math
+
+import pytest
+import torch
+
+import shai_amd.ops as ops
+from shai_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def rnd(*shape, scale=1.0, device="cuda"):
+    return (torch.randn(*shape, device=device) * scale).to(torch.bfloat16)
+
+
+def close(a, b, atol, rtol=2e-2):
+    a = a.float()
+    b = b.float()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).float().mean().item()
+    assert torch.isfinite(a).all(), "non-finite output"
+    assert bad < 1e-3, f"{bad*100:.3f}% elements out of tolerance; max err {err.max().item():.4g}"
+
+
+@pytest.mark.parametrize("D", [320, 768, 4096, 1280, 5120])
+def test_rmsnorm(cuda, D):
+    torch.manual_seed(0)
+    x, r, w = rnd(67, D), rnd(67, D), rnd(D)
+    y, nr = ops.rmsnorm(x, w, 1e-6, residual=r)
+    yr, nrr = ref.rmsnorm(x, w, 1e-6, residual=r)
+    close(y, yr, 2e-2)
+    close(nr, nrr, 1e-2)
+    y2, _ = ops.rmsnorm(x, w, 1e-5)
+    close(y2, ref.rmsnorm(x, w, 1e-5)[0], 2e-2)
+
+
+@pytest.mark.parametrize("D", [64, 768, 1024, 3072])
+def test_layernorm(cuda, D):
+    torch.manual_seed(1)
+    x, w, b = rnd(129, D, scale=3.0) + 1.0, rnd(D), rnd(D)
+    close(ops.layernorm(x, w, b, 1e-5)[0], ref.layernorm(x, w, b, 1e-5)[0], 2e-2)
+    close(ops.layernorm(x, None, None, 1e-6)[0], ref.layernorm(x, None, None, 1e-6)[0], 2e-2)
+
+
+@pytest.mark.parametrize("N,HW,C,G", [(2, 4096, 320, 32), (1, 256, 1280, 32), (2, 64, 2560, 32), (1, 16384, 128, 32),
+                                      (3, 100, 64, 32)])
+def test_groupnorm(cuda, N, HW, C, G):
+    torch.manual_seed(2)
+    x = rnd(N, HW, C, scale=2.0) + 0.5
+    g, b = rnd(C), rnd(C)
+    sc, sh = ops.groupnorm_stats(x, g, b, G, 1e-5)
+    scr, shr = ref.groupnorm_stats(x, g, b, G, 1e-5)
+    torch.testing.assert_close(sc, scr, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(sh, shr, atol=1e-3, rtol=1e-3)
+    close(ops.groupnorm_apply(x, sc, sh, True), ref.groupnorm_apply(x, scr, shr, True), 2e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (1000, 320, 1280), (77, 1024, 1024), (8192, 640, 320),
+                                   (5, 4096, 4096), (300, 96, 72)])
+@pytest.mark.parametrize("act", ["none", "silu", "gelu"])
+def test_gemm(cuda, M, N, K, act):
+    torch.manual_seed(3)
+    x, w, b, r = rnd(M, K), rnd(N, K, scale=1 / math.sqrt(K)), rnd(N), rnd(M, N)
+    close(ops.linear(x, w, b, act=act, residual=r), ref.linear(x, w, b, act, r), 2e-2)
+
+
+def test_gemm_identity_asymmetric(cuda):
+    """A = I with an asymmetric W catches row/col swaps in the C write."""
+    M = N = K = 128
+    a = torch.eye(M, device="cuda").to(torch.bfloat16)
+    w = (torch.arange(N * K, device="cuda").float().view(N, K) % 17 - 8).to(torch.bfloat16)
+    y = ops.linear(a, w)
+    torch.testing.assert_close(y.float(), w.float().t(), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("act", ["gelu", "silu"])
+def test_gemm_glu(cuda, act):
+    torch.manual_seed(4)
+    M, N, K = 500, 2 * 640, 320
+    x, w, b = rnd(M, K), rnd(N, K, scale=1 / math.sqrt(K)), rnd(N)
+    close(ops.linear(x, w, b, act=act, glu=True), ref.linear(x, w, b, act, glu=True), 2e-2)
+
+
+def test_bmm(cuda):
+    torch.manual_seed(5)
+    a, w = rnd(3, 200, 64), rnd(3, 150, 64)
+    close(ops.bmm(a, w, 0.5), (torch.matmul(a.float(), w.float().transpose(1, 2)) * 0.5), 2e-2)
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(N=2, H=32, W=32, C=320, Co=320, k=3, s=1, p=1),
+    dict(N=1, H=16, W=16, C=640, Co=1280, k=3, s=2, p=1),
+    dict(N=2, H=8, W=8, C=128, Co=64, k=1, s=1, p=0),
+    dict(N=1, H=24, W=20, C=8, Co=320, k=3, s=1, p=1),
+    dict(N=1, H=16, W=16, C=512, Co=3, k=3, s=1, p=1),
+])
+def test_conv2d(cuda, cfg):
+    torch.manual_seed(6)
+    x = rnd(cfg["N"], cfg["H"], cfg["W"], cfg["C"])
+    w = ops.pack_conv_weight(rnd(cfg["Co"], cfg["C"], cfg["k"], cfg["k"], scale=1 / math.sqrt(cfg["C"] * 9)))
+    b = rnd(cfg["Co"])
+    y = ops.conv2d(x, w, b, cfg["k"], cfg["k"], cfg["s"], cfg["p"])
+    yr = ref.conv2d(x, w, b, cfg["k"], cfg["k"], cfg["s"], cfg["p"])
+    close(y, yr, 3e-2)
+
+
+def test_conv2d_fused(cuda):
+    """GroupNorm+SiLU prologue, concat, upsample, temb bias and residual epilogue."""
+    torch.manual_seed(7)
+    N, H, W, C1, C2, Co = 2, 16, 16, 320, 640, 320
+    x, x2 = rnd(N, H, W, C1), rnd(N, H, W, C2)
+    sc, sh = ops.groupnorm_stats(torch.cat([x, x2], -1), rnd(C1 + C2), rnd(C1 + C2), 32, 1e-5)
+    w = ops.pack_conv_weight(rnd(Co, C1 + C2, 3, 3, scale=1 / math.sqrt((C1 + C2) * 9)))
+    b, temb = rnd(Co), rnd(N, Co)
+    res = rnd(N, 2 * H, 2 * W, Co)
+    y = ops.conv2d(x, w, b, 3, 3, 1, 1, upsample=True, x2=x2, norm=(sc, sh, "silu"), temb=temb, residual=res)
+    yr = ref.conv2d(x, w, b, 3, 3, 1, 1, upsample=True, x2=x2, norm=(sc, sh, "silu"), temb=temb, residual=res)
+    close(y, yr, 3e-2)
+
+
+@pytest.mark.parametrize("B,Sq,Skv,Hq,Hkv,D,causal", [
+    (2, 256, 256, 4, 4, 64, False),
+    (1, 1000, 77, 5, 5, 64, False),
+    (2, 333, 333, 8, 2, 128, True),
+    (1, 128, 128, 32, 8, 128, True),
+    (3, 197, 197, 12, 12, 64, False),
+    (1, 1056, 1056, 3, 3, 128, False),
+])
+def test_flash_attn(cuda, B, Sq, Skv, Hq, Hkv, D, causal):
+    torch.manual_seed(8)
+    q, k, v = rnd(B, Sq, Hq, D), rnd(B, Skv, Hkv, D), rnd(B, Skv, Hkv, D)
+    o = ops.attention(q, k, v, causal=causal)
+    orf = ref.attention(q, k, v, 1 / math.sqrt(D), causal)
+    close(o, orf, 2e-2)
+
+
+def test_flash_attn_strided_qkv_and_lens(cuda):
+    torch.manual_seed(9)
+    B, S, H, D = 3, 150, 12, 64
+    qkv = rnd(B, S, 3, H, D)
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    lens = torch.tensor([150, 77, 5], device="cuda", dtype=torch.int32)
+    o = ops.attention(q, k, v, kv_lens=lens)
+    orf = ref.attention(q, k, v, 1 / math.sqrt(D), kv_lens=lens)
+    close(o, orf, 2e-2)
+
+
+def test_flash_attn_bias(cuda):
+    torch.manual_seed(10)
+    B, S, H, D = 2, 96, 4, 64
+    q, k, v = rnd(B, S, H, D), rnd(B, S, H, D), rnd(B, S, H, D)
+    bias = rnd(H, S, S, scale=2.0)
+    close(ops.attention(q, k, v, scale=1.0, bias=bias), ref.attention(q, k, v, 1.0, bias=bias), 3e-2)
+
+
+def test_flash_attn_spike_forces_rescale(cuda):
+    """A late key with a huge score forces the online-softmax rescale branch."""
+    torch.manual_seed(11)
+    B, S, H, D = 1, 256, 2, 128
+    q, k, v = rnd(B, S, H, D), rnd(B, S, H, D), rnd(B, S, H, D)
+    k[:, 200] = q[:, 10] * 4
+    close(ops.attention(q, k, v), ref.attention(q, k, v, 1 / math.sqrt(D)), 2e-2)
+
+
+def _paged_setup(B, Hkv, D, ctx, nblocks=64):
+    kc = rnd(nblocks, Hkv, 64, D)
+    vc = rnd(nblocks, Hkv, 64, D)
+    maxb = max((c + 63) // 64 for c in ctx)
+    perm = torch.randperm(nblocks, device="cuda").to(torch.int32)
+    bt = torch.zeros(B, maxb, dtype=torch.int32, device="cuda")
+    i = 0
+    for b, c in enumerate(ctx):
+        nb = (c + 63) // 64
+        bt[b, :nb] = perm[i:i + nb]
+        i += nb
+    return kc, vc, bt
+
+
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (64, 8, 8), (128, 64, 8)])
+def test_decode_attn(cuda, D, Hq, Hkv):
+    torch.manual_seed(12)
+    ctx = [1, 64, 300, 1000]
+    B = len(ctx)
+    kc, vc, bt = _paged_setup(B, Hkv, D, ctx)
+    q = rnd(B, Hq, D)
+    lens = torch.tensor(ctx, dtype=torch.int32, device="cuda")
+    for splits in (1, 3):
+        o = ops.decode_attention(q, kc, vc, bt, lens, num_splits=splits)
+        close(o, ref.decode_attention(q, kc, vc, bt, lens, 1 / math.sqrt(D)), 2e-2)
+
+
+def test_paged_prefill_attn(cuda):
+    torch.manual_seed(13)
+    D, Hq, Hkv = 128, 8, 2
+    ctx = [100, 300]
+    q_lens = [37, 300]
+    kc, vc, bt = _paged_setup(2, Hkv, D, ctx)
+    q = rnd(2, 300, Hq, D)
+    kl = torch.tensor(ctx, dtype=torch.int32, device="cuda")
+    ql = torch.tensor(q_lens, dtype=torch.int32, device="cuda")
+    o = ops.paged_attention(q, kc, vc, bt, kl, ql)
+    orf = ref.paged_attention(q, kc, vc, bt, kl, ql, 1 / math.sqrt(D))
+    close(o[0, :37], orf[0, :37], 2e-2)
+    close(o[1], orf[1], 2e-2)
+
+
+def test_kv_write(cuda):
+    torch.manual_seed(14)
+    T, H, D = 70, 8, 128
+    k, v = rnd(T, H, D), rnd(T, H, D)
+    kc, vc = torch.zeros(4, H, 64, D, dtype=torch.bfloat16, device="cuda"), torch.zeros(4, H, 64, D,
+                                                                                      dtype=torch.bfloat16,
+                                                                                      device="cuda")
+    slots = torch.randperm(256, device="cuda")[:T].to(torch.int32)
+    kr, vr = kc.clone(), vc.clone()
+    ops.kv_write(k, v, kc, vc, slots)
+    ref.kv_write(k, v, kr, vr, slots)
+    assert torch.equal(kc, kr) and torch.equal(vc, vr)
+
+
+def test_rope(cuda):
+    torch.manual_seed(15)
+    T, H, D = 33, 8, 128
+    qkv = rnd(T, 3 * H * D)
+    q = qkv[:, : H * D].view(T, H, D)
+    pos = torch.randint(0, 500, (T,), device="cuda", dtype=torch.int32)
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2, device="cuda").float() / D))
+    fr = torch.outer(torch.arange(512, device="cuda").float(), inv)
+    c, s = fr.cos().contiguous(), fr.sin().contiguous()
+    qr = q.clone()
+    ops.rope(q, pos, c, s)
+    ref.rope(qr, pos, c, s, D)
+    close(q, qr, 2e-2)
+
+
+def test_rope_pairs(cuda):
+    torch.manual_seed(16)
+    B, T, H, D = 1, 40, 3, 128
+    x = rnd(B, T, H, D)
+    ang = torch.rand(T, D // 2, device="cuda") * 6
+    xr = x.clone()
+    ops.rope_pairs(x, ang.cos().contiguous(), ang.sin().contiguous())
+    ref.rope_pairs(xr, ang.cos(), ang.sin())
+    close(x, xr, 2e-2)
+
+
+def test_gated_and_bias_act(cuda):
+    torch.manual_seed(17)
+    x = rnd(100, 2 * 1280)
+    close(ops.gated_act(x, "gelu"), ref.gated_act(x, "gelu"), 2e-2)
+    close(ops.gated_act(x, "silu", gate_first=True), ref.gated_act(x, "silu", True), 2e-2)
+    y, b, r = rnd(64, 320), rnd(320), rnd(64, 320)
+    close(ops.bias_act(y, b, r, "silu", 0.5), ref.bias_act(y, b, r, "silu", 0.5), 2e-2)
+
+
+@pytest.mark.parametrize("pred", [0, 1, 2])
+def test_sched_step(cuda, pred):
+    torch.manual_seed(18)
+    lat = rnd(2, 64, 64, 4)
+    mo = rnd(4, 64, 64, 4)
+    a = lat.clone()
+    ops.sched_step(mo, lat, True, 7.5, pred, 0.5, 0.7, -0.05)
+    ref.sched_step(mo, a, True, 7.5, pred, 0.5, 0.7, -0.05)
+    close(lat, a, 3e-2)
+
+
+def test_softmax_embedding(cuda):
+    torch.manual_seed(19)
+    x = rnd(10, 4096)
+    y = x.clone()
+    ops.softmax_(y, 0.125)
+    close(y, torch.softmax(x.float() * 0.125, -1), 1e-3)
+    table = rnd(1000, 256)
+    ids = torch.randint(0, 1000, (3, 17), device="cuda")
+    assert torch.equal(ops.embedding(ids, table), table[ids])
