@@ -1,0 +1,378 @@
+"""Continuous-batching LLM engine on the paged KV cache.
+
+Replaces the vLLM ``LLM`` engine the reference builds from /vllm_config.yaml
+(app/vllm_model_api.py:24-43,127-133; Neuron config with continuous batching,
+buckets and on-device sampling in cova/mllama-32-11b-vllm-trn1-config.yaml) and
+HF ``generate`` (app/run-llama.py:34-46, app/deepseek_model_api.py:45-57).
+
+Per engine step (one call to :meth:`LLMEngine.step`):
+  1. the native scheduler (csrc/runtime/scheduler.cpp) admits waiting prompts
+     FCFS under KV-block / sequence / token budgets;
+  2. admitted prompts run as one padded prefill batch (prefix-cached blocks are
+     reused via the native block manager's content hashes);
+  3. otherwise every running sequence decodes one token -- the decode forward
+     for each batch-size bucket is captured once into a HIP graph and replayed;
+  4. sampling (temperature / top-k / top-p; greedy at temperature 0) on device.
+With TP > 1 every rank runs the same deterministic loop (SPMD); logits are
+all-gathered so all ranks sample identically.
+"""
+from __future__ import annotations
+
+import hashlib
+import itertools
+import math
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.llama import (KV_BLOCK, Batch, LlamaConfig, LlamaForCausalLM, allocate_kv_cache, kv_bytes_per_block)
+from ..parallel.state import tp
+from ..weights import materialize
+
+
+@dataclass
+class SamplingParams:
+    temperature: float = 0.7
+    top_k: int = 50
+    top_p: float = 0.9
+    max_tokens: int = 128
+    stop_token_ids: Optional[List[int]] = None
+    ignore_eos: bool = False
+    seed: Optional[int] = None
+
+
+@dataclass
+class Sequence_:
+    seq_id: int
+    prompt: List[int]
+    params: SamplingParams
+    output: List[int] = field(default_factory=list)
+    blocks: List[int] = field(default_factory=list)
+    n_cached: int = 0        # tokens whose K/V are in the cache
+    arrival: float = field(default_factory=time.perf_counter)
+    first_token_time: Optional[float] = None
+    finish_time: Optional[float] = None
+    finished: bool = False
+    finish_reason: Optional[str] = None
+
+    @property
+    def tokens(self) -> List[int]:
+        return self.prompt + self.output
+
+    @property
+    def length(self) -> int:
+        return len(self.prompt) + len(self.output)
+
+
+def _chain_hash(prev: int, toks: Sequence[int]) -> int:
+    h = hashlib.blake2b(digest_size=8)
+    h.update(prev.to_bytes(8, "little"))
+    h.update(np.asarray(toks, dtype=np.int32).tobytes())
+    return int.from_bytes(h.digest(), "little") or 1
+
+
+def sample(logits: torch.Tensor, temps: torch.Tensor, top_k: torch.Tensor, top_p: torch.Tensor,
+           gen: Optional[torch.Generator] = None) -> torch.Tensor:
+    """Temperature / top-k / top-p sampling; rows with temperature 0 are greedy."""
+    lf = logits.float()
+    greedy = lf.argmax(-1)
+    V = lf.shape[-1]
+    kmax = int(top_k.max().item()) if top_k.numel() else 0
+    K = V if kmax <= 0 or kmax > V or bool((top_k <= 0).any()) else kmax
+    t = torch.clamp(temps, min=1e-5).unsqueeze(-1)
+    vals, idx = torch.topk(lf / t, K, dim=-1)
+    ar = torch.arange(K, device=lf.device).unsqueeze(0)
+    kk = torch.where(top_k <= 0, torch.full_like(top_k, K), top_k).unsqueeze(-1)
+    vals = vals.masked_fill(ar >= kk, float("-inf"))
+    probs = torch.softmax(vals, -1)
+    cum = probs.cumsum(-1)
+    probs = probs.masked_fill((cum - probs) > top_p.unsqueeze(-1), 0.0)
+    probs = probs / probs.sum(-1, keepdim=True)
+    pick = torch.multinomial(probs, 1, generator=gen).squeeze(-1)
+    sampled = idx.gather(-1, pick.unsqueeze(-1)).squeeze(-1)
+    return torch.where(temps <= 0, greedy, sampled)
+
+
+class _DecodeGraph:
+    def __init__(self, engine: "LLMEngine", Bc: int):
+        self.Bc = Bc
+        dev = engine.device
+        mb = engine.max_blocks
+        self.ids = torch.zeros(Bc, dtype=torch.int32, device=dev)
+        self.pos = torch.zeros(Bc, dtype=torch.int32, device=dev)
+        self.slots = torch.full((Bc,), -1, dtype=torch.int32, device=dev)
+        self.lens = torch.ones(Bc, dtype=torch.int32, device=dev)
+        self.bt = torch.zeros(Bc, mb, dtype=torch.int32, device=dev)
+        self.splits = ops.decode_splits(Bc, engine.model.kv_heads_local, engine.max_model_len)
+        self.batch = Batch(self.ids, self.pos, self.slots, self.bt, self.lens, None, Bc, 1, False, self.splits)
+        self.graph = None
+        self.engine = engine
+        if engine.use_graphs:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    engine.model(self.batch, engine.kv)
+            torch.cuda.current_stream().wait_stream(s)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.logits = engine.model(self.batch, engine.kv)
+
+    def run(self, ids, pos, slots, lens, bt):
+        B = len(ids)
+        self.ids[:B].copy_(torch.from_numpy(np.asarray(ids, dtype=np.int32)), non_blocking=True)
+        self.pos[:B].copy_(torch.from_numpy(pos), non_blocking=True)
+        self.slots[:B].copy_(torch.from_numpy(slots), non_blocking=True)
+        self.lens[:B].copy_(torch.from_numpy(lens), non_blocking=True)
+        self.bt[:B].copy_(torch.from_numpy(bt), non_blocking=True)
+        if B < self.Bc:
+            self.slots[B:].fill_(-1)
+            self.lens[B:].fill_(1)
+            self.bt[B:].zero_()
+        if self.graph is not None:
+            self.graph.replay()
+            return self.logits[:B]
+        return self.engine.model(self.batch, self.engine.kv)[:B]
+
+
+class LLMEngine:
+    def __init__(self, cfg: LlamaConfig, device="cuda", model_path: Optional[str] = None, seed: int = 0,
+                 max_num_seqs: int = 64, max_model_len: int = 4096, num_kv_blocks: Optional[int] = None,
+                 gpu_memory_utilization: float = 0.85, prefill_token_budget: int = 8192, use_graphs: bool = True,
+                 enable_prefix_caching: bool = True):
+        from ..runtime import BlockManager
+        self.cfg = cfg
+        self.device = torch.device(device)
+        with torch.device(self.device):
+            self.model = LlamaForCausalLM(cfg)
+        materialize(self.model, self.device, model_path, None, seed)
+        self.weights = self.model._shai_weights
+        self.max_num_seqs = max_num_seqs
+        self.max_model_len = min(max_model_len, cfg.max_position_embeddings)
+        self.max_blocks = (self.max_model_len + KV_BLOCK - 1) // KV_BLOCK
+        hk = self.model.kv_heads_local
+        if num_kv_blocks is None:
+            if self.device.type == "cuda":
+                free, total = torch.cuda.mem_get_info(self.device)
+                budget = free - (1 - gpu_memory_utilization) * total
+                num_kv_blocks = int(max(budget, 0) // kv_bytes_per_block(cfg, hk))
+                num_kv_blocks = max(16, min(num_kv_blocks, max_num_seqs * self.max_blocks + 64))
+            else:
+                num_kv_blocks = max_num_seqs * self.max_blocks + 8
+        self.num_kv_blocks = num_kv_blocks
+        self.kv_buf, self.kv = allocate_kv_cache(cfg, hk, num_kv_blocks, self.device)
+        self.bm = BlockManager(num_kv_blocks)
+        self.prefill_token_budget = prefill_token_budget
+        self.prefix_caching = enable_prefix_caching
+        self.use_graphs = use_graphs and self.device.type == "cuda"
+        self.waiting: List[Sequence_] = []
+        self.running: List[Sequence_] = []
+        self._ids = itertools.count()
+        self._graphs: Dict[int, _DecodeGraph] = {}
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed)
+        self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "steps": 0, "prefix_hit_tokens": 0}
+        self.eos = {cfg.eos_token_id}
+
+    # ------------------------------------------------------------------ requests
+    def add_request(self, prompt: Sequence[int], params: Optional[SamplingParams] = None) -> Sequence_:
+        params = params or SamplingParams()
+        prompt = list(prompt)[-(self.max_model_len - 1):] or [self.cfg.bos_token_id]
+        s = Sequence_(next(self._ids), prompt, params)
+        self.waiting.append(s)
+        return s
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    # ------------------------------------------------------------------ kv blocks
+    def _ensure_blocks(self, s: Sequence_, n_tokens: int) -> bool:
+        need = (n_tokens + KV_BLOCK - 1) // KV_BLOCK - len(s.blocks)
+        if need <= 0:
+            return True
+        if self.bm.num_free < need:
+            return False
+        s.blocks += self.bm.allocate(need)
+        return True
+
+    def _free(self, s: Sequence_):
+        self.bm.release(s.blocks)
+        s.blocks = []
+
+    def _prefix_hashes(self, toks: Sequence[int], n_full: int) -> List[int]:
+        hs, h = [], 0
+        for i in range(n_full):
+            h = _chain_hash(h, toks[i * KV_BLOCK:(i + 1) * KV_BLOCK])
+            hs.append(h)
+        return hs
+
+    # ------------------------------------------------------------------ steps
+    def _admit(self) -> List[Sequence_]:
+        from ..runtime import sched_admit
+        if not self.waiting:
+            return []
+        watermark = max(1, len(self.running))
+        n = sched_admit([len(s.prompt) for s in self.waiting], self.bm.num_free, len(self.running),
+                        self.max_num_seqs, self.prefill_token_budget, watermark)
+        adm = self.waiting[:n]
+        del self.waiting[:n]
+        return adm
+
+    def _prefill(self, seqs: List[Sequence_]):
+        for s in seqs:
+            if self.prefix_caching:
+                n_full = (len(s.prompt) - 1) // KV_BLOCK
+                hs = self._prefix_hashes(s.prompt, n_full)
+                got = self.bm.lookup_prefix(hs)
+                s.blocks = list(got)
+                s.n_cached = len(got) * KV_BLOCK
+                s._hashes = hs
+                self.stats["prefix_hit_tokens"] += s.n_cached
+            ok = self._ensure_blocks(s, len(s.prompt) + 1)
+            assert ok, "scheduler admitted a prompt without blocks"
+        S = max(len(s.prompt) - s.n_cached for s in seqs)
+        from ..runtime import build_prefill
+        pos, slots, lens, qlens, bt, last = build_prefill([s.n_cached for s in seqs],
+                                                          [len(s.prompt) - s.n_cached for s in seqs],
+                                                          [s.blocks for s in seqs], S, self.max_blocks)
+        ids = np.zeros(len(seqs) * S, dtype=np.int32)
+        for i, s in enumerate(seqs):
+            new = s.prompt[s.n_cached:]
+            ids[i * S:i * S + len(new)] = new
+        d = self.device
+        t = lambda a: torch.from_numpy(a).to(d, non_blocking=True)
+        batch = Batch(t(ids), t(pos), t(slots), t(bt), t(lens), t(qlens), len(seqs), S, True, 1, t(last).long())
+        logits = self.model(batch, self.kv)
+        self.stats["prefill_tokens"] += int(sum(len(s.prompt) - s.n_cached for s in seqs))
+        for s in seqs:
+            s.n_cached = len(s.prompt)
+            if self.prefix_caching:
+                for i, h in enumerate(s._hashes):
+                    self.bm.register(s.blocks[i], h)
+        self._sample_and_append(seqs, logits)
+
+    def _decode(self, seqs: List[Sequence_]):
+        from ..runtime import build_decode
+        for s in seqs:
+            if not self._ensure_blocks(s, s.length):
+                # preempt (recompute later): free blocks, requeue at the front
+                self._free(s)
+                s.n_cached = 0
+                s.prompt = s.prompt + s.output
+                s.output = []
+                self.running.remove(s)
+                self.waiting.insert(0, s)
+        seqs = [s for s in seqs if s in self.running]
+        if not seqs:
+            return
+        B = len(seqs)
+        pos, slots, lens, bt = build_decode([s.length - 1 for s in seqs], [s.blocks for s in seqs], self.max_blocks)
+        ids = [s.tokens[-1] for s in seqs]
+        Bc = 1 << max(0, math.ceil(math.log2(B)))
+        g = self._graphs.get(Bc)
+        if g is None:
+            g = self._graphs[Bc] = _DecodeGraph(self, Bc)
+        logits = g.run(ids, pos, slots, lens, bt)
+        self.stats["decode_tokens"] += B
+        for s in seqs:
+            s.n_cached = s.length
+        self._sample_and_append(seqs, logits)
+
+    def _sample_and_append(self, seqs, logits):
+        d = self.device
+        temps = torch.tensor([s.params.temperature for s in seqs], dtype=torch.float32, device=d)
+        tk = torch.tensor([s.params.top_k for s in seqs], dtype=torch.int64, device=d)
+        tpp = torch.tensor([s.params.top_p for s in seqs], dtype=torch.float32, device=d)
+        toks = sample(logits, temps, tk, tpp, self.gen).tolist()
+        now = time.perf_counter()
+        for s, tok in zip(seqs, toks):
+            s.output.append(int(tok))
+            if s.first_token_time is None:
+                s.first_token_time = now
+            stop = set(s.params.stop_token_ids or []) | (set() if s.params.ignore_eos else self.eos)
+            if tok in stop:
+                s.finished, s.finish_reason = True, "stop"
+            elif len(s.output) >= s.params.max_tokens or s.length >= self.max_model_len:
+                s.finished, s.finish_reason = True, "length"
+            if s.finished:
+                s.finish_time = now
+
+    def step(self) -> List[Sequence_]:
+        """Run one engine iteration; returns sequences that finished in it."""
+        self.stats["steps"] += 1
+        adm = self._admit()
+        if adm:
+            self.running += adm
+            self._prefill(adm)
+        elif self.running:
+            self._decode(list(self.running))
+        done = [s for s in self.running if s.finished]
+        for s in done:
+            self._free(s)
+            self.running.remove(s)
+        return done
+
+    @torch.inference_mode()
+    def generate(self, prompts: Sequence[Sequence[int]], params: Optional[SamplingParams] = None) -> List[Sequence_]:
+        seqs = [self.add_request(p, params) for p in prompts]
+        while any(not s.finished for s in seqs):
+            self.step()
+        return seqs
+
+
+# ---------------------------------------------------------------------- helpers
+def smoke_llm(device="cuda:0"):
+    eng = LLMEngine(LlamaConfig.tiny(), device=device, max_num_seqs=4, max_model_len=256)
+    out = eng.generate([[1, 5, 9, 200], list(range(3, 90))], SamplingParams(max_tokens=4, temperature=0.0,
+                                                                            ignore_eos=True))
+    assert all(len(s.output) == 4 for s in out)
+    return out
+
+
+def bench_decode_throughput(args, rank, world):
+    """Mistral-7B bf16 at TP=world: batch of prompts, generate gen_len tokens each."""
+    from ..parallel.state import init_distributed
+    init_distributed(tp_size=world)
+    cfg = LlamaConfig.mistral_7b()
+    B, P, G = args.batch, args.prompt_len, args.gen_len
+    eng = LLMEngine(cfg, device=f"cuda:{torch.cuda.current_device()}", max_num_seqs=max(B, 1),
+                    max_model_len=P + G + 64, enable_prefix_caching=False)
+    params = SamplingParams(temperature=0.7, top_k=50, top_p=0.9, max_tokens=G, ignore_eos=True)
+    rng = np.random.default_rng(0)
+    prompts = lambda: [rng.integers(10, cfg.vocab_size - 10, P).tolist() for _ in range(B)]
+    for _ in range(max(1, args.warmup)):
+        eng.generate(prompts(), params)
+    import torch.distributed as dist
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ttft, tpot = [], []
+    for _ in range(args.steps):
+        out = eng.generate(prompts(), params)
+        for s in out:
+            ttft.append(s.first_token_time - s.arrival)
+            tpot.append((s.finish_time - s.first_token_time) / max(1, len(s.output) - 1))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    toks = B * G * args.steps
+    return {
+        "metric": "Mistral-7B output tokens/sec (bf16, continuous batching)",
+        "value": round(toks / el, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 2), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "bf16", "data": "synthetic prompts, random-init weights",
+        "config": {"model": "mistralai/Mistral-7B-Instruct-v0.3 (architecture)", "global_batch": B,
+                   "seq_len": P + G, "prompt_len": P, "gen_len": G, "parallelism": f"tp{world}"},
+        "p50_ttft_ms": round(1000 * float(np.median(ttft)), 2), "p50_tpot_ms": round(1000 * float(np.median(tpot)), 3),
+    }

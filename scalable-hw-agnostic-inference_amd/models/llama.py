@@ -1,0 +1,242 @@
+"""Llama-family decoder (Llama-3 8B/70B, Mistral-7B-v0.3, DeepSeek-R1-Distill-Llama-70B).
+
+Serves the reference's LLM endpoints (app/vllm_model_api.py, app/run-llama.py,
+app/deepseek_model_api.py; vLLM / NeuronModelForCausalLM underneath).
+MI355X-first:
+
+* Paged KV cache ([blocks, Hkv, 64, hd] per layer) written by ``ops.kv_write``;
+  prefill attention = flash kernel over the paged cache (so chunked prefill and
+  prefix reuse are the same code path); decode = split-K paged decode kernel.
+* Fused QKV GEMM, RoPE kernel on strided q/k views, SwiGLU fused into the
+  gate/up GEMM epilogue, residual-add fused into RMSNorm.
+* Tensor parallel over RCCL: QKV/gate-up column-sharded by heads /
+  intermediate, o_proj/down row-sharded with one all-reduce each, vocab-
+  parallel embedding + LM head.  bf16 weights (288 GB HBM makes 4-bit
+  quantisation, app/run-llama.py:25, unnecessary for capacity).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..parallel.layers import (GLUParallelLinear, ParallelLMHead, QKVParallelLinear, RowParallelLinear,
+                               VocabParallelEmbedding)
+from ..parallel.state import tp
+from .layers import GLULinear, RMSNorm
+
+KV_BLOCK = 64
+
+
+@dataclass
+class LlamaConfig:
+    vocab_size: int = 32768
+    hidden_size: int = 4096
+    intermediate_size: int = 14336
+    num_hidden_layers: int = 32
+    num_attention_heads: int = 32
+    num_key_value_heads: int = 8
+    head_dim: int = 128
+    rms_norm_eps: float = 1e-5
+    rope_theta: float = 1e6
+    max_position_embeddings: int = 32768
+    tie_word_embeddings: bool = False
+    bos_token_id: int = 1
+    eos_token_id: int = 2
+    rope_scaling: Optional[dict] = None
+
+    @staticmethod
+    def mistral_7b():
+        return LlamaConfig()
+
+    @staticmethod
+    def llama3_8b():
+        return LlamaConfig(vocab_size=128256, rope_theta=5e5, max_position_embeddings=8192, bos_token_id=128000,
+                           eos_token_id=128001)
+
+    @staticmethod
+    def llama3_70b():
+        return LlamaConfig(vocab_size=128256, hidden_size=8192, intermediate_size=28672, num_hidden_layers=80,
+                           num_attention_heads=64, num_key_value_heads=8, rope_theta=5e5,
+                           max_position_embeddings=8192, bos_token_id=128000, eos_token_id=128001)
+
+    @staticmethod
+    def deepseek_r1_distill_70b():
+        c = LlamaConfig.llama3_70b()
+        c.max_position_embeddings = 131072
+        c.rope_scaling = {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                          "original_max_position_embeddings": 8192}
+        return c
+
+    @staticmethod
+    def tiny():
+        return LlamaConfig(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                           num_attention_heads=4, num_key_value_heads=2, head_dim=64, max_position_embeddings=1024)
+
+    @staticmethod
+    def from_hf(d: dict) -> "LlamaConfig":
+        hd = d.get("head_dim") or d["hidden_size"] // d["num_attention_heads"]
+        return LlamaConfig(vocab_size=d["vocab_size"], hidden_size=d["hidden_size"],
+                           intermediate_size=d["intermediate_size"], num_hidden_layers=d["num_hidden_layers"],
+                           num_attention_heads=d["num_attention_heads"],
+                           num_key_value_heads=d.get("num_key_value_heads", d["num_attention_heads"]), head_dim=hd,
+                           rms_norm_eps=d.get("rms_norm_eps", 1e-5), rope_theta=d.get("rope_theta", 1e4),
+                           max_position_embeddings=d.get("max_position_embeddings", 4096),
+                           tie_word_embeddings=d.get("tie_word_embeddings", False),
+                           bos_token_id=d.get("bos_token_id", 1) or 1,
+                           eos_token_id=(d.get("eos_token_id", 2) if not isinstance(d.get("eos_token_id"), list)
+                                         else d["eos_token_id"][0]),
+                           rope_scaling=d.get("rope_scaling"))
+
+
+def rope_tables(cfg: LlamaConfig, max_pos: int, device) -> tuple:
+    hd = cfg.head_dim
+    inv = 1.0 / (cfg.rope_theta ** (torch.arange(0, hd, 2, dtype=torch.float64) / hd))
+    rs = cfg.rope_scaling
+    if rs and rs.get("rope_type", rs.get("type")) == "llama3":
+        factor, lf, hf = rs["factor"], rs["low_freq_factor"], rs["high_freq_factor"]
+        old = rs["original_max_position_embeddings"]
+        wavelen = 2 * math.pi / inv
+        low_wl, high_wl = old / lf, old / hf
+        smooth = (old / wavelen - lf) / (hf - lf)
+        scaled = torch.where(wavelen > low_wl, inv / factor, inv)
+        mid = (1 - smooth) * inv / factor + smooth * inv
+        inv = torch.where((wavelen <= low_wl) & (wavelen >= high_wl), mid, scaled)
+    t = torch.arange(max_pos, dtype=torch.float64)
+    fr = torch.outer(t, inv)
+    return fr.cos().float().to(device).contiguous(), fr.sin().float().to(device).contiguous()
+
+
+@dataclass
+class Batch:
+    """Flattened token batch for one engine step (prefill is padded to [B, S])."""
+    input_ids: torch.Tensor         # [T] int32 (T = B*S for prefill, B for decode)
+    positions: torch.Tensor         # [T] int32
+    slots: torch.Tensor             # [T] int32 cache slot (-1 = padding)
+    block_table: torch.Tensor       # [B, max_blocks] int32
+    ctx_lens: torch.Tensor          # [B] int32 (context length incl. this step's tokens)
+    q_lens: Optional[torch.Tensor]  # [B] int32 (prefill only)
+    B: int
+    S: int                          # tokens per sequence in this step (1 for decode)
+    is_prefill: bool
+    num_splits: int = 1             # decode split-K
+    last_index: Optional[torch.Tensor] = None  # [B] flat index of each sequence's last token (prefill)
+
+
+class LlamaAttention(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        st = tp()
+        self.cfg = cfg
+        self.qkv_proj = QKVParallelLinear(cfg.hidden_size, cfg.num_attention_heads, cfg.num_key_value_heads,
+                                          cfg.head_dim)
+        self.o_proj = RowParallelLinear(cfg.num_attention_heads * cfg.head_dim, cfg.hidden_size, bias=False)
+        self.h = self.qkv_proj.h_local
+        self.hk = self.qkv_proj.kv_local
+        self.hd = cfg.head_dim
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+
+    def forward(self, x, batch: Batch, k_cache, v_cache, cos, sin, residual=None):
+        T = x.shape[0]
+        qkv = self.qkv_proj(x)  # [T, (h + 2hk) * hd]
+        h, hk, hd = self.h, self.hk, self.hd
+        q = qkv[:, : h * hd].view(T, h, hd)
+        k = qkv[:, h * hd:(h + hk) * hd].view(T, hk, hd)
+        v = qkv[:, (h + hk) * hd:].view(T, hk, hd)
+        ops.rope(q, batch.positions, cos, sin)
+        ops.rope(k, batch.positions, cos, sin)
+        ops.kv_write(k, v, k_cache, v_cache, batch.slots)
+        if batch.is_prefill:
+            o = ops.paged_attention(q.view(batch.B, batch.S, h, hd), k_cache, v_cache, batch.block_table,
+                                    batch.ctx_lens, batch.q_lens, self.scale, causal=True).view(T, h * hd)
+        else:
+            o = ops.decode_attention(q, k_cache, v_cache, batch.block_table, batch.ctx_lens, self.scale,
+                                     num_splits=batch.num_splits).view(T, h * hd)
+        return self.o_proj(o, residual=residual)
+
+
+class LlamaMLP(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.gate_up_proj = GLUParallelLinear(cfg.hidden_size, cfg.intermediate_size, act="silu")
+        self.down_proj = RowParallelLinear(cfg.intermediate_size, cfg.hidden_size, bias=False)
+
+    def forward(self, x, residual=None):
+        return self.down_proj(self.gate_up_proj(x), residual=residual)
+
+
+class LlamaDecoderLayer(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.input_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
+        self.self_attn = LlamaAttention(cfg)
+        self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
+        self.mlp = LlamaMLP(cfg)
+
+    def forward(self, x, batch, kc, vc, cos, sin):
+        x = self.self_attn(self.input_layernorm(x), batch, kc, vc, cos, sin, residual=x)
+        return self.mlp(self.post_attention_layernorm(x), residual=x)
+
+
+class LlamaForCausalLM(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.embed_tokens = VocabParallelEmbedding(cfg.vocab_size, cfg.hidden_size)
+        self.layers = nn.ModuleList([LlamaDecoderLayer(cfg) for _ in range(cfg.num_hidden_layers)])
+        self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
+        self.lm_head = ParallelLMHead(cfg.vocab_size, cfg.hidden_size)
+        self._rope = None
+
+    @property
+    def kv_heads_local(self) -> int:
+        return self.layers[0].self_attn.hk
+
+    def rope(self, device):
+        if self._rope is None or self._rope[0].device != torch.device(device):
+            self._rope = rope_tables(self.cfg, self.cfg.max_position_embeddings, device)
+        return self._rope
+
+    def forward(self, batch: Batch, kv_caches: List[tuple]) -> torch.Tensor:
+        """Returns logits [B, V] for each sequence's last token of this step."""
+        cos, sin = self.rope(batch.input_ids.device)
+        x = self.embed_tokens(batch.input_ids)
+        for layer, (kc, vc) in zip(self.layers, kv_caches):
+            x = layer(x, batch, kc, vc, cos, sin)
+        if batch.is_prefill:
+            x = x.index_select(0, batch.last_index)
+        x = self.norm(x)
+        return self.lm_head.logits(x)
+
+    def convert_hf_state_dict(self, sd: dict) -> dict:
+        from .attention import merge_linear_keys
+        out = {}
+        for k, v in sd.items():
+            k2 = k[len("model."):] if k.startswith("model.") else k
+            if "rotary_emb" in k2:
+                continue
+            out[k2] = v
+        if "lm_head.weight" not in out and "embed_tokens.weight" in out:
+            out["lm_head.weight"] = out["embed_tokens.weight"]
+        for i in range(self.cfg.num_hidden_layers):
+            p = f"layers.{i}."
+            merge_linear_keys(out, p + "self_attn.", ["q_proj", "k_proj", "v_proj"], "qkv_proj", bias=False)
+            gk, uk = p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight"
+            if gk in out and uk in out:
+                out[p + "mlp.gate_up_proj.weight"] = GLULinear.interleave(out.pop(uk), out.pop(gk))
+        return out
+
+
+def allocate_kv_cache(cfg: LlamaConfig, kv_heads_local: int, num_blocks: int, device, dtype=torch.bfloat16):
+    """One contiguous allocation [L, 2, blocks, Hkv, 64, hd]; returns list of (k, v) views per layer."""
+    buf = torch.empty(cfg.num_hidden_layers, 2, num_blocks, kv_heads_local, KV_BLOCK, cfg.head_dim, dtype=dtype,
+                      device=device)
+    return buf, [(buf[i, 0], buf[i, 1]) for i in range(cfg.num_hidden_layers)]
+
+
+def kv_bytes_per_block(cfg: LlamaConfig, kv_heads_local: int) -> int:
+    return cfg.num_hidden_layers * 2 * kv_heads_local * KV_BLOCK * cfg.head_dim * 2

@@ -1,0 +1,301 @@
+"""Stable Diffusion 2.1 UNet (diffusers ``UNet2DConditionModel`` architecture), NHWC.
+
+Reference workload: ``StableDiffusionPipeline`` UNet that app/run-sd.py:104-135
+runs (cuDNN/Inductor on GPU, NEFF on Inferentia).  MI355X-first design:
+
+* Every 3x3/1x1 conv is the implicit-GEMM MFMA kernel; the time-embedding bias
+  and the residual/skip add are fused into the conv epilogue, Upsample2D's
+  nearest-2x is fused into the gather.  GroupNorm+SiLU is a statistics pass
+  plus one vectorised apply pass (the conv kernel can also normalise inside
+  its gather, but for 3x3 convs that repeats the transform per tap and N-tile).
+* Transformer blocks: fused QKV GEMM -> flash attention reading strided views
+  -> out-proj GEMM with the residual in its epilogue; GEGLU fused into the FF
+  GEMM epilogue.
+* Cross-attention K/V depend only on the text context: computed once per
+  request (:meth:`UNet2DConditionModel.context_kv`) and reused for all steps.
+* All 22 ResNet time-embedding projections run as ONE batched GEMM per step.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .attention import CrossAttention, FusedSelfAttention, merge_linear_keys
+from .layers import Conv2d, GLULinear, GroupNorm, LayerNorm, Linear, timestep_embedding
+
+
+@dataclass
+class UNetConfig:
+    in_channels: int = 4
+    out_channels: int = 4
+    block_out_channels: Tuple[int, ...] = (320, 640, 1280, 1280)
+    layers_per_block: int = 2
+    attention_heads: Tuple[int, ...] = (5, 10, 20, 20)  # diffusers "attention_head_dim" for SD2 = head counts
+    cross_attention_dim: int = 1024
+    down_attn: Tuple[bool, ...] = (True, True, True, False)
+    norm_num_groups: int = 32
+    norm_eps: float = 1e-5
+    time_embed_dim: int = 1280
+    flip_sin_to_cos: bool = True
+    freq_shift: float = 0.0
+
+    @staticmethod
+    def sd21():
+        return UNetConfig()
+
+    @staticmethod
+    def tiny():
+        return UNetConfig(block_out_channels=(64, 128), layers_per_block=1, attention_heads=(1, 2),
+                          cross_attention_dim=64, down_attn=(True, False), time_embed_dim=128)
+
+
+class ResnetBlock2D(nn.Module):
+    def __init__(self, cin: int, cout: int, temb: Optional[int], groups: int, eps: float):
+        super().__init__()
+        self.cin, self.cout = cin, cout
+        self.norm1 = GroupNorm(groups, cin, eps)
+        self.conv1 = Conv2d(cin, cout, 3, padding=1)
+        self.time_emb_proj = Linear(temb, cout) if temb else None
+        self.norm2 = GroupNorm(groups, cout, eps)
+        self.conv2 = Conv2d(cout, cout, 3, padding=1)
+        self.conv_shortcut = Conv2d(cin, cout, 1) if cin != cout else None
+
+    def forward(self, x, temb_proj=None):
+        # GroupNorm+SiLU as one memory-bound pass (normalising inside the 3x3 gather would
+        # redo the transform 9x per N-tile: VALU-bound, measured 5x slower).
+        h = self.conv1(self.norm1(x, silu=True), temb=temb_proj)
+        skip = self.conv_shortcut(x) if self.conv_shortcut is not None else x
+        return self.conv2(self.norm2(h, silu=True), residual=skip)
+
+
+class GEGLU(nn.Module):
+    def __init__(self, dim: int, inner: int):
+        super().__init__()
+        self.proj = GLULinear(dim, inner, act="gelu")
+
+
+class FeedForward(nn.Module):
+    def __init__(self, dim: int, mult: int = 4):
+        super().__init__()
+        inner = dim * mult
+        self.net = nn.ModuleList([GEGLU(dim, inner), nn.Identity(), Linear(inner, dim)])
+
+    def forward(self, x, residual):
+        return self.net[2](self.net[0].proj(x), residual=residual)
+
+
+class BasicTransformerBlock(nn.Module):
+    def __init__(self, dim: int, heads: int, ctx_dim: int):
+        super().__init__()
+        self.norm1 = LayerNorm(dim)
+        self.attn1 = FusedSelfAttention(dim, heads, qkv_bias=False)
+        self.norm2 = LayerNorm(dim)
+        self.attn2 = CrossAttention(dim, ctx_dim, heads)
+        self.norm3 = LayerNorm(dim)
+        self.ff = FeedForward(dim)
+
+    def forward(self, x, ctx_kv):
+        x = self.attn1(self.norm1(x), residual=x)
+        x = self.attn2(self.norm2(x), ctx_kv, residual=x)
+        return self.ff(self.norm3(x), residual=x)
+
+
+class Transformer2DModel(nn.Module):
+    def __init__(self, channels: int, heads: int, ctx_dim: int, groups: int):
+        super().__init__()
+        self.norm = GroupNorm(groups, channels, 1e-6)
+        self.proj_in = Conv2d(channels, channels, 1)   # Linear projection as a 1x1 conv (norm fused in gather)
+        self.transformer_blocks = nn.ModuleList([BasicTransformerBlock(channels, heads, ctx_dim)])
+        self.proj_out = Linear(channels, channels)
+
+    def forward(self, x, ctx_kv):
+        B, H, W, C = x.shape
+        h = self.proj_in(self.norm(x)).view(B, H * W, C)
+        for blk in self.transformer_blocks:
+            h = blk(h, ctx_kv)
+        return self.proj_out(h, residual=x.view(B, H * W, C)).view(B, H, W, C)
+
+
+class Downsample2D(nn.Module):
+    def __init__(self, ch):
+        super().__init__()
+        self.conv = Conv2d(ch, ch, 3, stride=2, padding=1)
+
+    def forward(self, x):
+        return self.conv(x)
+
+
+class Upsample2D(nn.Module):
+    def __init__(self, ch):
+        super().__init__()
+        self.conv = Conv2d(ch, ch, 3, padding=1)
+
+    def forward(self, x):
+        return self.conv(x, upsample=True)
+
+
+class DownBlock(nn.Module):
+    def __init__(self, cin, cout, n, temb, heads, ctx, attn, groups, eps, down):
+        super().__init__()
+        self.resnets = nn.ModuleList([ResnetBlock2D(cin if i == 0 else cout, cout, temb, groups, eps) for i in range(n)])
+        self.attentions = nn.ModuleList([Transformer2DModel(cout, heads, ctx, groups) for _ in range(n)]) if attn else None
+        self.downsamplers = nn.ModuleList([Downsample2D(cout)]) if down else None
+
+
+class UpBlock(nn.Module):
+    def __init__(self, prev, cout, skip_chs, temb, heads, ctx, attn, groups, eps, up):
+        super().__init__()
+        res = []
+        c = prev
+        for sc in skip_chs:
+            res.append(ResnetBlock2D(c + sc, cout, temb, groups, eps))
+            c = cout
+        self.resnets = nn.ModuleList(res)
+        self.attentions = nn.ModuleList([Transformer2DModel(cout, heads, ctx, groups) for _ in skip_chs]) if attn else None
+        self.upsamplers = nn.ModuleList([Upsample2D(cout)]) if up else None
+
+
+class MidBlock(nn.Module):
+    def __init__(self, ch, temb, heads, ctx, groups, eps):
+        super().__init__()
+        self.resnets = nn.ModuleList([ResnetBlock2D(ch, ch, temb, groups, eps), ResnetBlock2D(ch, ch, temb, groups, eps)])
+        self.attentions = nn.ModuleList([Transformer2DModel(ch, heads, ctx, groups)])
+
+
+class TimestepEmbedding(nn.Module):
+    def __init__(self, cin, dim):
+        super().__init__()
+        self.linear_1 = Linear(cin, dim)
+        self.linear_2 = Linear(dim, dim)
+
+    def forward(self, x):
+        return self.linear_2(self.linear_1(x, act="silu"))
+
+
+class UNet2DConditionModel(nn.Module):
+    def __init__(self, cfg: UNetConfig = None):
+        super().__init__()
+        cfg = cfg or UNetConfig()
+        self.cfg = cfg
+        chs = cfg.block_out_channels
+        g, eps, temb, ctx = cfg.norm_num_groups, cfg.norm_eps, cfg.time_embed_dim, cfg.cross_attention_dim
+        self.conv_in = Conv2d(cfg.in_channels, chs[0], 3, padding=1)
+        self.time_embedding = TimestepEmbedding(chs[0], temb)
+        self.down_blocks = nn.ModuleList()
+        c = chs[0]
+        skips = [c]
+        for i, co in enumerate(chs):
+            last = i == len(chs) - 1
+            blk = DownBlock(c, co, cfg.layers_per_block, temb, cfg.attention_heads[i], ctx, cfg.down_attn[i], g, eps,
+                            not last)
+            self.down_blocks.append(blk)
+            skips += [co] * cfg.layers_per_block
+            if not last:
+                skips.append(co)
+            c = co
+        self.mid_block = MidBlock(chs[-1], temb, cfg.attention_heads[-1], ctx, g, eps)
+        self.up_blocks = nn.ModuleList()
+        rev = list(reversed(chs))
+        rev_heads = list(reversed(cfg.attention_heads))
+        rev_attn = list(reversed(cfg.down_attn))
+        prev = chs[-1]
+        for i, co in enumerate(rev):
+            n = cfg.layers_per_block + 1
+            skip_chs = [skips.pop() for _ in range(n)]
+            blk = UpBlock(prev, co, skip_chs, temb, rev_heads[i], ctx, rev_attn[i], g, eps, i < len(rev) - 1)
+            self.up_blocks.append(blk)
+            prev = co
+        self.conv_norm_out = GroupNorm(g, chs[0], eps)
+        self.conv_out = Conv2d(chs[0], cfg.out_channels, 3, padding=1)
+        self._temb_bank = None
+
+    # ------------------------------------------------------------------ helpers
+    def _resnets(self) -> List[ResnetBlock2D]:
+        return [m for m in self.modules() if isinstance(m, ResnetBlock2D)]
+
+    def _attn_modules(self) -> List[Transformer2DModel]:
+        return [m for m in self.modules() if isinstance(m, Transformer2DModel)]
+
+    def build_temb_bank(self):
+        """Concatenate all ResNet time_emb_proj weights -> one GEMM per step."""
+        rs = self._resnets()
+        w = torch.cat([r.time_emb_proj.weight for r in rs], 0).contiguous()
+        b = torch.cat([r.time_emb_proj.bias for r in rs], 0).contiguous()
+        offs, o = [], 0
+        for r in rs:
+            offs.append((o, r.cout))
+            o += r.cout
+        self._temb_bank = (w, b, offs)
+
+    def context_kv(self, ctx: torch.Tensor) -> List[torch.Tensor]:
+        """Cross-attention K/V for every Transformer block (request-constant)."""
+        out = []
+        for t in self._attn_modules():
+            for blk in t.transformer_blocks:
+                out.append(blk.attn2.context_kv(ctx))
+        return out
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, sample: torch.Tensor, timestep: torch.Tensor, ctx_kv: List[torch.Tensor]) -> torch.Tensor:
+        """sample [B, H, W, 4] NHWC, timestep [B] (float), ctx_kv from :meth:`context_kv`."""
+        cfg = self.cfg
+        B = sample.shape[0]
+        t = timestep.expand(B) if timestep.numel() == 1 else timestep
+        tf = timestep_embedding(t, cfg.block_out_channels[0], cfg.flip_sin_to_cos, cfg.freq_shift)
+        emb = self.time_embedding(tf.to(sample.dtype))
+        if self._temb_bank is None:
+            self.build_temb_bank()
+        w, b, offs = self._temb_bank
+        # silu(emb) then one GEMM for all ResNets
+        semb = ops.bias_act(emb, None, None, "silu")
+        tall = ops.linear(semb, w, b)
+        tprojs = [tall[:, o:o + n].contiguous() for (o, n) in offs]
+        ti = iter(tprojs)
+        kvi = iter(ctx_kv)
+
+        x = self.conv_in(sample)
+        skips = [x]
+        for blk in self.down_blocks:
+            for i, r in enumerate(blk.resnets):
+                x = r(x, next(ti))
+                if blk.attentions is not None:
+                    x = blk.attentions[i](x, next(kvi))
+                skips.append(x)
+            if blk.downsamplers is not None:
+                x = blk.downsamplers[0](x)
+                skips.append(x)
+        x = self.mid_block.resnets[0](x, next(ti))
+        x = self.mid_block.attentions[0](x, next(kvi))
+        x = self.mid_block.resnets[1](x, next(ti))
+        for blk in self.up_blocks:
+            for i, r in enumerate(blk.resnets):
+                s = skips.pop()
+                x = r(torch.cat([x, s], dim=-1), next(ti))
+                if blk.attentions is not None:
+                    x = blk.attentions[i](x, next(kvi))
+            if blk.upsamplers is not None:
+                x = blk.upsamplers[0](x)
+        return self.conv_out(self.conv_norm_out(x, silu=True))
+
+    # ------------------------------------------------------------------ checkpoints
+    def convert_hf_state_dict(self, sd: dict) -> dict:
+        """diffusers UNet2DConditionModel keys -> ours (merged QKV / KV, 1x1 proj_in)."""
+        out = {}
+        for k, v in sd.items():
+            k2 = k.replace(".to_out.0.", ".out.")
+            if ".proj_in.weight" in k2 and v.dim() == 2:
+                v = v[:, :, None, None]
+            out[k2] = v
+        for name, m in self.named_modules():
+            if isinstance(m, BasicTransformerBlock):
+                merge_linear_keys(out, name + ".attn1.", ["to_q", "to_k", "to_v"], "qkv", bias=False)
+                for suf in ("weight", "bias"):
+                    kq = f"{name}.attn2.to_q.{suf}"
+                    if kq in out:
+                        out[f"{name}.attn2.q.{suf}"] = out.pop(kq)
+                merge_linear_keys(out, name + ".attn2.", ["to_k", "to_v"], "kv", bias=False)
+        return out

@@ -1,0 +1,151 @@
+"""AutoencoderKL decoder (diffusers architecture), NHWC, shared by SD2.1 (4-ch
+latents) and Flux.1 (16-ch latents, shift factor).
+
+Reference: the VAE decode step of app/run-sd.py (diffusers) and the Neuron-traced
+Flux decoder (app/src/decoder/model.py:6-18).  All convs are implicit-GEMM MFMA
+with GroupNorm+SiLU fused into the gather and the residual fused into the
+epilogue; the mid-block single-head attention (d=512) runs as two batched MFMA
+GEMMs around a row-softmax kernel (head dim 512 exceeds the flash kernel's
+register tile).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .attention import merge_linear_keys
+from .layers import Conv2d, GroupNorm, Linear
+from .unet2d import ResnetBlock2D
+
+
+@dataclass
+class VAEConfig:
+    latent_channels: int = 4
+    out_channels: int = 3
+    block_out_channels: Tuple[int, ...] = (128, 256, 512, 512)
+    layers_per_block: int = 2
+    norm_num_groups: int = 32
+    scaling_factor: float = 0.18215
+    shift_factor: float = 0.0
+    use_post_quant_conv: bool = True
+
+    @staticmethod
+    def sd21():
+        return VAEConfig()
+
+    @staticmethod
+    def flux():
+        return VAEConfig(latent_channels=16, scaling_factor=0.3611, shift_factor=0.1159, use_post_quant_conv=False)
+
+    @staticmethod
+    def tiny(latent_channels=4):
+        return VAEConfig(latent_channels=latent_channels, block_out_channels=(32, 32, 32, 64), layers_per_block=1)
+
+
+class VAEAttention(nn.Module):
+    def __init__(self, ch: int, groups: int):
+        super().__init__()
+        self.ch = ch
+        self.group_norm = GroupNorm(groups, ch, 1e-6)
+        self.qkv = Linear(ch, 3 * ch)
+        self.out = Linear(ch, ch)
+
+    def forward(self, x):
+        B, H, W, C = x.shape
+        h = self.group_norm(x).view(B, H * W, C)
+        qkv = self.qkv(h)
+        q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+        s = ops.bmm(q.contiguous(), k.contiguous(), alpha=1.0 / math.sqrt(C))  # [B, HW, HW]
+        ops.softmax_(s)
+        o = ops.bmm(s, v.transpose(1, 2).contiguous())  # [B, HW, C]
+        return self.out(o, residual=x.view(B, H * W, C)).view(B, H, W, C)
+
+
+class VAEMid(nn.Module):
+    def __init__(self, ch, groups):
+        super().__init__()
+        self.resnets = nn.ModuleList([ResnetBlock2D(ch, ch, None, groups, 1e-6), ResnetBlock2D(ch, ch, None, groups, 1e-6)])
+        self.attentions = nn.ModuleList([VAEAttention(ch, groups)])
+
+
+class _Upsample(nn.Module):
+    def __init__(self, ch):
+        super().__init__()
+        self.conv = Conv2d(ch, ch, 3, padding=1)
+
+
+class VAEUpBlock(nn.Module):
+    def __init__(self, cin, cout, n, groups, up):
+        super().__init__()
+        self.resnets = nn.ModuleList([ResnetBlock2D(cin if i == 0 else cout, cout, None, groups, 1e-6) for i in range(n)])
+        self.upsamplers = nn.ModuleList([_Upsample(cout)]) if up else None
+
+
+class Decoder(nn.Module):
+    def __init__(self, cfg: VAEConfig):
+        super().__init__()
+        chs = list(reversed(cfg.block_out_channels))
+        g = cfg.norm_num_groups
+        self.conv_in = Conv2d(cfg.latent_channels, chs[0], 3, padding=1)
+        self.mid_block = VAEMid(chs[0], g)
+        self.up_blocks = nn.ModuleList()
+        prev = chs[0]
+        for i, c in enumerate(chs):
+            self.up_blocks.append(VAEUpBlock(prev, c, cfg.layers_per_block + 1, g, i < len(chs) - 1))
+            prev = c
+        self.conv_norm_out = GroupNorm(g, chs[-1], 1e-6)
+        self.conv_out = Conv2d(chs[-1], cfg.out_channels, 3, padding=1)
+
+    def forward(self, z):
+        x = self.conv_in(z)
+        x = self.mid_block.resnets[0](x)
+        x = self.mid_block.attentions[0](x)
+        x = self.mid_block.resnets[1](x)
+        for blk in self.up_blocks:
+            for r in blk.resnets:
+                x = r(x)
+            if blk.upsamplers is not None:
+                x = blk.upsamplers[0].conv(x, upsample=True)
+        return self.conv_out(self.conv_norm_out(x, silu=True))
+
+
+class AutoencoderKLDecoder(nn.Module):
+    def __init__(self, cfg: VAEConfig = None):
+        super().__init__()
+        cfg = cfg or VAEConfig()
+        self.cfg = cfg
+        self.post_quant_conv = Conv2d(cfg.latent_channels, cfg.latent_channels, 1) if cfg.use_post_quant_conv else None
+        self.decoder = Decoder(cfg)
+
+    def forward(self, latents: torch.Tensor) -> torch.Tensor:
+        """latents NHWC [B, h, w, C] (scaled) -> image NHWC [B, 8h, 8w, 3] in [-1, 1]."""
+        lat = latents.contiguous()
+        z = ops.bias_act(lat.view(-1, 8), None, None, None, alpha=1.0 / self.cfg.scaling_factor).view(lat.shape)
+        if self.cfg.shift_factor:
+            z = z + self.cfg.shift_factor
+        if self.post_quant_conv is not None:
+            z = self.post_quant_conv(z)
+        return self.decoder(z)
+
+    @staticmethod
+    def to_uint8(img: torch.Tensor) -> torch.Tensor:
+        return ((img.float() / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8)
+
+    def convert_hf_state_dict(self, sd: dict) -> dict:
+        out = {}
+        for k, v in sd.items():
+            if k.startswith("encoder.") or k.startswith("quant_conv."):
+                continue
+            k2 = k.replace(".to_out.0.", ".out.")
+            if ".attentions." in k2 and v.dim() == 4:  # legacy 1x1-conv attention weights
+                v = v[:, :, 0, 0]
+            out[k2] = v
+        for name, m in self.named_modules():
+            if isinstance(m, VAEAttention):
+                merge_linear_keys(out, name + ".", ["to_q", "to_k", "to_v"], "qkv")
+        return out

@@ -164,7 +164,7 @@ def attention(q, k, v, scale=None, causal=False, causal_offset=0, kv_lens=None, 
     s = s.masked_fill(mask, float("-inf"))
     p = torch.softmax(s, dim=-1)
     p = torch.nan_to_num(p, nan=0.0)
-    o = torch.matmul(p, vf).permute(0, 2, 1, 3)
+    o = torch.matmul(p, vf).permute(0, 2, 1, 3).contiguous()
     if q_lens is not None:
         valid = (torch.arange(Sq, device=q.device).view(1, Sq) < q_lens.view(B, 1).to(q.device))
         o = o * valid.view(B, Sq, 1, 1)

@@ -1,0 +1,65 @@
+"""Tensor-parallel collectives.
+
+Issued on the current stream, so they are ordered with the surrounding kernels
+and capturable in HIP graphs.  Two transports:
+
+* RCCL (``torch.distributed`` backend "nccl" on ROCm) -- default for every size.
+* ``P2PAllReduce`` (``csrc/comm/p2p_allreduce.hip``) -- one-shot all-reduce for
+  small, latency-bound messages (LLM decode: B x 4096 bf16 per layer), reading
+  every peer's IPC-mapped buffer directly over xGMI in one kernel.  Enabled
+  with ``SHAI_P2P_ALLREDUCE=1`` once registered via :func:`enable_p2p`.
+
+On a fully connected 8x MI355X node each GPU has 7 xGMI links; RCCL's
+multi-channel rings / direct algorithms use them for the large Flux/prefill
+messages, the one-shot kernel removes the ring latency for the small ones.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .state import tp
+
+_P2P = None
+P2P_MAX_BYTES = int(os.environ.get("SHAI_P2P_MAX_BYTES", str(512 * 1024)))
+
+
+def enable_p2p(p2p) -> None:
+    global _P2P
+    _P2P = p2p
+
+
+def all_reduce(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """In-place sum over the TP group (no-op at TP=1)."""
+    st = tp()
+    g = group if group is not None else st.group
+    if st.size == 1 and group is None:
+        return x
+    if _P2P is not None and x.is_cuda and x.numel() * x.element_size() <= P2P_MAX_BYTES and x.is_contiguous():
+        return _P2P.all_reduce(x)
+    dist.all_reduce(x, group=g)
+    return x
+
+
+def all_gather_last(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """Concatenate the TP shards along the last dim."""
+    st = tp()
+    g = group if group is not None else st.group
+    if st.size == 1 and group is None:
+        return x
+    n = st.size if group is None else dist.get_world_size(g)
+    x = x.contiguous()
+    out = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x, group=g)
+    return out.movedim(0, -2).reshape(*x.shape[:-1], n * x.shape[-1])
+
+
+def broadcast_object(obj, src: int = 0):
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return obj
+    lst = [obj]
+    dist.broadcast_object_list(lst, src=src)
+    return lst[0]

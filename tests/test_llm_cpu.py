@@ -1,0 +1,91 @@
+"""LLM engine on CPU (fp32 reference ops): HF transformers parity with the same
+weights, paged-KV / prefix-cache / continuous-batching behaviour, native
+block manager and scheduler helpers."""
+import numpy as np
+import pytest
+import torch
+
+from shai_amd.engines.llm import LLMEngine, SamplingParams, sample
+from shai_amd.models.llama import LlamaConfig
+from shai_amd.weights import load_into
+
+
+def _hf_tiny():
+    transformers = pytest.importorskip("transformers")
+    c = LlamaConfig.tiny()
+    hc = transformers.LlamaConfig(vocab_size=c.vocab_size, hidden_size=c.hidden_size,
+                                  intermediate_size=c.intermediate_size, num_hidden_layers=c.num_hidden_layers,
+                                  num_attention_heads=c.num_attention_heads, num_key_value_heads=c.num_key_value_heads,
+                                  head_dim=c.head_dim, rms_norm_eps=c.rms_norm_eps, rope_theta=c.rope_theta,
+                                  max_position_embeddings=c.max_position_embeddings, tie_word_embeddings=False)
+    torch.manual_seed(0)
+    m = transformers.LlamaForCausalLM(hc).eval()
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(p.to(torch.bfloat16).float())  # bf16-representable weights
+    return c, m
+
+
+def test_llama_matches_transformers():
+    c, hf = _hf_tiny()
+    eng = LLMEngine(c, device="cpu", max_num_seqs=2, max_model_len=256, enable_prefix_caching=False)
+    load_into(eng.model, {k: v.clone() for k, v in hf.state_dict().items()}, eng.model.convert_hf_state_dict,
+              strict=True)
+    prompt = [3, 17, 99, 250, 7, 7, 400, 12]
+    with torch.no_grad():
+        ref = hf(torch.tensor([prompt])).logits[0, -1].float()
+    seq = eng.add_request(prompt, SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True))
+    # capture the prefill logits through the model directly
+    from shai_amd.runtime import build_prefill
+    eng.step()
+    assert seq.finished and seq.output[0] == int(ref.argmax())
+    # greedy continuation equals HF greedy generate
+    out = eng.generate([prompt], SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True))[0].output
+    with torch.no_grad():
+        g = hf.generate(torch.tensor([prompt]), max_new_tokens=6, do_sample=False)[0, len(prompt):].tolist()
+    assert out[:3] == g[:3]
+
+
+def test_continuous_batching_and_prefix_cache():
+    eng = LLMEngine(LlamaConfig.tiny(), device="cpu", max_num_seqs=3, max_model_len=512)
+    p = SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True)
+    long = list(range(5, 205))
+    a = eng.generate([long], p)[0].output
+    hits0 = eng.stats["prefix_hit_tokens"]
+    b = eng.generate([long], p)[0].output
+    assert eng.stats["prefix_hit_tokens"] - hits0 == 192  # 3 full 64-token blocks reused
+    assert a == b
+    # more requests than max_num_seqs -> queued and completed
+    outs = eng.generate([[i + 3, i + 9, 11] for i in range(7)], p)
+    assert all(len(s.output) == 4 and s.finished for s in outs)
+    assert eng.bm.num_free == eng.num_kv_blocks
+
+
+def test_block_manager_native():
+    from shai_amd.runtime import BlockManager, build_decode, build_prefill, sched_admit
+    bm = BlockManager(8)
+    a = bm.allocate(3)
+    assert len(set(a)) == 3 and bm.num_free == 5
+    bm.register(a[0], 123)
+    bm.release(a)
+    assert bm.num_free == 8
+    got = bm.lookup_prefix([123, 456])
+    assert got == [a[0]] and bm.refcount(a[0]) == 1
+    with pytest.raises(MemoryError):
+        bm.allocate(8)
+    assert sched_admit([100, 100, 5000], free_blocks=10, running=0, max_seqs=8, token_budget=4096,
+                       watermark_blocks=1) == 2
+    pos, slots, lens, bt = build_decode([70, 3], [[4, 5], [9]], 4)
+    assert pos.tolist() == [70, 3] and slots.tolist() == [5 * 64 + 6, 9 * 64 + 3] and lens.tolist() == [71, 4]
+    pos, slots, lens, ql, bt, last = build_prefill([64, 0], [2, 3], [[1, 2], [3]], 3, 2)
+    assert slots.tolist() == [2 * 64, 2 * 64 + 1, -1, 3 * 64, 3 * 64 + 1, 3 * 64 + 2]
+    assert last.tolist() == [1, 5] and lens.tolist() == [66, 3]
+
+
+def test_sampling():
+    logits = torch.full((3, 100), -10.0)
+    logits[:, 42] = 10.0
+    logits[1, 7] = 9.0
+    t = torch.tensor([0.0, 1.0, 0.7])
+    out = sample(logits, t, torch.tensor([50, 1, 0]), torch.tensor([0.9, 0.9, 1.0]))
+    assert out.tolist()[0] == 42 and out.tolist()[1] == 42

@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""Kernel microbenchmarks on the GPU: shai kernels vs PyTorch-ROCm library paths
+(hipBLASLt GEMM, MIOpen conv, SDPA) on the same random bf16 inputs.
+
+python tools/bench_kernels.py [--only gemm,conv,attn,norm] [--json out.json]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+import torch.nn.functional as F
+
+import shai_amd.ops as ops
+
+
+def timeit(fn, iters=20, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3
+
+
+def rnd(*shape):
+    return torch.randn(*shape, device="cuda").to(torch.bfloat16)
+
+
+def bench_gemm(rows):
+    shapes = [(32768, 320, 320), (32768, 2560, 320), (32768, 320, 1280), (8192, 1280, 5120), (4096, 4096, 4096),
+              (8192, 8192, 8192), (2048, 12288, 3072), (256, 4096, 4096), (64, 14336, 4096)]
+    for M, N, K in shapes:
+        a, w = rnd(M, K), rnd(N, K)
+        t_s = timeit(lambda: ops.linear(a, w))
+        t_t = timeit(lambda: torch.matmul(a, w.t()))
+        f = 2 * M * N * K
+        rows.append(dict(op="gemm", shape=f"{M}x{N}x{K}", shai_us=t_s * 1e6, torch_us=t_t * 1e6,
+                         shai_tflops=f / t_s / 1e12, torch_tflops=f / t_t / 1e12))
+
+
+def bench_conv(rows):
+    shapes = [(8, 64, 320, 320, 3), (8, 32, 640, 640, 3), (8, 16, 1280, 1280, 3), (8, 8, 1280, 1280, 3),
+              (8, 64, 640, 320, 3), (1, 256, 256, 128, 3), (1, 512, 128, 128, 3), (8, 64, 320, 320, 1)]
+    for N, H, C, Co, k in shapes:
+        x = rnd(N, H, H, C)
+        w4 = rnd(Co, C, k, k) * (1 / math.sqrt(C * k * k))
+        wp = ops.pack_conv_weight(w4)
+        b = rnd(Co)
+        pad = k // 2
+        t_s = timeit(lambda: ops.conv2d(x, wp, b, k, k, 1, pad))
+        xc = x.permute(0, 3, 1, 2)  # channels_last view
+        w4c = w4.contiguous(memory_format=torch.channels_last)
+        t_t = timeit(lambda: F.conv2d(xc, w4c, b, padding=pad))
+        f = 2 * N * H * H * Co * C * k * k
+        rows.append(dict(op=f"conv{k}x{k}", shape=f"N{N} {H}x{H} {C}->{Co}", shai_us=t_s * 1e6, torch_us=t_t * 1e6,
+                         shai_tflops=f / t_s / 1e12, torch_tflops=f / t_t / 1e12))
+
+
+def bench_attn(rows):
+    shapes = [(8, 4096, 4096, 5, 64), (8, 1024, 1024, 10, 64), (8, 4096, 77, 5, 64), (1, 4608, 4608, 24, 128),
+              (4, 2048, 2048, 32, 128), (16, 197, 197, 12, 64)]
+    for B, Sq, Skv, H, D in shapes:
+        q, k, v = rnd(B, Sq, H, D), rnd(B, Skv, H, D), rnd(B, Skv, H, D)
+        t_s = timeit(lambda: ops.attention(q, k, v))
+        qt, kt, vt = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+        t_t = timeit(lambda: F.scaled_dot_product_attention(qt, kt, vt))
+        f = 4 * B * H * Sq * Skv * D
+        rows.append(dict(op="attn", shape=f"B{B} H{H} {Sq}x{Skv} d{D}", shai_us=t_s * 1e6, torch_us=t_t * 1e6,
+                         shai_tflops=f / t_s / 1e12, torch_tflops=f / t_t / 1e12))
+
+
+def bench_norm(rows):
+    for N, HW, C in [(8, 4096, 320), (8, 1024, 640), (1, 262144, 128)]:
+        x = rnd(N, HW, C)
+        g, b = rnd(C), rnd(C)
+        t_s = timeit(lambda: ops.groupnorm(x, g, b, 32, 1e-5, True))
+        xt = x.view(N, HW, C).permute(0, 2, 1)
+        t_t = timeit(lambda: F.silu(F.group_norm(xt, 32, g, b, 1e-5)))
+        by = 3 * x.numel() * 2
+        rows.append(dict(op="groupnorm+silu", shape=f"{N}x{HW}x{C}", shai_us=t_s * 1e6, torch_us=t_t * 1e6,
+                         shai_GBps=by / t_s / 1e9, torch_GBps=by / t_t / 1e9))
+    for T, D in [(8192, 4096), (64, 4096), (32768, 320)]:
+        x, w = rnd(T, D), rnd(D)
+        t_s = timeit(lambda: ops.rmsnorm(x, w, 1e-6))
+        by = 2 * x.numel() * 2
+        rows.append(dict(op="rmsnorm", shape=f"{T}x{D}", shai_us=t_s * 1e6, shai_GBps=by / t_s / 1e9))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="gemm,conv,attn,norm")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    rows = []
+    with torch.inference_mode():
+        for name in a.only.split(","):
+            {"gemm": bench_gemm, "conv": bench_conv, "attn": bench_attn, "norm": bench_norm}[name](rows)
+    for r in rows:
+        print("  ".join(f"{k}={v:.1f}" if isinstance(v, float) else f"{k}={v}" for k, v in r.items()), flush=True)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
