@@ -7,6 +7,13 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <cstdio>
+#include <cstdlib>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
 #include "kernels/launchers.h"
 
 using at::Tensor;
@@ -17,6 +24,130 @@ namespace {
 #define SHAI_CHECK(cond, ...) TORCH_CHECK(cond, "shai: ", __VA_ARGS__)
 
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+// v2 GEMM (LDS-DMA) unless the problem needs v1 features (fused GN gather) or
+// exceeds the 2 GiB buffer-descriptor range.  SHAI_GEMM_V1=1 forces v1.
+bool use_v2(const shai::GemmArgs& g, long a_bytes, long w_bytes, long a2_bytes) {
+  static const bool force_v1 = getenv("SHAI_GEMM_V1") != nullptr;
+  if (force_v1 || g.in_scale != nullptr) return false;
+  const long lim = 0x7fffffffL - 64;
+  if (a_bytes > lim || w_bytes > lim || a2_bytes > lim) return false;
+  if (g.conv && g.A2 != nullptr && (g.Cin % 64 != 0 || g.Cin1 % 64 != 0)) return false;
+  return true;
+}
+
+// ---- GEMM autotuner: the first eager call of a problem shape times every
+// (tile config, split-K) candidate with HIP events and caches the winner.
+// Calls made while the stream is being captured into a graph (or with
+// SHAI_GEMM_AUTOTUNE=0) use the cached choice, else the analytic planner.
+struct Choice {
+  int cfg, splits;
+};
+std::mutex g_tune_mu;
+std::unordered_map<std::string, Choice> g_tuned;
+
+std::string gemm_key(const shai::GemmArgs& g) {
+  char buf[256];
+  snprintf(buf, sizeof(buf), "%d:%d,%d,%d,b%d,g%d|%d,%d,%d,%d,%d,%d,%d,%d,%d", g.conv, g.M, g.N, g.K, g.batch, g.glu,
+           g.Nimg, g.H, g.Wd, g.Cin, g.Cin1, g.KH, g.stride, g.upsample, g.A2 != nullptr);
+  return buf;
+}
+
+bool autotune_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SHAI_GEMM_AUTOTUNE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+int max_splits_for(const shai::GemmArgs& g) {
+  const int batch = g.batch > 0 ? g.batch : 1;
+  if (batch != 1) return 1;
+  const long kt = (g.K + 63) / 64;
+  int s = 1;
+  while (s < 16 && kt / (s * 2) >= 4) s *= 2;
+  return s;
+}
+
+void launch_choice(const shai::GemmArgs& g, const Tensor& like, Choice c) {
+  Tensor ws;
+  float* wsp = nullptr;
+  if (c.splits > 1) {
+    ws = at::empty({(long)c.splits * g.M * g.N}, like.options().dtype(at::kFloat));
+    wsp = ws.data_ptr<float>();
+  }
+  shai::launch_gemm2_cfg(g, wsp, c.cfg, c.splits, stream());
+}
+
+Choice tune(const shai::GemmArgs& g, const Tensor& like) {
+  Choice def;
+  shai::gemm2_plan(g, &def.cfg, &def.splits);
+  const int ms = max_splits_for(g);
+  std::vector<Choice> cands;
+  for (int c = 0; c < shai::gemm2_num_cfgs(); ++c)
+    for (int s = 1; s <= ms; s *= 2) cands.push_back({c, s});
+  hipStream_t st = stream();
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  Choice best = def;
+  float best_ms = 1e30f;
+  for (const Choice& c : cands) {
+    launch_choice(g, like, c);  // warm (also instantiates caches)
+    hipEventRecord(e0, st);
+    for (int r = 0; r < 3; ++r) launch_choice(g, like, c);
+    hipEventRecord(e1, st);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best_ms) {
+      best_ms = ms;
+      best = c;
+    }
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  return best;
+}
+
+void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_bytes, long a2_bytes) {
+  if (!use_v2(g, a_bytes, w_bytes, a2_bytes)) {
+    shai::launch_gemm(g, stream());
+    return;
+  }
+  const std::string key = gemm_key(g);
+  Choice c{-1, 1};
+  {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    auto it = g_tuned.find(key);
+    if (it != g_tuned.end()) c = it->second;
+  }
+  if (c.cfg < 0) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    hipStreamIsCapturing(stream(), &cs);
+    if (cs == hipStreamCaptureStatusNone && autotune_enabled()) {
+      c = tune(g, like);
+      std::lock_guard<std::mutex> lk(g_tune_mu);
+      g_tuned[key] = c;
+    } else {
+      shai::gemm2_plan(g, &c.cfg, &c.splits);
+    }
+  }
+  launch_choice(g, like, c);
+}
+
+std::vector<std::string> gemm_tuning_table() {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  std::vector<std::string> out;
+  for (auto& kv : g_tuned) {
+    int bm, bn;
+    shai::gemm2_cfg_info(kv.second.cfg, &bm, &bn);
+    out.push_back(kv.first + " -> " + std::to_string(bm) + "x" + std::to_string(bn) + " splitk=" +
+                  std::to_string(kv.second.splits));
+  }
+  return out;
+}
 
 const shai::bf16_t* cptr(const Tensor& t) { return reinterpret_cast<const shai::bf16_t*>(t.data_ptr()); }
 shai::bf16_t* mptr(const Tensor& t) { return reinterpret_cast<shai::bf16_t*>(t.data_ptr()); }
@@ -187,7 +318,8 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
   g.res_alpha = res_alpha;
   g.act = act;
   g.glu = glu;
-  shai::launch_gemm(g, stream());
+  const long a_bytes = (batched ? (long)a.size(0) * a.stride(0) : (long)g.M * g.lda) * 2;
+  run_gemm(g, a, a_bytes, (long)g.N * g.ldw * 2, 0);
 }
 
 // x: [N, H, W, C1] NHWC; x2 optional [N, H, W, C2]; w: [Cout, KH*KW*Cin]; out: [N, OH, OW, Cout]
@@ -264,7 +396,7 @@ void conv2d(const Tensor& x, const optional<Tensor>& x2, const Tensor& w, const 
     g.in_shift = in_shift->data_ptr<float>();
     g.in_act = in_act;
   }
-  shai::launch_gemm(g, stream());
+  run_gemm(g, x, x.numel() * 2, w.numel() * 2, x2 ? x2->numel() * 2 : 0);
 }
 
 // ---------------------------------------------------------------- attention
@@ -440,6 +572,8 @@ void softmax_(const Tensor& x, double scale) {
   shai::launch_softmax(mptr(x), x.numel() / x.size(-1), x.size(-1), scale, stream());
 }
 
+std::vector<std::string> gemm_tuning() { return gemm_tuning_table(); }
+
 void embedding(const Tensor& ids, const Tensor& table, const Tensor& out) {
   check_i32(ids, "ids");
   check_bf16(table, "table");
@@ -467,6 +601,7 @@ TORCH_LIBRARY(shai, m) {
   m.def("sched_step(Tensor model_out, Tensor(a!) latents, bool cfg, float guidance, int pred_type, float a_t, float a_prev, float dt) -> ()");
   m.def("softmax_(Tensor(a!) x, float scale) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out) -> ()");
+  m.def("gemm_tuning() -> str[]", &gemm_tuning);
 }
 
 TORCH_LIBRARY_IMPL(shai, CUDA, m) {

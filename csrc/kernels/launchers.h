@@ -93,7 +93,14 @@ struct GemmArgs {
   const float* in_shift;
   int in_act;
 };
-void launch_gemm(const GemmArgs& a, hipStream_t s);
+void launch_gemm(const GemmArgs& a, hipStream_t s);       // v1: register-staged (supports fused GN gather)
+// v2: LDS-DMA staged, tile configs + split-K (ws: fp32 workspace of gemm2_workspace_bytes, may be null)
+void launch_gemm2(const GemmArgs& a, float* ws, hipStream_t s);
+size_t gemm2_workspace_bytes(const GemmArgs& a);
+void gemm2_plan(const GemmArgs& a, int* cfg, int* splits);
+void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStream_t s);
+int gemm2_num_cfgs();
+void gemm2_cfg_info(int cfg, int* bm, int* bn);
 
 // ---------------------------------------------------------------- attention
 struct AttnArgs {

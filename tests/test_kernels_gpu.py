@@ -279,3 +279,24 @@ def test_softmax_embedding(cuda):
     table = rnd(1000, 256)
     ids = torch.randint(0, 1000, (3, 17), device="cuda")
     assert torch.equal(ops.embedding(ids, table), table[ids])
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 512, 8192), (64, 14336, 4096), (8, 4096, 4096), (1000, 320, 2880)])
+def test_gemm_splitk_shapes(cuda, M, N, K):
+    torch.manual_seed(20)
+    x, w, b, r = rnd(M, K), rnd(N, K, scale=1 / math.sqrt(K)), rnd(N), rnd(M, N)
+    close(ops.linear(x, w, b, act="silu", residual=r), ref.linear(x, w, b, "silu", r), 2e-2)
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(N=8, H=8, W=8, C=1280, Co=1280),
+    dict(N=2, H=16, W=16, C=2560, Co=1280),
+])
+def test_conv2d_small_spatial_splitk(cuda, cfg):
+    torch.manual_seed(21)
+    x = rnd(cfg["N"], cfg["H"], cfg["W"], cfg["C"])
+    w = ops.pack_conv_weight(rnd(cfg["Co"], cfg["C"], 3, 3, scale=1 / math.sqrt(cfg["C"] * 9)))
+    b, res = rnd(cfg["Co"]), rnd(cfg["N"], cfg["H"], cfg["W"], cfg["Co"])
+    temb = rnd(cfg["N"], cfg["Co"])
+    close(ops.conv2d(x, w, b, 3, 3, 1, 1, temb=temb, residual=res),
+          ref.conv2d(x, w, b, 3, 3, 1, 1, temb=temb, residual=res), 3e-2)
