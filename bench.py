@@ -152,6 +152,10 @@ def main():
         res = bench_sd21(args, rank, world) if args.workload == "sd21" else bench_mistral(args, rank, world)
     if rank == 0:
         print(json.dumps(res), flush=True)
+        save = os.environ.get("SHAI_GEMM_TUNE_SAVE")
+        if save:
+            import shai_amd.native as native
+            native.save_gemm_tuning(save)
     if world > 1:
         import torch.distributed as dist
         dist.barrier()

@@ -574,6 +574,30 @@ void softmax_(const Tensor& x, double scale) {
 
 std::vector<std::string> gemm_tuning() { return gemm_tuning_table(); }
 
+// Export / import the autotuner cache ("key=cfg,splits") so later processes skip tuning.
+std::vector<std::string> gemm_tuning_export() {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  std::vector<std::string> out;
+  for (auto& kv : g_tuned) out.push_back(kv.first + "=" + std::to_string(kv.second.cfg) + "," + std::to_string(kv.second.splits));
+  return out;
+}
+
+int64_t gemm_tuning_import(const std::vector<std::string>& entries) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  int64_t n = 0;
+  for (const auto& e : entries) {
+    const auto eq = e.rfind('=');
+    const auto cm = e.rfind(',');
+    if (eq == std::string::npos || cm == std::string::npos || cm < eq) continue;
+    const int cfg = atoi(e.substr(eq + 1, cm - eq - 1).c_str());
+    const int sp = atoi(e.substr(cm + 1).c_str());
+    if (cfg < 0 || cfg >= shai::gemm2_num_cfgs() || sp < 1) continue;
+    g_tuned[e.substr(0, eq)] = Choice{cfg, sp};
+    ++n;
+  }
+  return n;
+}
+
 void embedding(const Tensor& ids, const Tensor& table, const Tensor& out) {
   check_i32(ids, "ids");
   check_bf16(table, "table");
@@ -602,6 +626,8 @@ TORCH_LIBRARY(shai, m) {
   m.def("softmax_(Tensor(a!) x, float scale) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out) -> ()");
   m.def("gemm_tuning() -> str[]", &gemm_tuning);
+  m.def("gemm_tuning_export() -> str[]", &gemm_tuning_export);
+  m.def("gemm_tuning_import(str[] entries) -> int", &gemm_tuning_import);
 }
 
 TORCH_LIBRARY_IMPL(shai, CUDA, m) {

@@ -152,29 +152,39 @@ __global__ void __launch_bounds__(256, 2) flash_fwd_kernel(const AttnArgs p) {
         sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kb], 0, 0, 0);
       }
     }
-    // ---- scale, bias, mask (log2 domain)
+    // ---- mask (+ bias), row max on raw scores, exp2 with the scale folded into one FMA
     const int key0 = t * KT;
     const bool need_mask = (key0 + KT > kv_len) || (p.causal && key0 + KT - 1 > q0 + c_off);
     float mloc = -INFINITY;
+    if (bias_row) {  // T5 relative-position bias: additive in the natural-log domain
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-        float sv = sacc[kb][r] * sl2;
-        if (bias_row) sv += (key < p.Skv ? bf2f(bias_row[key]) : 0.f) * kLog2e;
-        if (need_mask) {
-          const bool bad = key >= kv_len || (p.causal && key > qi + c_off);
-          sv = bad ? -INFINITY : sv;
+        for (int r = 0; r < 16; ++r) {
+          const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          sacc[kb][r] += (key < p.Skv ? bf2f(bias_row[key]) : 0.f) / p.scale;
         }
-        sacc[kb][r] = sv;
-        mloc = fmaxf(mloc, sv);
-      }
     }
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    if (need_mask) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          const bool bad = key >= kv_len || (p.causal && key > qi + c_off);
+          sacc[kb][r] = bad ? -INFINITY : sacc[kb][r];
+        }
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) mloc = fmaxf(mloc, fmaxf(sacc[kb][r], sacc[kb][r + 1]));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64)) * sl2;   // scale > 0: max commutes with scaling
     const float m_new = fmaxf(m_run, mloc);
     const float m_use = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f(m_run - m_use);
+    // Skip the O rescale when no row max grew in this tile (exact: alpha == 1).
+    const bool grew = __any(m_new > m_run);
+    const float alpha = grew ? __builtin_amdgcn_exp2f(m_run - m_use) : 1.f;
     m_run = m_new;
     float lsum = 0.f;
     bf16x8 pf[2][2];
@@ -182,7 +192,7 @@ __global__ void __launch_bounds__(256, 2) flash_fwd_kernel(const AttnArgs p) {
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float e = exp2f(sacc[kb][r] - m_use);
+        const float e = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], sl2, -m_use));
         sacc[kb][r] = e;
         lsum += e;
       }
@@ -195,10 +205,12 @@ __global__ void __launch_bounds__(256, 2) flash_fwd_kernel(const AttnArgs p) {
       }
     }
     l_run = l_run * alpha + lsum;
+    if (grew) {
 #pragma unroll
-    for (int d = 0; d < ND; ++d)
+      for (int d = 0; d < ND; ++d)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+    }
 
     // ---- O^T += V^T P^T
 #pragma unroll

@@ -140,7 +140,38 @@ __global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict_
 #pragma unroll
   for (int i = 0; i < 8; ++i) s0[i] = q0[i] = s1[i] = q1[i] = 0.f;
   if (active) {
-    for (int p = p0 + pl; p < p1; p += P) {
+    int p = p0 + pl;
+    // 4 independent 16-byte loads in flight per thread
+    for (; p + 3 * P < p1; p += 4 * P) {
+      uint4_ v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4_*>(xn + (long)(p + u * P) * C + cv0 * 8);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          s0[i] += f[i];
+          q0[i] += f[i] * f[i];
+        }
+      }
+      if (second) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4_*>(xn + (long)(p + u * P) * C + (cv0 + 256) * 8);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float f[8];
+          unpack8(v[u], f);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            s1[i] += f[i];
+            q1[i] += f[i] * f[i];
+          }
+        }
+      }
+    }
+    for (; p < p1; p += P) {
       const bf16_t* xp = xn + (long)p * C;
       float f[8];
       unpack8(*reinterpret_cast<const uint4_*>(xp + cv0 * 8), f);
@@ -205,18 +236,32 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const float* __restric
                                                           float* __restrict__ shift, int HW, int C, int G, int NB,
                                                           float eps) {
   __shared__ float mean_s[128], rstd_s[128];
+  __shared__ float red[2][256];
   const int n = blockIdx.x;
   const int Cg = C / G;
+  // 256 threads = L lanes per group x G groups (L = 256 / G); lanes stride over the partials
+  const int L = 256 / G;
+  const int g0 = threadIdx.x % G, lane_k = threadIdx.x / G;
+  float a = 0.f, b = 0.f;
+  if (lane_k < L) {
+    for (int k = lane_k; k < NB; k += L) {
+      const float2 v = *reinterpret_cast<const float2*>(part + (((long)n * NB + k) * G + g0) * 2);
+      a += v.x;
+      b += v.y;
+    }
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
   for (int g = threadIdx.x; g < G; g += blockDim.x) {
-    double a = 0.0, b = 0.0;
-    for (int k = 0; k < NB; ++k) {
-      const float* p = part + (((long)n * NB + k) * G + g) * 2;
-      a += p[0];
-      b += p[1];
+    double sa = 0.0, sb = 0.0;
+    for (int l = 0; l < L; ++l) {
+      sa += red[0][l * G + g];
+      sb += red[1][l * G + g];
     }
     const double cnt = (double)HW * Cg;
-    const double mean = a / cnt;
-    double var = b / cnt - mean * mean;
+    const double mean = sa / cnt;
+    double var = sb / cnt - mean * mean;
     if (var < 0) var = 0;
     mean_s[g] = (float)mean;
     rstd_s[g] = (float)(1.0 / sqrt(var + (double)eps));
@@ -259,8 +304,8 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const bf16_t* __restrict_
 }
 
 int gn_num_blocks(int HW) {
-  // ~512 pixels per block, at most 256 partial slots per sample
-  int nb = (HW + 511) / 512;
+  // ~256 pixels per block (one partial slot each), at most 256 slots per sample
+  int nb = (HW + 255) / 256;
   if (nb > 256) nb = 256;
   if (nb < 1) nb = 1;
   return nb;

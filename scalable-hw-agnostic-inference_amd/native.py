@@ -40,8 +40,32 @@ def _load_kernels() -> None:
                 raise NativeUnavailable(f"{KERNELS_LIB} not found; run `python csrc/build.py`")
             torch.ops.load_library(KERNELS_LIB)
             _kernels_loaded = True
+            _autoload_tuning()
         except Exception as e:  # pragma: no cover - depends on build state
             _kernels_error = e
+
+
+def _autoload_tuning() -> None:
+    path = os.environ.get("SHAI_GEMM_TUNE_FILE")
+    if path and os.path.exists(path):
+        load_gemm_tuning(path)
+
+
+def save_gemm_tuning(path: str) -> int:
+    """Persist the GEMM autotuner cache (shape key -> tile config, split-K)."""
+    import json
+    entries = list(ops().gemm_tuning_export())
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "w") as f:
+        json.dump(entries, f, indent=0)
+    return len(entries)
+
+
+def load_gemm_tuning(path: str) -> int:
+    import json
+    with open(path) as f:
+        entries = json.load(f)
+    return int(torch.ops.shai.gemm_tuning_import(entries))
 
 
 def kernels_available() -> bool:

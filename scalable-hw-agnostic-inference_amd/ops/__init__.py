@@ -77,8 +77,7 @@ def groupnorm_stats(x: torch.Tensor, gamma, beta, groups: int, eps: float):
     if not _gpu(x):
         return ref.groupnorm_stats(x3, gamma, beta, groups, eps)
     HW = x3.shape[1]
-    nb = min(256, max(1, (HW + 511) // 512))
-    part = torch.empty(N * nb * groups * 2, dtype=torch.float32, device=x.device)
+    part = torch.empty(N * 256 * groups * 2, dtype=torch.float32, device=x.device)
     scale = torch.empty(N, C, dtype=torch.float32, device=x.device)
     shift = torch.empty(N, C, dtype=torch.float32, device=x.device)
     _K().groupnorm_stats(x3, gamma, beta, part, scale, shift, int(groups), float(eps))
