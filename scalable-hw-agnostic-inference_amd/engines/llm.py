@@ -376,3 +376,88 @@ def bench_decode_throughput(args, rank, world):
                    "seq_len": P + G, "prompt_len": P, "gen_len": G, "parallelism": f"tp{world}"},
         "p50_ttft_ms": round(1000 * float(np.median(ttft)), 2), "p50_tpot_ms": round(1000 * float(np.median(tpot)), 3),
     }
+
+
+# ---------------------------------------------------------------------- online service
+class LLMService:
+    """Thread-safe front end: a dedicated engine thread runs continuous batching;
+    callers submit prompts (text or ids) and wait on futures.
+
+    Replaces the reference's offline ``LLM.generate`` per HTTP request
+    (app/vllm_model_api.py:38-43), so concurrent requests share decode steps."""
+
+    def __init__(self, engine: LLMEngine, tokenizer=None):
+        import queue
+        import threading
+        self.engine = engine
+        self.tokenizer = tokenizer
+        self._q: "queue.Queue" = queue.Queue()
+        self._futs = {}
+        self._t = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
+        self._t.start()
+
+    def _loop(self):
+        import queue
+        while True:
+            try:
+                block = not self.engine.has_work()
+                while True:
+                    item = self._q.get(block=block, timeout=None if block else 0)
+                    block = False
+                    ids, params, fut = item
+                    s = self.engine.add_request(ids, params)
+                    self._futs[s.seq_id] = (s, fut)
+            except queue.Empty:
+                pass
+            try:
+                with torch.inference_mode():
+                    done = self.engine.step()
+            except BaseException as e:  # fail every in-flight request
+                for sid, (s, fut) in list(self._futs.items()):
+                    if not fut.done():
+                        fut.set_exception(e)
+                self._futs.clear()
+                self.engine.waiting.clear()
+                self.engine.running.clear()
+                continue
+            for s in done:
+                ent = self._futs.pop(s.seq_id, None)
+                if ent is not None:
+                    ent[1].set_result(s)
+
+    def submit_ids(self, ids, params: SamplingParams):
+        from concurrent.futures import Future
+        f = Future()
+        self._q.put((list(ids), params, f))
+        return f
+
+    def encode(self, text: str):
+        if self.tokenizer is None:
+            raise RuntimeError("no tokenizer")
+        enc = self.tokenizer(text, padding="longest", truncation=True, max_length=self.engine.max_model_len - 1)
+        ids = enc["input_ids"]
+        ids = ids[0] if hasattr(ids, "dim") and ids.dim() == 2 else ids
+        return [int(i) for i in (ids.tolist() if hasattr(ids, "tolist") else ids)]
+
+    def generate_text(self, prompt: str, params: SamplingParams, timeout: Optional[float] = None):
+        t0 = time.time()
+        s = self.submit_ids(self.encode(prompt), params).result(timeout)
+        text = self.tokenizer.decode(s.output, skip_special_tokens=True)
+        return text, time.time() - t0, s
+
+
+def llama_config_for(model_id: str, model_path: Optional[str] = None, size: str = "") -> LlamaConfig:
+    import json
+    if model_path and os.path.exists(os.path.join(model_path, "config.json")):
+        with open(os.path.join(model_path, "config.json")) as f:
+            d = json.load(f)
+        d = d.get("text_config", d)
+        return LlamaConfig.from_hf(d)
+    m = (model_id or "").lower()
+    if size == "tiny":
+        return LlamaConfig.tiny()
+    if "70b" in m or "deepseek" in m:
+        return LlamaConfig.deepseek_r1_distill_70b() if "deepseek" in m else LlamaConfig.llama3_70b()
+    if "llama" in m:
+        return LlamaConfig.llama3_8b()
+    return LlamaConfig.mistral_7b()

@@ -1,0 +1,126 @@
+"""API contract tests: every reference endpoint on tiny CPU models
+via FastAPI's TestClient -- paths, JSON keys, types, base64 payloads, report format."""
+import base64
+import io
+import re
+
+import numpy as np
+import pytest
+from fastapi.testclient import TestClient
+
+from shai_amd.serving.common import LatencyCollector, ServerEnv, latency_report
+
+REPORT_RE = re.compile(r"RESULT FOR .+: Latency P0=\d+\.\d Latency P50=\d+\.\d Latency P90=\d+\.\d "
+                       r"Latency P95=\d+\.\d Latency P99=\d+\.\d Latency P100=\d+\.\d$")
+
+
+def env(**kw):
+    base = dict(app="t", pod_name="pod0", nodepool="mi355x", model_id="m", device="cpu", config="tiny",
+                num_inference_steps=2, max_new_tokens=4, max_seq_len=16, height=64, width=64)
+    base.update(kw)
+    return ServerEnv(**base)
+
+
+def test_percentile_rule_matches_reference():
+    lc = LatencyCollector()
+    lc.latency_list = [0.5, 0.1, 0.3, 0.2, 0.4]
+    assert lc.percentile(0) == 0.1 and lc.percentile(100) == 0.5
+    assert lc.percentile(50) == 0.3   # pos 2.5 -> floor (frac not > .5)
+    assert lc.percentile(90) == 0.5   # pos 4.5 -> floor 4
+    lc.latency_list = [1, 2, 3, 4, 5, 6, 7]
+    assert lc.percentile(90) == 7     # pos 6.3 -> floor 6
+    assert lc.percentile(95) == 7     # 6.65 -> ceil clipped
+    r = latency_report(lc, "stable_diffusion_512", "pod0")
+    assert r.startswith("RESULT FOR stable_diffusion_512 on pod0: Latency P0=1000.0") and REPORT_RE.match(r)
+
+
+def test_sd_server():
+    from shai_amd.serving import sd
+    c = TestClient(sd.create_app(env=env(app="sd21")))
+    assert c.get("/health").json() == {"message": "pod0is healthy"}
+    assert c.get("/readiness").json() == {"message": "pod0is ready"}
+    assert c.get("/").json()["message"].startswith("This ism pod pod0")
+    r = c.post("/genimage", json={"prompt": "a cat"}).json()
+    assert set(r) == {"prompt", "response", "latency"} and isinstance(r["latency"], str)
+    from PIL import Image
+    im = Image.open(io.BytesIO(base64.b64decode(r["response"])))
+    assert im.size == (64, 64)
+    m = c.get("/load/2/infer/2").json()["message"]
+    assert m.startswith("benchmark report:RESULT FOR stable_diffusion_512 on pod0:")
+    assert REPORT_RE.match(m[len("benchmark report:"):])
+    prom = c.get("/metrics").text
+    assert "sd21_counter_total" in prom and "mi355x_total" in prom
+    assert c.get("/serve").status_code == 200
+
+
+def test_llm_api_server():
+    from shai_amd.serving import llm_api
+    c = TestClient(llm_api.create_app(env=env(app="mistral")))
+    assert c.get("/health").json() == {"message": "pod0 is healthy"}
+    r = c.post("/generate", json={"prompt": "What model are you?", "max_new_tokens": 5}).json()
+    assert set(r) == {"text", "execution_time"} and isinstance(r["execution_time"], float)
+    base64.b64decode(r["text"]).decode()
+    # multimodal variant: optional base64 image
+    from PIL import Image
+    buf = io.BytesIO()
+    Image.new("RGB", (8, 8)).save(buf, format="PNG")
+    r2 = c.post("/generate", json={"prompt": "describe", "max_new_tokens": 3,
+                                   "image": base64.b64encode(buf.getvalue()).decode()})
+    assert r2.status_code == 200
+    rep = base64.b64decode(c.post("/benchmark", json={"n_runs": 3, "max_new_tokens": 4, "prompt": "hi"}).json()
+                           ["report"]).decode()
+    assert rep.startswith("RESULT FOR benchmark:mistral on mi355x with 4 output tokens: Latency P0=")
+
+
+def test_llm_gradio_server():
+    from shai_amd.serving import llm_gradio
+    c = TestClient(llm_gradio.create_app(env=env(app="llama")))
+    r = c.post("/gentext", json={"prompt": "write a poem"}).json()
+    assert set(r) == {"prompt", "response", "latency"} and isinstance(r["latency"], str)
+    r = c.post("/sentiment", json={"prompt": "great movie"}).json()
+    assert set(r) == {"prompt", "response", "latency"}
+    assert c.get("/health").json() == {"message": "pod0is healthy"}
+
+
+def test_bert_server():
+    from shai_amd.serving import bert
+    c = TestClient(bert.create_app(env=env(app="bert")))
+    r = c.post("/sentiment", json={"prompt": "Hamilton is great"}).json()
+    assert r["response"] in ("POSITIVE", "NEGATIVE") and isinstance(r["latency"], float)
+    assert c.options("/sentiment", headers={"Origin": "http://x", "Access-Control-Request-Method": "POST"}
+                     ).headers.get("access-control-allow-origin") in ("*", "http://x")
+
+
+def _img_b64(w=96, h=80):
+    from PIL import Image
+    buf = io.BytesIO()
+    Image.fromarray((np.random.default_rng(0).random((h, w, 3)) * 255).astype(np.uint8)).save(buf, format="PNG")
+    return base64.b64encode(buf.getvalue()).decode()
+
+
+def test_vit_server():
+    from shai_amd.serving import vit
+    c = TestClient(vit.create_app(env=env(app="vit")))
+    src = _img_b64()
+    r = c.post("/imgcls", json={"prompt": src}).json()
+    assert r["image"] == src and r["response"].startswith("LABEL_") and isinstance(r["latency"], float)
+
+
+def test_yolos_server():
+    from shai_amd.serving import yolos
+    c = TestClient(yolos.create_app(env=env(app="yolos")))
+    r = c.post("/detectobj", json={"prompt": _img_b64()}).json()
+    assert set(r) == {"image", "response", "latency"} and isinstance(r["response"], list)
+    for d in r["response"]:
+        assert set(d) == {"score", "label", "box"} and set(d["box"]) == {"xmin", "ymin", "xmax", "ymax"}
+
+
+def test_t5_server():
+    from shai_amd.serving import t5_api
+    c = TestClient(t5_api.create_app(env=env(app="t5")))
+    r = c.post("/generate", json={"prompt": "a caption", "max_new_tokens": 16}).json()
+    txt = base64.b64decode(r["text"]).decode()
+    assert txt.startswith("[") and isinstance(r["execution_time"], float)
+    rep = base64.b64decode(c.post("/benchmark", json={"n_runs": 2, "max_new_tokens": 16, "prompt": "x"}).json()
+                           ["report"]).decode()
+    assert rep.startswith("RESULT FOR benchmark:t5 on mi355x with 16 output tokens:")
