@@ -1,1 +1,1 @@
-"""shai_amd.controller"""
+"""Control loops."""
