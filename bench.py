@@ -9,6 +9,8 @@ VAE decode) -- nothing is skipped inside the timed region.  N GPUs run N
 data-parallel replicas (one process per GPU, torch.distributed over RCCL for
 the barrier / max-reduction), so per-GPU work is fixed: weak scaling.
 
+``--workload flux``: Flux.1-dev 512x512 (10 steps by default) images/s + p50 latency.
+
 ``--workload mistral``: Mistral-7B bf16 decode throughput (tokens/s) through the
 native LLM engine at TP = N (see shai_amd.engines.llm).
 
@@ -125,6 +127,54 @@ def bench_sd21(args, rank, world):
     return res
 
 
+REF_FLUX_512_10STEP_S = 5.61   # cova/README.md:98 (Neuron TP8 Flux service, 512x512, 10 steps, end-to-end)
+
+
+def bench_flux(args, rank, world):
+    """Flux.1-dev txt2img (CLIP-L + T5-XXL 512 tokens + 12B MMDiT + 16-ch VAE), one replica per GPU."""
+    import torch
+    from shai_amd.engines.flux import FluxEngine, FluxPipelineConfig
+    steps_inf = args.inference_steps if args.inference_steps != 50 else 10
+    eng = FluxEngine(FluxPipelineConfig.dev(args.height, args.width, 512), device="cuda", seed=rank,
+                     use_graphs=not args.no_graphs)
+    prompts = [f"A cat holding a sign that says hello world, variant {rank}-{i}" for i in range(args.batch)]
+    for i in range(args.warmup):
+        eng.generate(prompts, steps_inf, seed=10 + i, output="tensor")
+    lat = []
+    for i in range(args.latency_runs):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.generate(prompts[:1], steps_inf, seed=20 + i)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t0)
+    _barrier(world)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        img = eng.generate(prompts, steps_inf, seed=30 + i, output="tensor")
+    torch.cuda.synchronize()
+    _barrier(world)
+    elapsed = _max_over_ranks(time.perf_counter() - t0, world)
+    value = args.batch * args.steps * world / elapsed
+    p50 = statistics.median(lat) if lat else None
+    return {
+        "metric": f"Flux.1-dev {args.height}x{args.width} images/sec ({steps_inf} steps)",
+        "value": round(value, 4), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2), "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(REF_FLUX_512_10STEP_S / p50, 3) if (p50 and steps_inf == 10 and args.height == 512)
+        else None,
+        "dtype": "bf16", "data": "synthetic prompts, random-init weights (full Flux.1-dev architecture)",
+        "config": {"model": "black-forest-labs/FLUX.1-dev (MMDiT 11.9B + T5-XXL + CLIP-L + VAE)",
+                   "global_batch": args.batch * world, "per_gpu_batch": args.batch, "seq_len": 512,
+                   "resolution": f"{args.height}x{args.width}", "inference_steps": steps_inf,
+                   "guidance_scale": 3.5, "parallelism": f"dp{world}", "hip_graphs": not args.no_graphs},
+        "p50_latency_ms_bs1": round(1000 * p50, 1) if p50 else None,
+        "baseline_note": "vs_baseline = 5.61 s (reference Flux 512^2 10-step end-to-end on Neuron TP8, "
+                         "cova/README.md:98) / our p50 single-image latency",
+        "outputs_finite": bool(torch.isfinite(img.float()).all().item()),
+    }
+
+
 def bench_mistral(args, rank, world):
     import torch
     from shai_amd.engines.llm import bench_decode_throughput
@@ -136,7 +186,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="sd21", choices=["sd21", "mistral"])
+    ap.add_argument("--workload", default="sd21", choices=["sd21", "mistral", "flux"])
     ap.add_argument("--batch", type=int, default=8, help="images per GPU per step (sd21) / sequences (mistral)")
     ap.add_argument("--inference-steps", type=int, default=50)
     ap.add_argument("--height", type=int, default=512)
@@ -149,7 +199,8 @@ def main():
     import torch
     rank, world, local = _dist_init(args.gpus)
     with torch.inference_mode():
-        res = bench_sd21(args, rank, world) if args.workload == "sd21" else bench_mistral(args, rank, world)
+        fn = {"sd21": bench_sd21, "mistral": bench_mistral, "flux": bench_flux}[args.workload]
+        res = fn(args, rank, world)
     if rank == 0:
         print(json.dumps(res), flush=True)
         save = os.environ.get("SHAI_GEMM_TUNE_SAVE")

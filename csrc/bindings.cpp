@@ -80,7 +80,17 @@ void launch_choice(const shai::GemmArgs& g, const Tensor& like, Choice c) {
   shai::launch_gemm2_cfg(g, wsp, c.cfg, c.splits, stream());
 }
 
-Choice tune(const shai::GemmArgs& g, const Tensor& like) {
+// Candidates are timed into a scratch output so that in-place epilogues (C aliasing
+// the residual, e.g. x = x + gate * f(x)) are applied exactly once, by the caller's
+// final launch.
+Choice tune(const shai::GemmArgs& g_real, const Tensor& like) {
+  shai::GemmArgs g = g_real;
+  const long n_out = g.glu ? g.N / 2 : g.N;
+  const int nb = g.batch > 0 ? g.batch : 1;
+  Tensor scratch = at::empty({(long)nb * g.M * n_out + 8}, like.options().dtype(at::kBFloat16));
+  g.C = reinterpret_cast<shai::bf16_t*>(scratch.data_ptr());
+  g.ldc = n_out;
+  g.batch_c = (long)g.M * n_out;
   Choice def;
   shai::gemm2_plan(g, &def.cfg, &def.splits);
   const int ms = max_splits_for(g);
@@ -113,6 +123,7 @@ Choice tune(const shai::GemmArgs& g, const Tensor& like) {
 
 void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_bytes, long a2_bytes) {
   if (!use_v2(g, a_bytes, w_bytes, a2_bytes)) {
+    SHAI_CHECK(g.gate == nullptr, "gated GEMM epilogue needs the v2 kernel (operands < 2 GiB, SHAI_GEMM_V1 unset)");
     shai::launch_gemm(g, stream());
     return;
   }
@@ -223,6 +234,58 @@ void layernorm(const Tensor& x, const optional<Tensor>& w, const optional<Tensor
   shai::launch_layernorm(a, stream());
 }
 
+// y = LayerNorm(x) * (1 + scale[r / rows_per_mod]) + shift[r / rows_per_mod]  (AdaLN modulation, no affine)
+void layernorm_mod(const Tensor& x, const Tensor& scale, const Tensor& shift, const Tensor& out,
+                   int64_t rows_per_mod, double eps) {
+  check_rows(x, "x");
+  check_rows(out, "out");
+  check_bf16(scale, "scale");
+  check_bf16(shift, "shift");
+  const int D = x.size(-1);
+  SHAI_CHECK(D % 8 == 0 && D <= 8192, "layernorm_mod D must be a multiple of 8 and <= 8192");
+  SHAI_CHECK(x.dim() == 2 || x.is_contiguous(), "layernorm_mod x must be 2D strided or contiguous");
+  SHAI_CHECK(scale.dim() == 2 && shift.dim() == 2 && scale.size(1) == D && shift.size(1) == D &&
+                 scale.stride(0) == shift.stride(0) && scale.stride(0) % 8 == 0,
+             "scale/shift must be [G, D] with equal 16B-aligned row strides");
+  const long rows = x.numel() / D;
+  SHAI_CHECK(rows_per_mod > 0 && scale.size(0) * rows_per_mod >= rows, "modulation rows");
+  shai::RowNormArgs a{};
+  a.x = cptr(x);
+  a.w = cptr(scale);
+  a.b = cptr(shift);
+  a.out = mptr(out);
+  a.rows = rows;
+  a.D = D;
+  a.x_stride = x.dim() == 2 ? x.stride(0) : D;
+  a.out_stride = out.dim() == 2 ? out.stride(0) : D;
+  a.eps = eps;
+  a.w_offset = 1.f;
+  a.rows_per_w = rows_per_mod;
+  a.w_stride = scale.stride(0);
+  shai::launch_layernorm(a, stream());
+}
+
+// In-place per-head RMSNorm(q), RMSNorm(k) + pair RoPE on a packed QKV buffer [rows, >= 2*H*D].
+void qk_norm_rope(const Tensor& x, const optional<Tensor>& q_w, const optional<Tensor>& k_w,
+                  const optional<Tensor>& cos, const optional<Tensor>& sin, int64_t H, int64_t D, int64_t S,
+                  double eps) {
+  check_bf16(x, "x");
+  SHAI_CHECK(x.dim() == 2 && x.size(1) >= 2 * H * D && x.stride(0) % 2 == 0, "qk_norm_rope x [rows, >= 2*H*D]");
+  SHAI_CHECK(D % 2 == 0 && D <= 128, "qk_norm_rope head dim must be even and <= 128");
+  SHAI_CHECK(cos.has_value() == sin.has_value(), "cos and sin go together");
+  if (q_w) { check_bf16(*q_w, "q_w"); SHAI_CHECK(q_w->numel() == D, "q_w [D]"); }
+  if (k_w) { check_bf16(*k_w, "k_w"); SHAI_CHECK(k_w->numel() == D, "k_w [D]"); }
+  if (cos) {
+    check_f32(*cos, "cos");
+    check_f32(*sin, "sin");
+    SHAI_CHECK(cos->numel() == S * D / 2 && sin->numel() == S * D / 2, "cos/sin must be [S, D/2]");
+  }
+  SHAI_CHECK(S > 0, "S > 0");
+  shai::launch_qk_norm_rope(mptr(x), x.stride(0), x.size(0), S, H, D, optr(q_w), optr(k_w),
+                            cos ? cos->data_ptr<float>() : nullptr, sin ? sin->data_ptr<float>() : nullptr, eps,
+                            stream());
+}
+
 void groupnorm_stats(const Tensor& x, const optional<Tensor>& gamma, const optional<Tensor>& beta,
                      const Tensor& partials, const Tensor& scale, const Tensor& shift, int64_t G, double eps) {
   check_bf16(x, "x");
@@ -272,7 +335,7 @@ void groupnorm_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, 
 // a: [M, K] or [B, M, K]; w: [N, K] or [B, N, K]; c: [M, N'] or [B, M, N'] (N' = N or N/2 for glu)
 void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tensor>& bias,
           const optional<Tensor>& bias2d, int64_t rows_per_bias2d, const optional<Tensor>& residual, double alpha,
-          double res_alpha, int64_t act, bool glu) {
+          double res_alpha, int64_t act, bool glu, const optional<Tensor>& gate, int64_t rows_per_gate) {
   check_rows(a, "a");
   check_rows(w, "w");
   check_bf16(c, "c");
@@ -313,6 +376,15 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
     g.residual = cptr(*residual);
     g.ldr = residual->stride(-2);
     g.batch_r = batched ? residual->stride(0) : 0;
+  }
+  if (gate) {
+    check_bf16(*gate, "gate");
+    SHAI_CHECK(gate->dim() == 2 && gate->size(1) == c.size(-1) && rows_per_gate > 0 &&
+                   gate->size(0) * rows_per_gate >= (long)g.batch * g.M,
+               "gate must be [G, N_out] with G * rows_per_gate >= rows");
+    g.gate = cptr(*gate);
+    g.gate_stride = gate->stride(0);
+    g.rows_per_gate = rows_per_gate;
   }
   g.alpha = alpha;
   g.res_alpha = res_alpha;
@@ -613,7 +685,9 @@ TORCH_LIBRARY(shai, m) {
   m.def("layernorm(Tensor x, Tensor? w, Tensor? b, Tensor(a!) out, Tensor? residual, Tensor(b!)? residual_out, float eps) -> ()");
   m.def("groupnorm_stats(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!) partials, Tensor(b!) scale, Tensor(c!) shift, int G, float eps) -> ()");
   m.def("groupnorm_apply(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, bool silu) -> ()");
-  m.def("gemm(Tensor a, Tensor w, Tensor(a!) c, Tensor? bias, Tensor? bias2d, int rows_per_bias2d, Tensor? residual, float alpha, float res_alpha, int act, bool glu) -> ()");
+  m.def("gemm(Tensor a, Tensor w, Tensor(a!) c, Tensor? bias, Tensor? bias2d, int rows_per_bias2d, Tensor? residual, float alpha, float res_alpha, int act, bool glu, Tensor? gate=None, int rows_per_gate=1) -> ()");
+  m.def("layernorm_mod(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, int rows_per_mod, float eps) -> ()");
+  m.def("qk_norm_rope(Tensor(a!) x, Tensor? q_w, Tensor? k_w, Tensor? cos, Tensor? sin, int H, int D, int S, float eps) -> ()");
   m.def("conv2d(Tensor x, Tensor? x2, Tensor w, Tensor(a!) out, Tensor? bias, Tensor? bias2d, Tensor? residual, Tensor? in_scale, Tensor? in_shift, int in_act, int kh, int kw, int stride, int pad, bool upsample, int act, float res_alpha) -> ()");
   m.def("flash_attn(Tensor q, Tensor k, Tensor v, Tensor(a!) o, float scale, bool causal, int causal_offset, Tensor? kv_lens, Tensor? q_lens, Tensor? bias, Tensor? block_table) -> ()");
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor(a!) o, Tensor block_table, Tensor ctx_lens, Tensor(b!) ws, int num_splits, float scale) -> ()");
@@ -636,6 +710,8 @@ TORCH_LIBRARY_IMPL(shai, CUDA, m) {
   m.impl("groupnorm_stats", &groupnorm_stats);
   m.impl("groupnorm_apply", &groupnorm_apply);
   m.impl("gemm", &gemm);
+  m.impl("layernorm_mod", &layernorm_mod);
+  m.impl("qk_norm_rope", &qk_norm_rope);
   m.impl("conv2d", &conv2d);
   m.impl("flash_attn", &flash_attn);
   m.impl("decode_attn", &decode_attn);

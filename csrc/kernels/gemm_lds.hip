@@ -1,6 +1,9 @@
 // bf16 MFMA GEMM / implicit-GEMM convolution, v2: LDS-DMA staging.
 //
-//   C[b,m,n] = act(alpha * sum_k A[b,m,k] * W[b,n,k] + bias[n] + bias2d[m/R, n]) + res_alpha * Res[b,m,n]
+//   C[b,m,n] = gate[(b*M+m)/G, n] * act(alpha * sum_k A[b,m,k] * W[b,n,k] + bias[n] + bias2d[m/R, n])
+//              + res_alpha * Res[b,m,n]
+//
+// (gate: optional AdaLN-Zero gate rows, e.g. Flux gate_msa / gate_mlp per image.)
 //
 // Operand tiles move global -> LDS with `buffer_load_dwordx4 ... lds` (no VGPR
 // round trip, no ds_write).  The buffer descriptor's range check supplies the
@@ -39,18 +42,10 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, bf16_t* lds_wav
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_wave_base, 16, voff, 0, 0, 0);
 }
 
-struct Epi {
-  const bf16_t* bias;
-  const bf16_t* bias2d;
-  int rows_per_bias2d;
-  const bf16_t* R;
-  long ldr;
-  float alpha, res_alpha;
-};
-
 // Apply the epilogue to 4 consecutive columns n..n+3 of row m and store.
 template <bool GLU, int ACT>
-__device__ __forceinline__ void epilogue4(const GemmArgs& p, bf16_t* C, const bf16_t* R, int m, int n, float v[4]) {
+__device__ __forceinline__ void epilogue4(const GemmArgs& p, bf16_t* C, const bf16_t* R, int m, int n, float v[4],
+                                          int b = 0) {
   const bool full = n + 3 < p.N && (p.ldc & 3) == 0 && (p.ldr & 3) == 0;
 #pragma unroll
   for (int e = 0; e < 4; ++e) v[e] *= p.alpha;
@@ -73,10 +68,15 @@ __device__ __forceinline__ void epilogue4(const GemmArgs& p, bf16_t* C, const bf
       for (int e = 0; e < 4 && n + e < p.N; ++e) v[e] += bf2f(b2[n + e]);
     }
   }
+  const bf16_t* gr = p.gate ? p.gate + ((long)b * p.M + m) / p.rows_per_gate * p.gate_stride : nullptr;
   if constexpr (GLU) {
-    const float o0 = v[0] * apply_act<ACT>(v[1]);
-    const float o1 = v[2] * apply_act<ACT>(v[3]);
+    float o0 = v[0] * apply_act<ACT>(v[1]);
+    float o1 = v[2] * apply_act<ACT>(v[3]);
     const int nc = n >> 1;
+    if (gr) {
+      o0 *= bf2f(gr[nc]);
+      o1 *= bf2f(gr[nc + 1]);
+    }
     float r0 = 0.f, r1 = 0.f;
     if (R) {
       r0 = bf2f(R[(long)m * p.ldr + nc]) * p.res_alpha;
@@ -91,6 +91,9 @@ __device__ __forceinline__ void epilogue4(const GemmArgs& p, bf16_t* C, const bf
   } else {
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = apply_act<ACT>(v[e]);
+    if (gr) {
+      for (int e = 0; e < 4 && n + e < p.N; ++e) v[e] *= bf2f(gr[n + e]);
+    }
     if (full) {
       if (R) {
         const uint2_ rr = *reinterpret_cast<const uint2_*>(R + (long)m * p.ldr + n);
@@ -350,7 +353,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm2_kernel(const GemmArgs p, f
           const int n = n0 + wn * TN + j * 32 + 8 * g + 4 * fh;
           if (n >= p.N) continue;
           float v[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-          epilogue4<GLU, ACT>(p, C, R, m, n, v);
+          epilogue4<GLU, ACT>(p, C, R, m, n, v, b);
         }
     }
   }

@@ -20,6 +20,8 @@ struct RowNormArgs {
   long x_stride, out_stride;  // row strides in elements
   float eps;
   float w_offset;           // y = norm(x) * (w + w_offset) + b
+  int rows_per_w;           // >0: w/b advance by w_stride every rows_per_w rows (AdaLN modulation per image)
+  long w_stride;
 };
 void launch_rmsnorm(const RowNormArgs& a, hipStream_t s);
 void launch_layernorm(const RowNormArgs& a, hipStream_t s);
@@ -52,6 +54,10 @@ void launch_bias_act(const bf16_t* x, const bf16_t* bias, const bf16_t* residual
 void launch_rope(bf16_t* x, const int* positions, const float* cos, const float* sin, int T, int H, int Dh,
                  int rot_dim, long tok_stride, int neox, hipStream_t s);
 // Flux 3-axis rope with precomputed per-token (cos, sin) pairs [T, Dh/2].
+// Flux: in-place per-head RMSNorm of q and k (weights optional) + pair RoPE (cos/sin optional, [S, D/2]).
+// x: [rows, >= 2*H*D] with row stride ld; q at column 0, k at column H*D; row r uses rope position r % S.
+void launch_qk_norm_rope(bf16_t* x, long ld, int rows, int S, int H, int D, const bf16_t* qw, const bf16_t* kw,
+                         const float* cs, const float* sn, float eps, hipStream_t s);
 void launch_rope_pairs(bf16_t* x, const float* cos, const float* sin, int B, int T, int H, int Dh, long batch_stride,
                        long tok_stride, hipStream_t s);
 // Scheduler step fused with classifier-free guidance (all fp32 math):
@@ -92,6 +98,10 @@ struct GemmArgs {
   const float* in_scale;
   const float* in_shift;
   int in_act;
+  // AdaLN-Zero gate: out = gate[(b*M + m) / rows_per_gate, n] * epi(...) + residual (v2 kernel only)
+  const bf16_t* gate;
+  long gate_stride;
+  int rows_per_gate;
 };
 void launch_gemm(const GemmArgs& a, hipStream_t s);       // v1: register-staged (supports fused GN gather)
 // v2: LDS-DMA staged, tile configs + split-K (ws: fp32 workspace of gemm2_workspace_bytes, may be null)

@@ -21,10 +21,15 @@ template <int MAXC, bool LAYERNORM>
 __global__ void __launch_bounds__(256) row_norm_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ residual, const bf16_t* __restrict__ w,
     const bf16_t* __restrict__ b, bf16_t* __restrict__ out, bf16_t* __restrict__ residual_out, int rows,
-    int D, long x_stride, long out_stride, float eps, float w_offset) {
+    int D, long x_stride, long out_stride, float eps, float w_offset, int rows_per_w, long w_stride) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
+  if (rows_per_w > 0) {  // per-image modulation rows (AdaLN): w/b = row group of a strided [G, *] tensor
+    const long wo = (long)(row / rows_per_w) * w_stride;
+    if (w) w += wo;
+    if (b) b += wo;
+  }
   const bf16_t* xr = x + (long)row * x_stride;
   uint4_ v[MAXC];
   float sum = 0.f, sumsq = 0.f;
@@ -101,7 +106,8 @@ static void launch_row_norm(const RowNormArgs& a, hipStream_t s) {
   const int chunks = (a.D + 511) / 512;
 #define SHAI_RN(C)                                                                                       \
   row_norm_kernel<C, LN><<<grid, block, 0, s>>>(a.x, a.residual, a.w, a.b, a.out, a.residual_out, a.rows, \
-                                                a.D, a.x_stride, a.out_stride, a.eps, a.w_offset)
+                                                a.D, a.x_stride, a.out_stride, a.eps, a.w_offset, \
+                                                a.rows_per_w, a.w_stride)
   if (chunks <= 1) SHAI_RN(1);
   else if (chunks <= 2) SHAI_RN(2);
   else if (chunks <= 4) SHAI_RN(4);

@@ -1,0 +1,189 @@
+"""Flux.1 text-to-image engine (CLIP-L pooled + T5-XXL + MMDiT + 16-ch VAE).
+
+Replaces the reference's Neuron pipeline (app/flux_model_api.py:94-211,298-328:
+CustomFluxPipeline with the transformer traced as four TP8 sub-graphs on
+NeuronCores 4-11, T5 TP8 on cores 0-7, CLIP/VAE on core 8, and four host
+round-trips per denoising step for the embedders / shape fix-ups).
+
+On MI355X every component lives on the same GPU (or the same TP group): the
+whole model is ~34 GB bf16 against 288 GB of HBM3E.  Per request:
+
+1. CLIP-L pooled + T5-XXL states (once), context_embedder (once).
+2. All AdaLN modulation vectors for ALL steps in one pass (FluxTransformer2DModel.modulations).
+3. Denoising loop: one HIP-graph replay of the full transformer step per
+   step (x_embedder -> 19 dual + 38 single blocks -> norm_out/proj_out), then
+   the fused flow-match Euler update (``ops.sched_step``).  The only per-step
+   host work is copying this step's modulation row into the graph's static
+   input and the replay itself.
+4. 16-channel VAE decode (scaling 0.3611, shift 0.1159), uint8 NHWC on host.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Dict, Optional, Sequence, Tuple
+
+import torch
+
+from .. import ops
+from ..models.clip import CLIPTextConfig, CLIPTextModel
+from ..models.flux import FluxConfig, FluxTransformer2DModel, pack_latents, unpack_latents_nhwc
+from ..models.t5 import T5Config, T5EncoderModel
+from ..models.vae import AutoencoderKLDecoder, VAEConfig
+from ..schedulers import PRED_FLOW, FlowMatchEulerScheduler
+from ..tokenizers import load_tokenizer
+from ..weights import materialize
+
+
+@dataclass
+class FluxPipelineConfig:
+    transformer: FluxConfig = field(default_factory=FluxConfig.dev)
+    clip: CLIPTextConfig = field(default_factory=CLIPTextConfig.clip_l)
+    t5: T5Config = field(default_factory=T5Config.xxl)
+    vae: VAEConfig = field(default_factory=VAEConfig.flux)
+    height: int = 512
+    width: int = 512
+    max_sequence_length: int = 512
+    guidance_scale: float = 3.5
+
+    @staticmethod
+    def dev(height=512, width=512, max_sequence_length=512):
+        return FluxPipelineConfig(height=height, width=width, max_sequence_length=max_sequence_length)
+
+    @staticmethod
+    def schnell(height=512, width=512, max_sequence_length=256):
+        return FluxPipelineConfig(transformer=FluxConfig.schnell(), height=height, width=width,
+                                  max_sequence_length=max_sequence_length, guidance_scale=0.0)
+
+    @staticmethod
+    def tiny():
+        t = FluxConfig.tiny()
+        return FluxPipelineConfig(
+            transformer=t,
+            clip=CLIPTextConfig(vocab_size=1000, hidden_size=t.pooled_projection_dim, intermediate_size=64,
+                                num_hidden_layers=1, num_attention_heads=1, bos_token_id=998, eos_token_id=999),
+            t5=T5Config(vocab_size=500, d_model=t.joint_attention_dim, d_ff=128, num_layers=1, num_heads=1),
+            vae=VAEConfig.tiny(latent_channels=16), height=64, width=64, max_sequence_length=16)
+
+
+class _StepGraph:
+    """HIP graph of one full transformer step for a (B, Nt, h2, w2) bucket."""
+
+    def __init__(self, model: FluxTransformer2DModel, B: int, Nt: int, h2: int, w2: int, device):
+        c = model.cfg
+        self.model = model
+        self.lat = torch.zeros(B, h2 * w2, c.in_channels, dtype=torch.bfloat16, device=device)
+        self.ctx = torch.zeros(B, Nt, c.hidden, dtype=torch.bfloat16, device=device)
+        self.mod = torch.zeros(B, model.mod_layout()[3], dtype=torch.bfloat16, device=device)
+        self.cos, self.sin = model.rope(Nt, h2, w2, device)
+        self.graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm-up: GEMM autotuning happens here, outside capture
+                self._fwd()
+        torch.cuda.current_stream().wait_stream(s)
+        with torch.cuda.graph(self.graph):
+            self.out = self._fwd()
+
+    def _fwd(self):
+        return self.model.forward_step(self.lat, self.ctx, self.mod, self.cos, self.sin)
+
+    def run(self, mod_rows: torch.Tensor) -> torch.Tensor:
+        self.mod.copy_(mod_rows)
+        self.graph.replay()
+        return self.out
+
+
+class FluxEngine:
+    def __init__(self, cfg: Optional[FluxPipelineConfig] = None, device="cuda", model_path: Optional[str] = None,
+                 seed: int = 0, use_graphs: bool = True):
+        self.cfg = cfg or FluxPipelineConfig.dev()
+        self.device = torch.device(device)
+        c = self.cfg
+        with torch.device(self.device):
+            self.clip = CLIPTextModel(c.clip)
+            self.t5 = T5EncoderModel(c.t5)
+            self.transformer = FluxTransformer2DModel(c.transformer)
+            self.vae = AutoencoderKLDecoder(c.vae)
+        materialize(self.clip, self.device, model_path, "text_encoder", seed)
+        materialize(self.t5, self.device, model_path, "text_encoder_2", seed + 1)
+        materialize(self.transformer, self.device, model_path, "transformer", seed + 2)
+        materialize(self.vae, self.device, model_path, "vae", seed + 3)
+        self.weights = self.transformer._shai_weights
+        self.clip_tok = load_tokenizer(model_path, subfolder="tokenizer", vocab_size=c.clip.vocab_size,
+                                       bos_id=c.clip.bos_token_id, eos_id=c.clip.eos_token_id,
+                                       pad_id=c.clip.pad_token_id, model_max_length=c.clip.max_position_embeddings)
+        self.t5_tok = load_tokenizer(model_path, subfolder="tokenizer_2", vocab_size=c.t5.vocab_size, bos_id=None,
+                                     eos_id=c.t5.eos_token_id, pad_id=c.t5.pad_token_id,
+                                     model_max_length=c.max_sequence_length)
+        self.scheduler = FlowMatchEulerScheduler()
+        self.use_graphs = use_graphs and self.device.type == "cuda"
+        self._graphs: Dict[Tuple[int, int, int, int], _StepGraph] = {}
+
+    # ------------------------------------------------------------------ pieces
+    @torch.no_grad()
+    def encode_prompts(self, prompts: Sequence[str], max_sequence_length: Optional[int] = None):
+        """-> (pooled CLIP-L [B, 768], T5 states [B, Nt, 4096]); T5 runs unmasked over the padded
+        sequence, as FluxPipeline does."""
+        L = max_sequence_length or self.cfg.max_sequence_length
+        ct = self.clip_tok(list(prompts), max_length=self.cfg.clip.max_position_embeddings, padding="max_length",
+                           truncation=True, return_tensors="pt")
+        _, pooled = self.clip(ct["input_ids"].to(self.device), output_pooled=True)
+        tt = self.t5_tok(list(prompts), max_length=L, padding="max_length", truncation=True, return_tensors="pt")
+        states = self.t5(tt["input_ids"].to(self.device))
+        return pooled.contiguous(), states
+
+    def _graph_for(self, B, Nt, h2, w2) -> _StepGraph:
+        key = (B, Nt, h2, w2)
+        g = self._graphs.get(key)
+        if g is None:
+            g = _StepGraph(self.transformer, B, Nt, h2, w2, self.device)
+            self._graphs[key] = g
+        return g
+
+    @torch.no_grad()
+    def generate(self, prompts: Sequence[str], num_inference_steps: int = 28, guidance_scale: Optional[float] = None,
+                 height: Optional[int] = None, width: Optional[int] = None, seed: Optional[int] = None,
+                 max_sequence_length: Optional[int] = None, output: str = "uint8") -> torch.Tensor:
+        c = self.cfg
+        H, W = height or c.height, width or c.width
+        assert H % 16 == 0 and W % 16 == 0, "Flux needs H, W multiples of 16"
+        B = len(prompts)
+        h, w = H // 8, W // 8
+        h2, w2 = h // 2, w // 2
+        g_scale = c.guidance_scale if guidance_scale is None else guidance_scale
+        pooled, states = self.encode_prompts(prompts, max_sequence_length)
+        Nt = states.shape[1]
+        tr = self.transformer
+        ctx = tr.context_embedder(states)
+        steps = self.scheduler.steps(num_inference_steps, image_seq_len=h2 * w2)
+        # modulations for every (step, image) row, hoisted out of the loop
+        t_rows = torch.tensor([sp.t / 1000.0 for sp in steps], device=self.device).repeat_interleave(B)
+        g_rows = (torch.full_like(t_rows, g_scale) if c.transformer.guidance_embeds else None)
+        mods = tr.modulations(t_rows, g_rows, pooled.repeat(len(steps), 1))
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(int(seed) if seed is not None else int(time.time_ns() % (2 ** 31)))
+        noise = torch.randn(B, c.vae.latent_channels, h, w, generator=gen, device=self.device, dtype=torch.float32)
+        lat = pack_latents(noise).to(torch.bfloat16).contiguous()
+        if self.use_graphs:
+            g = self._graph_for(B, Nt, h2, w2)
+            g.ctx.copy_(ctx)
+            g.lat.copy_(lat)
+            lat = g.lat
+            for i, sp in enumerate(steps):
+                out = g.run(mods[i * B:(i + 1) * B])
+                ops.sched_step(out, lat, False, 1.0, PRED_FLOW, 0.0, 0.0, sp.dt)
+        else:
+            cos, sin = tr.rope(Nt, h2, w2, self.device)
+            for i, sp in enumerate(steps):
+                out = tr.forward_step(lat, ctx, mods[i * B:(i + 1) * B], cos, sin)
+                ops.sched_step(out, lat, False, 1.0, PRED_FLOW, 0.0, 0.0, sp.dt)
+        img = self.vae(unpack_latents_nhwc(lat, h, w).contiguous())
+        if output == "tensor":
+            return img
+        return AutoencoderKLDecoder.to_uint8(img).cpu()
+
+    def __call__(self, prompt, num_inference_steps: int = 28, **kw):
+        prompts = [prompt] if isinstance(prompt, str) else list(prompt)
+        return self.generate(prompts, num_inference_steps, **kw)

@@ -123,6 +123,43 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return y.view(*lead, Nout)
 
 
+def gemm_into(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias=None, act=None, residual=None, gate=None,
+              rows_per_gate: int = 1, alpha: float = 1.0, res_alpha: float = 1.0, glu: bool = False) -> torch.Tensor:
+    """out = gate[row // rows_per_gate] * act(alpha * x @ w^T + bias) + res_alpha * residual, written into ``out``.
+
+    x / out / residual are 2D [M, *] or 3D [B, M, *] views whose rows may be strided
+    (e.g. the text / image halves of a joint-sequence buffer); the row index used
+    for ``gate`` is the flattened b * M + m (AdaLN-Zero gates per image)."""
+    if not _gpu(x):
+        return ref.gemm_into(x, w, out, bias, act, residual, gate, rows_per_gate, alpha, res_alpha, glu)
+    _K().gemm(x, w, out, bias, None, 1, residual, float(alpha), float(res_alpha), act_id(act), bool(glu), gate,
+              int(rows_per_gate))
+    return out
+
+
+def layernorm_mod(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, rows_per_mod: int,
+                  eps: float = 1e-6, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """AdaLN: LayerNorm(x) (no affine) * (1 + scale[r // rows_per_mod]) + shift[r // rows_per_mod].
+    scale / shift: [G, D] (may be strided column chunks of one modulation tensor)."""
+    if not _gpu(x):
+        y = ref.layernorm_mod(x, scale, shift, rows_per_mod, eps)
+        return out.copy_(y) if out is not None else y
+    x2 = x if x.dim() == 2 else x.reshape(-1, x.shape[-1])
+    y = out if out is not None else torch.empty(x2.shape, dtype=x.dtype, device=x.device)
+    _K().layernorm_mod(x2, scale, shift, y if y.dim() == 2 else y.view(-1, x.shape[-1]), int(rows_per_mod),
+                       float(eps))
+    return y.view(x.shape) if out is None else out
+
+
+def qk_norm_rope(x: torch.Tensor, q_w, k_w, cos, sin, heads: int, head_dim: int, seq: int, eps: float = 1e-6):
+    """In place on a packed QKV buffer x [rows, >= 2*H*D]: per-head RMSNorm of q and k (weights optional) and
+    pair RoPE with cos/sin [seq, D/2] (row r uses position r % seq)."""
+    if not _gpu(x):
+        return ref.qk_norm_rope(x, q_w, k_w, cos, sin, heads, head_dim, seq, eps)
+    _K().qk_norm_rope(x, q_w, k_w, cos, sin, int(heads), int(head_dim), int(seq), float(eps))
+    return x
+
+
 def bmm(a: torch.Tensor, w: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
     """Batched C[b] = alpha * a[b] @ w[b]^T (a [B,M,K], w [B,N,K])."""
     if not _gpu(a):
@@ -165,7 +202,8 @@ def attention(q, k, v, scale: Optional[float] = None, causal: bool = False, caus
     D = q.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if not _gpu(q):
-        return ref.attention(q, k, v, scale, causal, causal_offset, kv_lens, q_lens, bias)
+        o = ref.attention(q, k, v, scale, causal, causal_offset, kv_lens, q_lens, bias)
+        return out.copy_(o) if out is not None else o
     o = out if out is not None else torch.empty(q.shape, dtype=q.dtype, device=q.device)
     _K().flash_attn(q, k, v, o, float(scale), bool(causal), int(causal_offset), _i32(kv_lens), _i32(q_lens), bias,
                     None)

@@ -99,6 +99,53 @@ def linear(x, w, bias=None, act=None, residual=None, glu=False, alpha=1.0, res_a
     return y.to(x.dtype)
 
 
+def gate_rows(y, gate, rows_per_gate):
+    """y [..., M, N] * gate[(b*M + m) // rows_per_gate] (flattened row index)."""
+    N = y.shape[-1]
+    y2 = y.reshape(-1, N)
+    idx = torch.arange(y2.shape[0], device=y.device) // rows_per_gate
+    return (y2 * gate.float()[idx]).reshape(y.shape)
+
+
+def gemm_into(x, w, out, bias=None, act=None, residual=None, gate=None, rows_per_gate=1, alpha=1.0, res_alpha=1.0,
+              glu=False):
+    y = linear(x, w, bias, act, None, glu, alpha).float()
+    if gate is not None:
+        y = gate_rows(y, gate, rows_per_gate)
+    if residual is not None:
+        y = y + res_alpha * residual.float()
+    out.copy_(y.to(out.dtype))
+    return out
+
+
+def layernorm_mod(x, scale, shift, rows_per_mod, eps):
+    D = x.shape[-1]
+    xf = x.float().reshape(-1, D)
+    y = torch.nn.functional.layer_norm(xf, (D,), eps=eps)
+    idx = torch.arange(xf.shape[0], device=x.device) // rows_per_mod
+    y = y * (1 + scale.float()[idx]) + shift.float()[idx]
+    return y.reshape(x.shape).to(x.dtype)
+
+
+def qk_norm_rope(x, q_w, k_w, cos, sin, H, D, S, eps):
+    """In place on x [rows, >= 2*H*D]: RMSNorm per head on q (cols [0, HD)) and k (cols [HD, 2HD)), then pair RoPE
+    with row r at position r % S."""
+    rows = x.shape[0]
+    pos = torch.arange(rows, device=x.device) % S
+    for j, w in enumerate((q_w, k_w)):
+        t = x[:, j * H * D:(j + 1) * H * D].float().reshape(rows, H, D)
+        if w is not None:
+            t = t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+        if cos is not None:
+            c = cos[pos].view(rows, 1, D // 2)
+            s_ = sin[pos].view(rows, 1, D // 2)
+            a, b = t[..., 0::2].clone(), t[..., 1::2].clone()
+            t[..., 0::2] = a * c - b * s_
+            t[..., 1::2] = b * c + a * s_
+        x[:, j * H * D:(j + 1) * H * D] = t.reshape(rows, H * D).to(x.dtype)
+    return x
+
+
 def unpack_conv_weight(w_packed, cin, kh, kw):
     cout = w_packed.shape[0]
     return w_packed.reshape(cout, kh, kw, cin).permute(0, 3, 1, 2).contiguous()

@@ -124,3 +124,36 @@ def test_t5_server():
     rep = base64.b64decode(c.post("/benchmark", json={"n_runs": 2, "max_new_tokens": 16, "prompt": "x"}).json()
                            ["report"]).decode()
     assert rep.startswith("RESULT FOR benchmark:t5 on mi355x with 16 output tokens:")
+
+
+def test_flux_servers():
+    from PIL import Image
+    from shai_amd.serving import flux_api
+    e = env(app="flux", model_id="black-forest-labs/FLUX.1-dev")
+    eng = flux_api.build_engine(e)
+    c = TestClient(flux_api.create_app(engine=eng, env=e))
+    assert c.get("/health").json() == {"message": "pod0 is healthy"}
+    assert c.get("/readiness").json() == {"message": "pod0 is ready"}
+    r = c.post("/generate", json={"prompt": "a cat", "num_inference_steps": 2})
+    assert r.status_code == 200
+    j = r.json()
+    assert set(j) == {"image", "execution_time"} and isinstance(j["execution_time"], float)
+    im = Image.open(io.BytesIO(base64.b64decode(j["image"])))
+    assert max(im.size) <= 128
+    bad = c.post("/generate", json={"prompt": "a cat", "num_inference_steps": -1})
+    assert bad.status_code == 500 and bad.json()["detail"].startswith("Image serialization failed: ")
+    g = TestClient(flux_api.create_gradio_app(engine=eng, env=e))
+    assert g.get("/health").json() == {"message": "pod0is healthy"}
+    j = g.post("/text2img", json={"prompt": "a dog", "num_inference_steps": 2}).json()
+    assert isinstance(j["execution_time"], str)
+    assert Image.open(io.BytesIO(base64.b64decode(j["image"]))).size == (64, 64)
+    assert g.get("/serve").status_code == 200
+
+
+def test_flux_engine_tiny_deterministic():
+    import torch
+    from shai_amd.engines.flux import FluxEngine, FluxPipelineConfig
+    eng = FluxEngine(FluxPipelineConfig.tiny(), device="cpu")
+    a = eng.generate(["a red fox"], 3, seed=7)
+    b = eng.generate(["a red fox"], 3, seed=7)
+    assert a.shape == (1, 64, 64, 3) and a.dtype == torch.uint8 and torch.equal(a, b)
