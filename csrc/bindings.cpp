@@ -70,7 +70,53 @@ int max_splits_for(const shai::GemmArgs& g) {
   return s;
 }
 
+constexpr int kSkinnyCfg = 1000;  // Choice.cfg of the skinny streaming kernel (csrc/kernels/gemv.hip)
+
+// Persistent per-device ticket array for the skinny kernel's split-K fixup (self re-arming).
+// Allocated on first eager use; while a graph is being captured without it the kernel
+// runs with a single K group (no tickets needed).
+int* skinny_tickets(bool may_alloc) {
+  static std::mutex mu;
+  static std::unordered_map<int, int*> per_dev;
+  int dev = 0;
+  hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = per_dev.find(dev);
+  if (it != per_dev.end()) return it->second;
+  if (!may_alloc) return nullptr;
+  int* p = nullptr;
+  SHAI_CHECK(hipMalloc(&p, sizeof(int) * 65536) == hipSuccess, "hipMalloc tickets failed");
+  SHAI_CHECK(hipMemset(p, 0, sizeof(int) * 65536) == hipSuccess, "hipMemset tickets failed");
+  hipDeviceSynchronize();
+  per_dev[dev] = p;
+  return p;
+}
+
+bool stream_capturing() {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  hipStreamIsCapturing(stream(), &cs);
+  return cs != hipStreamCaptureStatusNone;
+}
+
+void launch_skinny_choice(const shai::GemmArgs& g, const Tensor& like) {
+  int* tickets = skinny_tickets(!stream_capturing());
+  shai::GemmArgs a = g;
+  Tensor ws;
+  float* wsp = nullptr;
+  const size_t bytes = shai::skinny_workspace_bytes(a);
+  if (bytes > 0 && tickets != nullptr && a.N / 32 <= 65536) {
+    ws = at::empty({(long)(bytes / sizeof(float))}, like.options().dtype(at::kFloat));
+    wsp = ws.data_ptr<float>();
+  }
+  if (wsp == nullptr) tickets = nullptr;
+  shai::launch_skinny(a, wsp, tickets, stream());
+}
+
 void launch_choice(const shai::GemmArgs& g, const Tensor& like, Choice c) {
+  if (c.cfg == kSkinnyCfg) {
+    launch_skinny_choice(g, like);
+    return;
+  }
   Tensor ws;
   float* wsp = nullptr;
   if (c.splits > 1) {
@@ -97,6 +143,7 @@ Choice tune(const shai::GemmArgs& g_real, const Tensor& like) {
   std::vector<Choice> cands;
   for (int c = 0; c < shai::gemm2_num_cfgs(); ++c)
     for (int s = 1; s <= ms; s *= 2) cands.push_back({c, s});
+  if (shai::skinny_supported(g)) cands.push_back({kSkinnyCfg, 1});
   hipStream_t st = stream();
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
@@ -142,7 +189,8 @@ void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_
       std::lock_guard<std::mutex> lk(g_tune_mu);
       g_tuned[key] = c;
     } else {
-      shai::gemm2_plan(g, &c.cfg, &c.splits);
+      if (shai::skinny_supported(g)) c = Choice{kSkinnyCfg, 1};
+      else shai::gemm2_plan(g, &c.cfg, &c.splits);
     }
   }
   launch_choice(g, like, c);
@@ -152,6 +200,10 @@ std::vector<std::string> gemm_tuning_table() {
   std::lock_guard<std::mutex> lk(g_tune_mu);
   std::vector<std::string> out;
   for (auto& kv : g_tuned) {
+    if (kv.second.cfg == kSkinnyCfg) {
+      out.push_back(kv.first + " -> skinny");
+      continue;
+    }
     int bm, bn;
     shai::gemm2_cfg_info(kv.second.cfg, &bm, &bn);
     out.push_back(kv.first + " -> " + std::to_string(bm) + "x" + std::to_string(bn) + " splitk=" +
@@ -335,7 +387,8 @@ void groupnorm_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, 
 // a: [M, K] or [B, M, K]; w: [N, K] or [B, N, K]; c: [M, N'] or [B, M, N'] (N' = N or N/2 for glu)
 void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tensor>& bias,
           const optional<Tensor>& bias2d, int64_t rows_per_bias2d, const optional<Tensor>& residual, double alpha,
-          double res_alpha, int64_t act, bool glu, const optional<Tensor>& gate, int64_t rows_per_gate) {
+          double res_alpha, int64_t act, bool glu, const optional<Tensor>& gate, int64_t rows_per_gate,
+          int64_t force_cfg) {
   check_rows(a, "a");
   check_rows(w, "w");
   check_bf16(c, "c");
@@ -391,6 +444,15 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
   g.act = act;
   g.glu = glu;
   const long a_bytes = (batched ? (long)a.size(0) * a.stride(0) : (long)g.M * g.lda) * 2;
+  if (force_cfg >= 0) {  // tests / tools: bypass the tuner (1000 = skinny kernel)
+    if (force_cfg == kSkinnyCfg) {
+      SHAI_CHECK(shai::skinny_supported(g), "skinny kernel does not support this problem");
+    } else {
+      SHAI_CHECK(force_cfg < shai::gemm2_num_cfgs(), "bad force_cfg");
+    }
+    launch_choice(g, a, Choice{(int)force_cfg, 1});
+    return;
+  }
   run_gemm(g, a, a_bytes, (long)g.N * g.ldw * 2, 0);
 }
 
@@ -663,7 +725,8 @@ int64_t gemm_tuning_import(const std::vector<std::string>& entries) {
     if (eq == std::string::npos || cm == std::string::npos || cm < eq) continue;
     const int cfg = atoi(e.substr(eq + 1, cm - eq - 1).c_str());
     const int sp = atoi(e.substr(cm + 1).c_str());
-    if (cfg < 0 || cfg >= shai::gemm2_num_cfgs() || sp < 1) continue;
+    if ((cfg < 0 || cfg >= shai::gemm2_num_cfgs()) && cfg != kSkinnyCfg) continue;
+    if (sp < 1) continue;
     g_tuned[e.substr(0, eq)] = Choice{cfg, sp};
     ++n;
   }
@@ -685,7 +748,7 @@ TORCH_LIBRARY(shai, m) {
   m.def("layernorm(Tensor x, Tensor? w, Tensor? b, Tensor(a!) out, Tensor? residual, Tensor(b!)? residual_out, float eps) -> ()");
   m.def("groupnorm_stats(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!) partials, Tensor(b!) scale, Tensor(c!) shift, int G, float eps) -> ()");
   m.def("groupnorm_apply(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, bool silu) -> ()");
-  m.def("gemm(Tensor a, Tensor w, Tensor(a!) c, Tensor? bias, Tensor? bias2d, int rows_per_bias2d, Tensor? residual, float alpha, float res_alpha, int act, bool glu, Tensor? gate=None, int rows_per_gate=1) -> ()");
+  m.def("gemm(Tensor a, Tensor w, Tensor(a!) c, Tensor? bias, Tensor? bias2d, int rows_per_bias2d, Tensor? residual, float alpha, float res_alpha, int act, bool glu, Tensor? gate=None, int rows_per_gate=1, int force_cfg=-1) -> ()");
   m.def("layernorm_mod(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, int rows_per_mod, float eps) -> ()");
   m.def("qk_norm_rope(Tensor(a!) x, Tensor? q_w, Tensor? k_w, Tensor? cos, Tensor? sin, int H, int D, int S, float eps) -> ()");
   m.def("conv2d(Tensor x, Tensor? x2, Tensor w, Tensor(a!) out, Tensor? bias, Tensor? bias2d, Tensor? residual, Tensor? in_scale, Tensor? in_shift, int in_act, int kh, int kw, int stride, int pad, bool upsample, int act, float res_alpha) -> ()");

@@ -110,6 +110,11 @@ size_t gemm2_workspace_bytes(const GemmArgs& a);
 void gemm2_plan(const GemmArgs& a, int* cfg, int* splits);
 void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStream_t s);
 int gemm2_num_cfgs();
+// skinny (decode-shaped, M <= 32) streaming GEMM; tickets: >= N/32 zero-initialised ints (self re-arming)
+bool skinny_supported(const GemmArgs& a);
+int skinny_kgroups(const GemmArgs& a);
+size_t skinny_workspace_bytes(const GemmArgs& a);
+void launch_skinny(const GemmArgs& a, float* ws, int* tickets, hipStream_t s);
 void gemm2_cfg_info(int cfg, int* bm, int* bn);
 
 // ---------------------------------------------------------------- attention

@@ -124,7 +124,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 
 def gemm_into(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias=None, act=None, residual=None, gate=None,
-              rows_per_gate: int = 1, alpha: float = 1.0, res_alpha: float = 1.0, glu: bool = False) -> torch.Tensor:
+              rows_per_gate: int = 1, alpha: float = 1.0, res_alpha: float = 1.0, glu: bool = False,
+              force_cfg: int = -1) -> torch.Tensor:
     """out = gate[row // rows_per_gate] * act(alpha * x @ w^T + bias) + res_alpha * residual, written into ``out``.
 
     x / out / residual are 2D [M, *] or 3D [B, M, *] views whose rows may be strided
@@ -133,7 +134,7 @@ def gemm_into(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias=None, ac
     if not _gpu(x):
         return ref.gemm_into(x, w, out, bias, act, residual, gate, rows_per_gate, alpha, res_alpha, glu)
     _K().gemm(x, w, out, bias, None, 1, residual, float(alpha), float(res_alpha), act_id(act), bool(glu), gate,
-              int(rows_per_gate))
+              int(rows_per_gate), int(force_cfg))
     return out
 
 
