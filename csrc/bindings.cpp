@@ -72,26 +72,6 @@ int max_splits_for(const shai::GemmArgs& g) {
 
 constexpr int kSkinnyCfg = 1000;  // Choice.cfg of the skinny streaming kernel (csrc/kernels/gemv.hip)
 
-// Persistent per-device ticket array for the skinny kernel's split-K fixup (self re-arming).
-// Allocated on first eager use; while a graph is being captured without it the kernel
-// runs with a single K group (no tickets needed).
-int* skinny_tickets(bool may_alloc) {
-  static std::mutex mu;
-  static std::unordered_map<int, int*> per_dev;
-  int dev = 0;
-  hipGetDevice(&dev);
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = per_dev.find(dev);
-  if (it != per_dev.end()) return it->second;
-  if (!may_alloc) return nullptr;
-  int* p = nullptr;
-  SHAI_CHECK(hipMalloc(&p, sizeof(int) * 65536) == hipSuccess, "hipMalloc tickets failed");
-  SHAI_CHECK(hipMemset(p, 0, sizeof(int) * 65536) == hipSuccess, "hipMemset tickets failed");
-  hipDeviceSynchronize();
-  per_dev[dev] = p;
-  return p;
-}
-
 bool stream_capturing() {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   hipStreamIsCapturing(stream(), &cs);
@@ -99,17 +79,14 @@ bool stream_capturing() {
 }
 
 void launch_skinny_choice(const shai::GemmArgs& g, const Tensor& like) {
-  int* tickets = skinny_tickets(!stream_capturing());
-  shai::GemmArgs a = g;
   Tensor ws;
   float* wsp = nullptr;
-  const size_t bytes = shai::skinny_workspace_bytes(a);
-  if (bytes > 0 && tickets != nullptr && a.N / 32 <= 65536) {
+  const size_t bytes = shai::skinny_workspace_bytes(g);
+  if (bytes > 0) {
     ws = at::empty({(long)(bytes / sizeof(float))}, like.options().dtype(at::kFloat));
     wsp = ws.data_ptr<float>();
   }
-  if (wsp == nullptr) tickets = nullptr;
-  shai::launch_skinny(a, wsp, tickets, stream());
+  shai::launch_skinny(g, wsp, stream());
 }
 
 void launch_choice(const shai::GemmArgs& g, const Tensor& like, Choice c) {
@@ -388,7 +365,7 @@ void groupnorm_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, 
 void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tensor>& bias,
           const optional<Tensor>& bias2d, int64_t rows_per_bias2d, const optional<Tensor>& residual, double alpha,
           double res_alpha, int64_t act, bool glu, const optional<Tensor>& gate, int64_t rows_per_gate,
-          int64_t force_cfg) {
+          int64_t force_cfg, double rms_eps) {
   check_rows(a, "a");
   check_rows(w, "w");
   check_bf16(c, "c");
@@ -444,6 +421,32 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
   g.act = act;
   g.glu = glu;
   const long a_bytes = (batched ? (long)a.size(0) * a.stride(0) : (long)g.M * g.lda) * 2;
+  if (rms_eps >= 0) {
+    // RMSNorm(a) folded in (norm gain pre-multiplied into w): fused into the skinny kernel for
+    // decode-shaped problems, otherwise an explicit unweighted RMSNorm pass feeds the GEMM.
+    SHAI_CHECK(!batched, "folded RMSNorm needs a 2D activation");
+    if (shai::skinny_supported(g) && force_cfg < 0) {
+      g.rms = 1;
+      g.rms_eps = (float)rms_eps;
+      launch_choice(g, a, Choice{kSkinnyCfg, 1});
+      return;
+    }
+    Tensor xn = at::empty({g.M, g.K}, a.options());
+    shai::RowNormArgs r{};
+    r.x = cptr(a);
+    r.out = mptr(xn);
+    r.rows = g.M;
+    r.D = g.K;
+    r.x_stride = g.lda;
+    r.out_stride = g.K;
+    r.eps = rms_eps;
+    SHAI_CHECK(g.K % 8 == 0 && g.K <= 8192, "folded RMSNorm: K must be a multiple of 8 and <= 8192");
+    shai::launch_rmsnorm(r, stream());
+    g.A = cptr(xn);
+    g.lda = g.K;
+    run_gemm(g, xn, (long)g.M * g.K * 2, (long)g.N * g.ldw * 2, 0);
+    return;
+  }
   if (force_cfg >= 0) {  // tests / tools: bypass the tuner (1000 = skinny kernel)
     if (force_cfg == kSkinnyCfg) {
       SHAI_CHECK(shai::skinny_supported(g), "skinny kernel does not support this problem");
@@ -680,6 +683,29 @@ void rope(const Tensor& x, const Tensor& positions, const Tensor& cos, const Ten
                     x.size(1), x.size(2), rot_dim, x.stride(0), neox, stream());
 }
 
+void rope_qkv_cache(const Tensor& qkv, const Tensor& positions, const Tensor& cos, const Tensor& sin,
+                    const Tensor& k_cache, const Tensor& v_cache, const Tensor& slots, int64_t H, int64_t Hkv) {
+  check_bf16(qkv, "qkv");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_i32(positions, "positions");
+  check_i32(slots, "slots");
+  check_f32(cos, "cos");
+  check_f32(sin, "sin");
+  SHAI_CHECK(qkv.dim() == 2 && qkv.stride(0) % 8 == 0, "qkv must be [T, (H + 2Hkv) * D] with 16B-aligned rows");
+  SHAI_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous() && k_cache.size(1) == Hkv &&
+                 k_cache.size(2) == 64,
+             "caches must be contiguous [blocks, Hkv, 64, D]");
+  const int D = k_cache.size(3);
+  SHAI_CHECK(D % 16 == 0 && qkv.size(1) == (H + 2 * Hkv) * D, "qkv width / head dim mismatch");
+  SHAI_CHECK(cos.size(-1) == D / 2, "cos/sin must be [max_pos, D/2] (full-dim NeoX rotation)");
+  const int T = qkv.size(0);
+  SHAI_CHECK(positions.numel() == T && slots.numel() == T, "positions / slots must have T entries");
+  shai::launch_rope_qkv_cache(mptr(qkv), qkv.stride(0), positions.data_ptr<int>(), cos.data_ptr<float>(),
+                              sin.data_ptr<float>(), mptr(k_cache), mptr(v_cache), slots.data_ptr<int>(), T, H, Hkv,
+                              D, stream());
+}
+
 void rope_pairs(const Tensor& x, const Tensor& cos, const Tensor& sin) {
   check_bf16(x, "x");
   check_f32(cos, "cos");
@@ -748,7 +774,7 @@ TORCH_LIBRARY(shai, m) {
   m.def("layernorm(Tensor x, Tensor? w, Tensor? b, Tensor(a!) out, Tensor? residual, Tensor(b!)? residual_out, float eps) -> ()");
   m.def("groupnorm_stats(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!) partials, Tensor(b!) scale, Tensor(c!) shift, int G, float eps) -> ()");
   m.def("groupnorm_apply(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, bool silu) -> ()");
-  m.def("gemm(Tensor a, Tensor w, Tensor(a!) c, Tensor? bias, Tensor? bias2d, int rows_per_bias2d, Tensor? residual, float alpha, float res_alpha, int act, bool glu, Tensor? gate=None, int rows_per_gate=1, int force_cfg=-1) -> ()");
+  m.def("gemm(Tensor a, Tensor w, Tensor(a!) c, Tensor? bias, Tensor? bias2d, int rows_per_bias2d, Tensor? residual, float alpha, float res_alpha, int act, bool glu, Tensor? gate=None, int rows_per_gate=1, int force_cfg=-1, float rms_eps=-1.0) -> ()");
   m.def("layernorm_mod(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, int rows_per_mod, float eps) -> ()");
   m.def("qk_norm_rope(Tensor(a!) x, Tensor? q_w, Tensor? k_w, Tensor? cos, Tensor? sin, int H, int D, int S, float eps) -> ()");
   m.def("conv2d(Tensor x, Tensor? x2, Tensor w, Tensor(a!) out, Tensor? bias, Tensor? bias2d, Tensor? residual, Tensor? in_scale, Tensor? in_shift, int in_act, int kh, int kw, int stride, int pad, bool upsample, int act, float res_alpha) -> ()");
@@ -759,6 +785,7 @@ TORCH_LIBRARY(shai, m) {
   m.def("bias_act(Tensor x, Tensor? bias, Tensor? residual, Tensor(a!) out, int act, float alpha) -> ()");
   m.def("rope(Tensor(a!) x, Tensor positions, Tensor cos, Tensor sin, int rot_dim, bool neox) -> ()");
   m.def("rope_pairs(Tensor(a!) x, Tensor cos, Tensor sin) -> ()");
+  m.def("rope_qkv_cache(Tensor(a!) qkv, Tensor positions, Tensor cos, Tensor sin, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor slots, int H, int Hkv) -> ()");
   m.def("sched_step(Tensor model_out, Tensor(a!) latents, bool cfg, float guidance, int pred_type, float a_t, float a_prev, float dt) -> ()");
   m.def("softmax_(Tensor(a!) x, float scale) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out) -> ()");
@@ -783,6 +810,7 @@ TORCH_LIBRARY_IMPL(shai, CUDA, m) {
   m.impl("bias_act", &bias_act);
   m.impl("rope", &rope);
   m.impl("rope_pairs", &rope_pairs);
+  m.impl("rope_qkv_cache", &rope_qkv_cache);
   m.impl("sched_step", &sched_step);
   m.impl("softmax_", &softmax_);
   m.impl("embedding", &embedding);

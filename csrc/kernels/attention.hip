@@ -295,8 +295,12 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
     const bf16_t* vc = p.v_cache + ((long)phys * p.Hkv + hk) * 64 * D;
     for (int id = tid; id < 64 * CPR; id += nthr) {
       const int row = id / CPR, ch = id % CPR;
-      const uint4_ kv = *reinterpret_cast<const uint4_*>(kc + row * D + ch * 8);
-      const uint4_ vv = *reinterpret_cast<const uint4_*>(vc + row * D + ch * 8);
+      // rows past the context are never-written cache memory: zero them, since P = 0 times a
+      // NaN bit pattern would still poison the P.V sum
+      const bool ok = bi * 64 + row < ctx;
+      const uint4_ zero = {0u, 0u, 0u, 0u};
+      const uint4_ kv = ok ? *reinterpret_cast<const uint4_*>(kc + row * D + ch * 8) : zero;
+      const uint4_ vv = ok ? *reinterpret_cast<const uint4_*>(vc + row * D + ch * 8) : zero;
       *reinterpret_cast<uint4_*>(sK + row * D + ((ch ^ (row & (CPR - 1))) << 3)) = kv;
       *reinterpret_cast<uint4_*>(sV + row * D + ch * 8) = vv;
     }
@@ -403,6 +407,69 @@ void launch_kv_write(const bf16_t* k, const bf16_t* v, bf16_t* k_cache, bf16_t* 
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   kv_write_kernel<<<(int)blocks, 256, 0, s>>>(k, v, k_cache, v_cache, slot_mapping, T, Hkv, D, k_ts, v_ts);
+}
+
+// Fused decode/prefill prologue on the packed QKV projection [T, (H + 2 Hkv) * D] (row stride ld):
+// NeoX RoPE on q (in place) and k, then k and v scattered into the paged caches [blocks, Hkv, 64, D].
+// One item = 16 elements: for q/k heads, 8 elements of each rotation half; for v heads, a 16-element
+// copy.  Replaces rope(q) + rope(k) + kv_write (3 launches and an extra pass over k).
+__global__ void rope_qkv_cache_kernel(bf16_t* __restrict__ qkv, long ld, const int* __restrict__ pos,
+                                      const float* __restrict__ cs, const float* __restrict__ sn,
+                                      bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, const int* __restrict__ slots,
+                                      int T, int H, int Hkv, int D) {
+  const int half = D >> 1;
+  const int per_head = D / 16;
+  const int heads = H + 2 * Hkv;
+  const long total = (long)T * heads * per_head;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % per_head);
+    const int hh = (int)((i / per_head) % heads);
+    const int t = (int)(i / ((long)per_head * heads));
+    bf16_t* row = qkv + (long)t * ld;
+    const int slot = slots[t];
+    if (hh >= H + Hkv) {  // v head: copy 16 elements
+      if (slot < 0) continue;
+      const int h = hh - H - Hkv;
+      const bf16_t* src = row + (long)hh * D + c * 16;
+      const long dst = (((long)(slot >> 6) * Hkv + h) * 64 + (slot & 63)) * D + c * 16;
+      *reinterpret_cast<uint4_*>(vc + dst) = *reinterpret_cast<const uint4_*>(src);
+      *reinterpret_cast<uint4_*>(vc + dst + 8) = *reinterpret_cast<const uint4_*>(src + 8);
+      continue;
+    }
+    bf16_t* xh = row + (long)hh * D;
+    const int p = pos[t];
+    float a[8], b[8];
+    unpack8(*reinterpret_cast<const uint4_*>(xh + 8 * c), a);
+    unpack8(*reinterpret_cast<const uint4_*>(xh + half + 8 * c), b);
+    const float* cp = cs + (long)p * half + 8 * c;
+    const float* sp = sn + (long)p * half + 8 * c;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float co = cp[e], si = sp[e];
+      const float x0 = a[e], x1 = b[e];
+      a[e] = x0 * co - x1 * si;
+      b[e] = x1 * co + x0 * si;
+    }
+    const uint4_ ua = pack8(a), ub = pack8(b);
+    if (hh < H) {
+      *reinterpret_cast<uint4_*>(xh + 8 * c) = ua;
+      *reinterpret_cast<uint4_*>(xh + half + 8 * c) = ub;
+    } else if (slot >= 0) {
+      const int h = hh - H;
+      const long dst = (((long)(slot >> 6) * Hkv + h) * 64 + (slot & 63)) * D;
+      *reinterpret_cast<uint4_*>(kc + dst + 8 * c) = ua;
+      *reinterpret_cast<uint4_*>(kc + dst + half + 8 * c) = ub;
+    }
+  }
+}
+
+void launch_rope_qkv_cache(bf16_t* qkv, long ld, const int* pos, const float* cos, const float* sin, bf16_t* k_cache,
+                           bf16_t* v_cache, const int* slots, int T, int H, int Hkv, int D, hipStream_t s) {
+  const long total = (long)T * (H + 2 * Hkv) * (D / 16);
+  long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  rope_qkv_cache_kernel<<<(int)blocks, 256, 0, s>>>(qkv, ld, pos, cos, sin, k_cache, v_cache, slots, T, H, Hkv, D);
 }
 
 }  // namespace shai

@@ -377,6 +377,14 @@ __global__ void gemm_splitk_reduce(const GemmArgs p, const float* __restrict__ w
         for (int e = 0; e < 4 && n + e < p.N; ++e) v[e] += src[e];
       }
     }
+    if (p.rms) {  // folded RMSNorm: per-row sum of squares partials follow the [splits][M][N] block
+      const float* ss = ws + (long)splits * p.M * p.N;
+      float t = 0.f;
+      for (int s = 0; s < splits; ++s) t += ss[(long)s * p.M + m];
+      const float r = rsqrtf(t / p.K + p.rms_eps);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] *= r;
+    }
     epilogue4<GLU, ACT>(p, p.C, p.residual, m, n, v);
   }
 }
@@ -521,6 +529,24 @@ void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStre
     const bool fast = (a.Cin % 64) == 0 && (a.A2 == nullptr || (a.Cin1 % 64) == 0);
     if (fast) launch_all<true, true>(a, ws, cfg, splits, s);
     else launch_all<true, false>(a, ws, cfg, splits, s);
+  }
+}
+
+// Split-K fold + full epilogue for fp32 partials laid out [splits][M][N] (also used by the skinny kernel).
+void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipStream_t s) {
+  if (a.glu) {
+    if (a.act == ACT_SILU) launch_reduce<true, ACT_SILU>(a, ws, splits, s);
+    else if (a.act == ACT_GELU_TANH) launch_reduce<true, ACT_GELU_TANH>(a, ws, splits, s);
+    else launch_reduce<true, ACT_GELU>(a, ws, splits, s);
+    return;
+  }
+  switch (a.act) {
+    case ACT_SILU: launch_reduce<false, ACT_SILU>(a, ws, splits, s); break;
+    case ACT_GELU: launch_reduce<false, ACT_GELU>(a, ws, splits, s); break;
+    case ACT_GELU_TANH: launch_reduce<false, ACT_GELU_TANH>(a, ws, splits, s); break;
+    case ACT_QUICK_GELU: launch_reduce<false, ACT_QUICK_GELU>(a, ws, splits, s); break;
+    case ACT_RELU: launch_reduce<false, ACT_RELU>(a, ws, splits, s); break;
+    default: launch_reduce<false, ACT_NONE>(a, ws, splits, s); break;
   }
 }
 

@@ -1,42 +1,62 @@
-// Skinny GEMM for decode-shaped problems (M <= 32 activation rows, e.g. LLM
-// decode batches, Flux/SD modulation GEMMs with few rows):
+// Skinny GEMM for decode-shaped problems (M <= 32 activation rows: LLM decode
+// batches, per-request modulation GEMMs):
 //
 //   C[m, n] = act(alpha * sum_k X[m, k] * W[n, k] + bias[n]) (+ res_alpha * R[m, n]),  GLU optional
 //
-// The problem is purely weight-bandwidth bound (W is read once, X is tiny and
-// L2-resident), so the kernel is organised around streaming W at HBM rate:
+// Purely weight-bandwidth bound, so the design goal is "keep enough bytes of W
+// in flight per CU to cover HBM latency" (Little's law: ~8 TB/s x ~2 us over 256
+// CUs is ~64 KB per CU), with every global load fully coalesced:
 //
-// * A workgroup owns 32 output columns n (= 32 rows of W) and a K range; its 8
-//   waves split that range.  Each wave runs 32x32x16 bf16 MFMAs with W as the A
-//   operand (rows n) and X^T as B (columns m; rows m >= M read as zero).
-// * K permutation: a lane (row r = lane & 31, half h = lane >> 5) loads 64
-//   contiguous bytes of its W row per 64-wide K step (4 x dwordx4, nontemporal
-//   so W does not evict X from L2) and feeds them to 4 MFMAs; X fragments use
-//   the same permuted K order, so the dot products are unchanged.  The next K
-//   step's loads are issued before the current step's MFMAs (register double
-//   buffer).
-// * Cross-wave reduction through LDS (padded, conflict-free), then either the
-//   fused epilogue directly (one K group) or, when more parallelism is needed
-//   to fill 256 CUs, a split over KG workgroups: each writes its fp32 partial
-//   tile, and the LAST workgroup to arrive (atomic ticket per tile; it resets
-//   the ticket, so the kernel is HIP-graph replay safe) sums the partials and
-//   runs the epilogue -- one launch, no separate reduce kernel.
+// * Workgroup = 4 waves, tile = 64 W rows (n) x all M <= 32 rows of X, walking
+//   its K range in 64-wide steps.  Each step's W tile (8 KB) and X tile (4 KB)
+//   move global -> LDS with buffer_load ... lds DMA (8 full 128 B rows per wave
+//   instruction; range check = zero fill for X rows >= M / W rows >= N), through
+//   a SK_STAGES-deep ring (6 x 12 KB), so 5 steps are always in flight while one
+//   is consumed.  Counted vmcnt + one s_barrier per step (same protocol as the
+//   3-stage GEMM in gemm_lds.hip, generalised to S stages).
+// * Wave w consumes the 16-wide K slice [16w, 16w + 16) of each step: two
+//   32x32x16 MFMAs (W rows 0-31 and 32-63 as A, X^T as B).  XOR-swizzled LDS
+//   image (source-side swizzle, conflict-free ds_read_b128).
+// * Cross-wave reduction through LDS, fused epilogue.  When N/64 tiles cannot
+//   fill the chip, K is additionally split over KG workgroups writing fp32
+//   partials that the shared split-K fold (gemm_lds.hip) reduces + epilogues.
 #include "common.h"
 #include "launchers.h"
 
 namespace shai {
 
 typedef __bf16 bf16x8s __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void sk_lds_void;
 
-constexpr int SK_WAVES = 8;
-constexpr int SK_PAD = 33;
+constexpr int SK_BN = 64;       // W rows per workgroup
+constexpr int SK_BK = 64;       // K per step
+constexpr int SK_WAVES = 4;
+constexpr int SK_STAGES = 6;
+constexpr int SK_STAGE_ELEMS = (SK_BN + 32) * SK_BK;   // W tile then X tile
+constexpr int SK_PER = 3;       // DMA instructions per wave per step (2 for W, 1 for X)
+constexpr uint32_t SK_OOB = 0x80000000u;
+
+__device__ __forceinline__ int sk_swz(int row, int ch) { return row * SK_BK + ((ch ^ ((row >> 1) & 7)) << 3); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sk_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+template <int N>
+__device__ __forceinline__ void sk_wait_upto(int pending) {
+  // s_waitcnt needs an immediate: allow `pending` DMA groups (of SK_PER loads) to stay in flight
+  if constexpr (N == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (pending >= N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N * SK_PER) : "memory");
+    else sk_wait_upto<N - 1>(pending);
+  }
+}
 
 template <bool GLU, int ACT>
-__device__ __forceinline__ void skinny_store(const GemmArgs& p, int n0, int m, int nl, float v0, float v1) {
-  // v0 = value at column n0 + nl, v1 = value at n0 + nl + 1 (used by GLU only)
-  const int n = n0 + nl;
+__device__ __forceinline__ void sk_store(const GemmArgs& p, int n, int m, float v0, float v1) {
+  if (n >= p.N) return;
   if constexpr (GLU) {
-    if (n >= p.N) return;
     const float a = v0 * p.alpha + (p.bias ? bf2f(p.bias[n]) : 0.f);
     const float g = v1 * p.alpha + (p.bias ? bf2f(p.bias[n + 1]) : 0.f);
     float o = a * apply_act<ACT>(g);
@@ -44,176 +64,201 @@ __device__ __forceinline__ void skinny_store(const GemmArgs& p, int n0, int m, i
     if (p.residual) o += bf2f(p.residual[(long)m * p.ldr + nc]) * p.res_alpha;
     p.C[(long)m * p.ldc + nc] = f2bf(o);
   } else {
-    if (n >= p.N) return;
     float o = apply_act<ACT>(v0 * p.alpha + (p.bias ? bf2f(p.bias[n]) : 0.f));
     if (p.residual) o += bf2f(p.residual[(long)m * p.ldr + n]) * p.res_alpha;
     p.C[(long)m * p.ldc + n] = f2bf(o);
   }
 }
 
-template <bool GLU, int ACT>
-__global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmArgs p, float* __restrict__ ws,
-                                                                    int* __restrict__ tickets, int kg_steps) {
-  __shared__ float red[SK_WAVES][32][SK_PAD];
-  __shared__ int last;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int tile = blockIdx.x;
-  const int kg = blockIdx.y, KG = gridDim.y;
-  const int n0 = tile * 32;
-  const int r = lane & 31, h = lane >> 5;
-
-  // K steps (64 wide) of this workgroup, split over the waves
-  const int ksteps = p.K >> 6;
-  const int g0 = kg * kg_steps, g1 = min(ksteps, g0 + kg_steps);
-  const int per = (g1 - g0 + SK_WAVES - 1) / SK_WAVES;
-  const int s0 = g0 + w * per, s1 = min(g1, s0 + per);
-
-  const bf16_t* wrow = p.W + (long)min(n0 + r, p.N - 1) * p.ldw + 32 * h;
-  // rows m >= M re-read row M-1: they only feed output columns m >= M, which are never stored
-  const bf16_t* xrow = p.A + (long)min(r, p.M - 1) * p.lda + 32 * h;
-  float16_ acc = {};
-
-  // Batched issue: all loads of U consecutive K steps go out back to back (U x 8
-  // dwordx4 per lane, 32 KB per wave in flight), then their MFMAs run.  Other
-  // waves' loads overlap this wave's (short) MFMA phase.  A software-pipelined
-  // ping-pong variant was defeated by the compiler's register reuse.
-  constexpr int U = 4;
-  for (int s = s0; s < s1; s += U) {
-    uint4_ wv[U][4], xv[U][4];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (s + u < s1) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          wv[u][j] = __builtin_nontemporal_load(reinterpret_cast<const uint4_*>(wrow + ((s + u) << 6) + 8 * j));
-          xv[u][j] = *reinterpret_cast<const uint4_*>(xrow + ((s + u) << 6) + 8 * j);
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (s + u < s1) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8s, wv[u][j]),
-                                                         __builtin_bit_cast(bf16x8s, xv[u][j]), acc, 0, 0, 0);
-      }
-    }
-  }
-  // C layout: lane column m = lane & 31; rows nl = (i & 3) + 8 * (i >> 2) + 4 * h
-#pragma unroll
-  for (int i = 0; i < 16; ++i) red[w][(i & 3) + 8 * (i >> 2) + 4 * h][r] = acc[i];
-  __syncthreads();
-
+// Epilogue over a reduced 64 (n) x 32 (m) tile held as get(nl, m).
+template <bool GLU, int ACT, typename Get>
+__device__ __forceinline__ void sk_epilogue(const GemmArgs& p, int n0, Get get) {
   const int tid = threadIdx.x;
-  if (KG == 1) {
-    if constexpr (GLU) {
-      const int m = tid >> 4, nl = (tid & 15) * 2;  // 512 threads = 32 m x 16 pairs
-      if (m < p.M) {
-        float v0 = 0.f, v1 = 0.f;
-#pragma unroll
-        for (int q = 0; q < SK_WAVES; ++q) {
-          v0 += red[q][nl][m];
-          v1 += red[q][nl + 1][m];
-        }
-        skinny_store<GLU, ACT>(p, n0, m, nl, v0, v1);
-      }
-    } else {
-#pragma unroll
-      for (int it = 0; it < 2; ++it) {
-        const int idx = tid + it * 512;
-        const int m = idx >> 5, nl = idx & 31;
-        if (m < p.M) {
-          float v = 0.f;
-#pragma unroll
-          for (int q = 0; q < SK_WAVES; ++q) v += red[q][nl][m];
-          skinny_store<GLU, ACT>(p, n0, m, nl, v, 0.f);
-        }
-      }
-    }
-    return;
-  }
-
-  // ---- split over KG workgroups: write this group's partial, last arrival reduces
-  float* part = ws + ((long)kg * gridDim.x + tile) * 1024;
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int idx = tid + it * 512;
-    const int m = idx >> 5, nl = idx & 31;
-    float v = 0.f;
-#pragma unroll
-    for (int q = 0; q < SK_WAVES; ++q) v += red[q][nl][m];
-    part[idx] = v;
-  }
-  __threadfence();
-  __syncthreads();
-  if (tid == 0) {
-    const int t = atomicAdd(&tickets[tile], 1);
-    last = (t == KG - 1);
-    if (last) tickets[tile] = 0;  // re-arm for the next launch / graph replay
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
   if constexpr (GLU) {
-    const int m = tid >> 4, nl = (tid & 15) * 2;
-    if (m < p.M) {
-      float v0 = 0.f, v1 = 0.f;
-      for (int q = 0; q < KG; ++q) {
-        const float* pp = ws + ((long)q * gridDim.x + tile) * 1024 + m * 32 + nl;
-        v0 += __builtin_nontemporal_load(pp);
-        v1 += __builtin_nontemporal_load(pp + 1);
-      }
-      skinny_store<GLU, ACT>(p, n0, m, nl, v0, v1);
+    // 32 pairs x 32 m = 1024 outputs, 4 per thread; consecutive threads -> consecutive pairs
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int idx = tid + it * 256;
+      const int m = idx >> 5, pr = idx & 31;
+      if (m < p.M) sk_store<GLU, ACT>(p, n0 + 2 * pr, m, get(2 * pr, m), get(2 * pr + 1, m));
     }
   } else {
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int idx = tid + it * 512;
-      const int m = idx >> 5, nl = idx & 31;
-      if (m < p.M) {
-        float v = 0.f;
-        for (int q = 0; q < KG; ++q) v += __builtin_nontemporal_load(ws + ((long)q * gridDim.x + tile) * 1024 + idx);
-        skinny_store<GLU, ACT>(p, n0, m, nl, v, 0.f);
+    for (int it = 0; it < 8; ++it) {
+      const int idx = tid + it * 256;
+      const int m = idx >> 6, nl = idx & 63;
+      if (m < p.M) sk_store<GLU, ACT>(p, n0 + nl, m, get(nl, m), 0.f);
+    }
+  }
+}
+
+template <bool GLU, int ACT, bool RMS>
+__global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmArgs p, float* __restrict__ ws,
+                                                                    int kg_steps) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t sk_smem[];
+  __shared__ float ss_red[SK_WAVES][64];
+  __shared__ float rstd_s[32];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tile = blockIdx.x, kg = blockIdx.y, KG = gridDim.y;
+  const int n0 = tile * SK_BN;
+
+  const int ksteps = (p.K + SK_BK - 1) / SK_BK;
+  const int t0 = kg * kg_steps;
+  const int nk = max(0, min(ksteps, t0 + kg_steps) - t0);
+
+  const __amdgpu_buffer_rsrc_t rW = sk_rsrc(p.W, (uint32_t)min((long)p.N * p.ldw * 2, 0x7fffffffL));
+  const __amdgpu_buffer_rsrc_t rX = sk_rsrc(p.A, (uint32_t)min((long)p.M * p.lda * 2, 0x7fffffffL));
+
+  // DMA geometry: a wave instruction fills 8 LDS rows x 128 B, lane-linear; the lane at
+  // LDS chunk position lpos fetches global chunk lpos ^ swz(row).
+  const int lrow = lane >> 3, lpos = lane & 7;
+  int wr[2], wc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    wr[j] = (w * 2 + j) * 8 + lrow;
+    wc[j] = lpos ^ ((wr[j] >> 1) & 7);
+  }
+  const int xr = w * 8 + lrow;
+  const int xc = lpos ^ ((xr >> 1) & 7);
+
+  auto stage = [&](int buf, int step) {
+    bf16_t* sw = sk_smem + buf * SK_STAGE_ELEMS;
+    bf16_t* sx = sw + SK_BN * SK_BK;
+    const int k0 = (t0 + step) * SK_BK;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wr[j], k = k0 + wc[j] * 8;
+      const uint32_t off = (n < p.N && k < p.K) ? (uint32_t)(((long)n * p.ldw + k) * 2) : SK_OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (sk_lds_void*)(sw + (w * 2 + j) * 8 * SK_BK), 16, off, 0, 0, 0);
+    }
+    const int k = k0 + xc * 8;
+    const uint32_t off = (xr < p.M && k < p.K) ? (uint32_t)(((long)xr * p.lda + k) * 2) : SK_OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (sk_lds_void*)(sx + w * 8 * SK_BK), 16, off, 0, 0, 0);
+  };
+
+  float16_ acc0 = {}, acc1 = {};
+  float ss = 0.f;  // folded RMSNorm: this lane's share of sum_k X[m, k]^2 (the 4 waves x 2 halves
+                   // together read every X element of every step exactly once)
+  const int fr = lane & 31, fh = lane >> 5;
+  const int ch = 2 * w + fh;  // this lane's 8-element chunk of the step's K range
+#pragma unroll
+  for (int i = 0; i < SK_STAGES - 1; ++i)
+    if (i < nk) stage(i, i);
+  int buf = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    sk_wait_upto<SK_STAGES - 2>(min(SK_STAGES - 2, nk - 1 - kt));
+    __builtin_amdgcn_s_barrier();
+    if (kt + SK_STAGES - 1 < nk) {
+      const int nb = buf == 0 ? SK_STAGES - 1 : buf - 1;  // buffer of step kt-1: every wave is past it
+      stage(nb, kt + SK_STAGES - 1);
+    }
+    const bf16_t* sw = sk_smem + buf * SK_STAGE_ELEMS;
+    const bf16_t* sx = sw + SK_BN * SK_BK;
+    const bf16x8s xf = *reinterpret_cast<const bf16x8s*>(sx + sk_swz(fr, ch));
+    const bf16x8s w0 = *reinterpret_cast<const bf16x8s*>(sw + sk_swz(fr, ch));
+    const bf16x8s w1 = *reinterpret_cast<const bf16x8s*>(sw + sk_swz(32 + fr, ch));
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, xf, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, xf, acc1, 0, 0, 0);
+    if constexpr (RMS) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = (float)xf[e];
+        ss += f * f;
       }
     }
+    buf = buf == SK_STAGES - 1 ? 0 : buf + 1;
+  }
+  if constexpr (RMS) ss_red[w][lane] = ss;
+
+  // ---- cross-wave reduction: red[w][nl][m] (padded), reusing the stage ring
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(sk_smem);
+  constexpr int RP = 33;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int nl = (i & 3) + 8 * (i >> 2) + 4 * fh;
+    red[(w * SK_BN + nl) * RP + fr] = acc0[i];
+    red[(w * SK_BN + 32 + nl) * RP + fr] = acc1[i];
+  }
+  __syncthreads();
+  auto row_ss = [&](int m) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < SK_WAVES; ++q) t += ss_red[q][m] + ss_red[q][m + 32];
+    return t;
+  };
+  if constexpr (RMS) {
+    if (KG == 1 && tid < 32) rstd_s[tid] = rsqrtf(row_ss(tid) / p.K + p.rms_eps);
+    __syncthreads();
+  }
+  auto wsum = [&](int nl, int m) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < SK_WAVES; ++q) v += red[(q * SK_BN + nl) * RP + m];
+    if constexpr (RMS) {
+      if (KG == 1) v *= rstd_s[m];
+    }
+    return v;
+  };
+  if (KG == 1) {
+    sk_epilogue<GLU, ACT>(p, n0, wsum);
+    return;
+  }
+  if constexpr (RMS) {  // row sum-of-squares partials for the fold (one tile per K group writes them)
+    if (tile == 0 && tid < p.M) ws[(long)KG * p.M * p.N + (long)kg * p.M + tid] = row_ss(tid);
+  }
+  // ---- split-K over workgroups: fp32 partials [kg][M][N]; launch_splitk_epilogue folds them.
+  // (An in-kernel last-arrival fixup needs a device-scope release per workgroup, i.e. an
+  // L2 writeback on this chip, and measured ~5x slower than the separate fold.)
+  float* part = ws + (long)kg * p.M * p.N;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int idx = tid + it * 256;
+    const int m = idx >> 6, nl = idx & 63;
+    if (m < p.M && n0 + nl < p.N) part[(long)m * p.N + n0 + nl] = wsum(nl, m);
   }
 }
 
 // ---------------------------------------------------------------------------- host side
 bool skinny_supported(const GemmArgs& a) {
-  return !a.conv && (a.batch <= 1) && a.M >= 1 && a.M <= 32 && a.K % 64 == 0 && a.N % 32 == 0 &&
-         a.bias2d == nullptr && a.gate == nullptr && a.in_scale == nullptr && (a.lda % 8) == 0 && (a.ldw % 8) == 0;
+  return !a.conv && (a.batch <= 1) && a.M >= 1 && a.M <= 32 && a.K % 8 == 0 && a.N % 2 == 0 &&
+         a.bias2d == nullptr && a.gate == nullptr && a.in_scale == nullptr && (a.lda % 8) == 0 &&
+         (a.ldw % 8) == 0 && (long)a.N * a.ldw * 2 < 0x7fffffffL;
 }
 
-// Number of K groups: enough workgroups to cover the CUs twice, each wave >= 2 K steps.
+// K groups: enough workgroups for ~2 per CU, each group >= 2 pipeline depths of K steps.
 int skinny_kgroups(const GemmArgs& a) {
-  const int tiles = a.N / 32, ksteps = a.K / 64;
+  const int tiles = (a.N + SK_BN - 1) / SK_BN, ksteps = (a.K + SK_BK - 1) / SK_BK;
   int kg = 1;
-  while (tiles * kg < 512 && ksteps / (kg * 2) >= 2 * SK_WAVES) kg *= 2;
+  while (tiles * kg < 512 && ksteps / (kg * 2) >= SK_STAGES) kg *= 2;
   return kg;
 }
 
 size_t skinny_workspace_bytes(const GemmArgs& a) {
   const int kg = skinny_kgroups(a);
-  return kg > 1 ? (size_t)kg * (a.N / 32) * 1024 * sizeof(float) : 0;
+  return kg > 1 ? ((size_t)kg * a.M * a.N + (a.rms ? (size_t)kg * a.M : 0)) * sizeof(float) : 0;
 }
 
-void launch_skinny(const GemmArgs& a, float* ws, int* tickets, hipStream_t s) {
-  const int kg = (ws != nullptr && tickets != nullptr) ? skinny_kgroups(a) : 1;
-  const int ksteps = a.K / 64;
+void launch_skinny(const GemmArgs& a, float* ws, hipStream_t s) {
+  const int kg = ws != nullptr ? skinny_kgroups(a) : 1;
+  const int ksteps = (a.K + SK_BK - 1) / SK_BK;
   const int kg_steps = (ksteps + kg - 1) / kg;
-  dim3 grid(a.N / 32, kg), block(SK_WAVES * 64);
-#define SK(G, A) skinny_gemm_kernel<G, A><<<grid, block, 0, s>>>(a, ws, tickets, kg_steps)
-#define SK_ACT(G)                                    \
-  switch (a.act) {                                   \
-    case ACT_SILU: SK(G, ACT_SILU); break;           \
-    case ACT_GELU: SK(G, ACT_GELU); break;           \
-    case ACT_GELU_TANH: SK(G, ACT_GELU_TANH); break; \
+  dim3 grid((a.N + SK_BN - 1) / SK_BN, kg), block(SK_WAVES * 64);
+  const size_t lds = (size_t)SK_STAGES * SK_STAGE_ELEMS * sizeof(bf16_t);
+#define SK(G, A)                                                               \
+  do {                                                                         \
+    if (a.rms) skinny_gemm_kernel<G, A, true><<<grid, block, lds, s>>>(a, ws, kg_steps);  \
+    else skinny_gemm_kernel<G, A, false><<<grid, block, lds, s>>>(a, ws, kg_steps);       \
+  } while (0)
+#define SK_ACT(G)                                      \
+  switch (a.act) {                                     \
+    case ACT_SILU: SK(G, ACT_SILU); break;             \
+    case ACT_GELU: SK(G, ACT_GELU); break;             \
+    case ACT_GELU_TANH: SK(G, ACT_GELU_TANH); break;   \
     case ACT_QUICK_GELU: SK(G, ACT_QUICK_GELU); break; \
-    case ACT_RELU: SK(G, ACT_RELU); break;           \
-    default: SK(G, ACT_NONE); break;                 \
+    case ACT_RELU: SK(G, ACT_RELU); break;             \
+    default: SK(G, ACT_NONE); break;                   \
   }
   if (a.glu) {
     SK_ACT(true)
@@ -222,6 +267,7 @@ void launch_skinny(const GemmArgs& a, float* ws, int* tickets, hipStream_t s) {
   }
 #undef SK_ACT
 #undef SK
+  if (kg > 1) launch_splitk_epilogue(a, ws, kg, s);
 }
 
 }  // namespace shai

@@ -58,6 +58,9 @@ void launch_rope(bf16_t* x, const int* positions, const float* cos, const float*
 // x: [rows, >= 2*H*D] with row stride ld; q at column 0, k at column H*D; row r uses rope position r % S.
 void launch_qk_norm_rope(bf16_t* x, long ld, int rows, int S, int H, int D, const bf16_t* qw, const bf16_t* kw,
                          const float* cs, const float* sn, float eps, hipStream_t s);
+// Llama/Mistral: NeoX RoPE on q (in place) and k + paged KV-cache write of k, v from the packed QKV rows.
+void launch_rope_qkv_cache(bf16_t* qkv, long ld, const int* pos, const float* cos, const float* sin, bf16_t* k_cache,
+                           bf16_t* v_cache, const int* slots, int T, int H, int Hkv, int D, hipStream_t s);
 void launch_rope_pairs(bf16_t* x, const float* cos, const float* sin, int B, int T, int H, int Dh, long batch_stride,
                        long tok_stride, hipStream_t s);
 // Scheduler step fused with classifier-free guidance (all fp32 math):
@@ -102,6 +105,10 @@ struct GemmArgs {
   const bf16_t* gate;
   long gate_stride;
   int rows_per_gate;
+  // RMSNorm folded into the GEMM (skinny kernel / split-K fold only): C = rstd[m] * (A W^T) ... with
+  // rstd[m] = rsqrt(mean_k A[m, k]^2 + rms_eps); the norm gain is pre-multiplied into W's columns.
+  int rms;
+  float rms_eps;
 };
 void launch_gemm(const GemmArgs& a, hipStream_t s);       // v1: register-staged (supports fused GN gather)
 // v2: LDS-DMA staged, tile configs + split-K (ws: fp32 workspace of gemm2_workspace_bytes, may be null)
@@ -110,11 +117,12 @@ size_t gemm2_workspace_bytes(const GemmArgs& a);
 void gemm2_plan(const GemmArgs& a, int* cfg, int* splits);
 void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStream_t s);
 int gemm2_num_cfgs();
-// skinny (decode-shaped, M <= 32) streaming GEMM; tickets: >= N/32 zero-initialised ints (self re-arming)
+void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipStream_t s);
+// skinny (decode-shaped, M <= 32) streaming GEMM; ws: skinny_workspace_bytes (fp32 split-K partials)
 bool skinny_supported(const GemmArgs& a);
 int skinny_kgroups(const GemmArgs& a);
 size_t skinny_workspace_bytes(const GemmArgs& a);
-void launch_skinny(const GemmArgs& a, float* ws, int* tickets, hipStream_t s);
+void launch_skinny(const GemmArgs& a, float* ws, hipStream_t s);
 void gemm2_cfg_info(int cfg, int* bm, int* bn);
 
 // ---------------------------------------------------------------- attention

@@ -77,10 +77,15 @@ def _chain_hash(prev: int, toks: Sequence[int]) -> int:
 
 
 def sample(logits: torch.Tensor, temps: torch.Tensor, top_k: torch.Tensor, top_p: torch.Tensor,
-           gen: Optional[torch.Generator] = None) -> torch.Tensor:
-    """Temperature / top-k / top-p sampling; rows with temperature 0 are greedy."""
+           gen: Optional[torch.Generator] = None, all_greedy: Optional[bool] = None) -> torch.Tensor:
+    """Temperature / top-k / top-p sampling; rows with temperature 0 are greedy (an all-greedy batch
+    skips the sort / multinomial path entirely)."""
     lf = logits.float()
     greedy = lf.argmax(-1)
+    if all_greedy is None:
+        all_greedy = bool((temps <= 0).all())
+    if all_greedy:
+        return greedy
     V = lf.shape[-1]
     kmax = int(top_k.max().item()) if top_k.numel() else 0
     K = V if kmax <= 0 or kmax > V or bool((top_k <= 0).any()) else kmax
@@ -151,6 +156,7 @@ class LLMEngine:
         with torch.device(self.device):
             self.model = LlamaForCausalLM(cfg)
         materialize(self.model, self.device, model_path, None, seed)
+        self.model.fold_norms()  # before any graph capture (re-folded lazily after a later load)
         self.weights = self.model._shai_weights
         self.max_num_seqs = max_num_seqs
         self.max_model_len = min(max_model_len, cfg.max_position_embeddings)
@@ -288,7 +294,8 @@ class LLMEngine:
         temps = torch.tensor([s.params.temperature for s in seqs], dtype=torch.float32, device=d)
         tk = torch.tensor([s.params.top_k for s in seqs], dtype=torch.int64, device=d)
         tpp = torch.tensor([s.params.top_p for s in seqs], dtype=torch.float32, device=d)
-        toks = sample(logits, temps, tk, tpp, self.gen).tolist()
+        toks = sample(logits, temps, tk, tpp, self.gen,
+                      all_greedy=all(s.params.temperature <= 0 for s in seqs)).tolist()
         now = time.perf_counter()
         for s, tok in zip(seqs, toks):
             s.output.append(int(tok))

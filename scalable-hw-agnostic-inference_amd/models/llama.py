@@ -140,16 +140,12 @@ class LlamaAttention(nn.Module):
         self.hd = cfg.head_dim
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
 
-    def forward(self, x, batch: Batch, k_cache, v_cache, cos, sin, residual=None):
+    def forward(self, x, batch: Batch, k_cache, v_cache, cos, sin, residual=None, rms_eps=None):
         T = x.shape[0]
-        qkv = self.qkv_proj(x)  # [T, (h + 2hk) * hd]
+        qkv = self.qkv_proj(x, rms_eps=rms_eps)  # [T, (h + 2hk) * hd]
         h, hk, hd = self.h, self.hk, self.hd
+        ops.rope_qkv_cache(qkv, batch.positions, cos, sin, k_cache, v_cache, batch.slots, h, hk)
         q = qkv[:, : h * hd].view(T, h, hd)
-        k = qkv[:, h * hd:(h + hk) * hd].view(T, hk, hd)
-        v = qkv[:, (h + hk) * hd:].view(T, hk, hd)
-        ops.rope(q, batch.positions, cos, sin)
-        ops.rope(k, batch.positions, cos, sin)
-        ops.kv_write(k, v, k_cache, v_cache, batch.slots)
         if batch.is_prefill:
             o = ops.paged_attention(q.view(batch.B, batch.S, h, hd), k_cache, v_cache, batch.block_table,
                                     batch.ctx_lens, batch.q_lens, self.scale, causal=True).view(T, h * hd)
@@ -165,8 +161,8 @@ class LlamaMLP(nn.Module):
         self.gate_up_proj = GLUParallelLinear(cfg.hidden_size, cfg.intermediate_size, act="silu")
         self.down_proj = RowParallelLinear(cfg.intermediate_size, cfg.hidden_size, bias=False)
 
-    def forward(self, x, residual=None):
-        return self.down_proj(self.gate_up_proj(x), residual=residual)
+    def forward(self, x, residual=None, rms_eps=None):
+        return self.down_proj(self.gate_up_proj(x, rms_eps=rms_eps), residual=residual)
 
 
 class LlamaDecoderLayer(nn.Module):
@@ -177,7 +173,11 @@ class LlamaDecoderLayer(nn.Module):
         self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         self.mlp = LlamaMLP(cfg)
 
-    def forward(self, x, batch, kc, vc, cos, sin):
+    def forward(self, x, batch, kc, vc, cos, sin, folded: bool = False):
+        if folded:  # norm gains live in the qkv / gate_up weights; RMS scaling fused into those GEMMs
+            eps = self.input_layernorm.eps
+            x = self.self_attn(x, batch, kc, vc, cos, sin, residual=x, rms_eps=eps)
+            return self.mlp(x, residual=x, rms_eps=self.post_attention_layernorm.eps)
         x = self.self_attn(self.input_layernorm(x), batch, kc, vc, cos, sin, residual=x)
         return self.mlp(self.post_attention_layernorm(x), residual=x)
 
@@ -191,6 +191,28 @@ class LlamaForCausalLM(nn.Module):
         self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps)
         self.lm_head = ParallelLMHead(cfg.vocab_size, cfg.hidden_size)
         self._rope = None
+        self._folded = False
+
+    @torch.no_grad()
+    def fold_norms(self):
+        """Pre-multiply every RMSNorm gain into the columns of the GEMM that consumes it
+        (input_layernorm -> qkv_proj, post_attention_layernorm -> gate_up_proj, norm -> lm_head)
+        and reset the gains to 1.  The forward then feeds the raw residual stream to those GEMMs
+        with ``rms_eps`` set: on the GPU the per-row 1/rms is computed from the activation tiles
+        already streaming through the decode GEMM, so the two norm kernels per layer disappear."""
+        def fold(lin_w, norm):
+            lin_w.copy_((lin_w.float() * norm.weight.float()[None, :]).to(lin_w.dtype))
+            norm.weight.fill_(1.0)
+        for layer in self.layers:
+            fold(layer.self_attn.qkv_proj.weight, layer.input_layernorm)
+            fold(layer.mlp.gate_up_proj.weight, layer.post_attention_layernorm)
+        fold(self.lm_head.weight, self.norm)
+        self._folded = True
+
+    def load_state_dict(self, *args, **kwargs):
+        r = super().load_state_dict(*args, **kwargs)
+        self._folded = False   # fresh (unfolded) weights: fold again before the next forward
+        return r
 
     @property
     def kv_heads_local(self) -> int:
@@ -203,14 +225,15 @@ class LlamaForCausalLM(nn.Module):
 
     def forward(self, batch: Batch, kv_caches: List[tuple]) -> torch.Tensor:
         """Returns logits [B, V] for each sequence's last token of this step."""
+        if not self._folded:
+            self.fold_norms()
         cos, sin = self.rope(batch.input_ids.device)
         x = self.embed_tokens(batch.input_ids)
         for layer, (kc, vc) in zip(self.layers, kv_caches):
-            x = layer(x, batch, kc, vc, cos, sin)
+            x = layer(x, batch, kc, vc, cos, sin, folded=True)
         if batch.is_prefill:
             x = x.index_select(0, batch.last_index)
-        x = self.norm(x)
-        return self.lm_head.logits(x)
+        return self.lm_head.logits(x, rms_eps=self.norm.eps)
 
     def convert_hf_state_dict(self, sd: dict) -> dict:
         from .attention import merge_linear_keys

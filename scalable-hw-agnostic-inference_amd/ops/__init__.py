@@ -101,13 +101,17 @@ def groupnorm(x, gamma, beta, groups, eps, silu=False):
 # ----------------------------------------------------------------------------- GEMM / conv
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act=None,
            residual: Optional[torch.Tensor] = None, glu: bool = False, alpha: float = 1.0,
-           res_alpha: float = 1.0) -> torch.Tensor:
+           res_alpha: float = 1.0, rms_eps: Optional[float] = None) -> torch.Tensor:
     """y = act(alpha * x @ w^T + bias) (+ res_alpha * residual).
 
     glu=True: ``w`` rows are interleaved (value_i, gate_i) pairs and the output
     has N/2 columns: value * act(gate) (SwiGLU / GEGLU fused in the epilogue).
+    rms_eps: x is RMS-normalised first (unweighted: the norm gain must already be
+    folded into w's columns); on the GPU this is fused into the decode GEMM.
     """
     if not _gpu(x):
+        if rms_eps is not None:
+            x = ref.rmsnorm(x, None, rms_eps)[0]
         return ref.linear(x, w, bias, act, residual, glu, alpha, res_alpha)
     K = x.shape[-1]
     N = w.shape[0]
@@ -119,7 +123,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     Nout = N // 2 if glu else N
     y = torch.empty(x2.shape[0], Nout, dtype=x.dtype, device=x.device)
     r2 = residual.reshape(-1, Nout) if residual is not None else None
-    _K().gemm(x2, w, y, bias, None, 1, r2, float(alpha), float(res_alpha), act_id(act), bool(glu))
+    _K().gemm(x2, w, y, bias, None, 1, r2, float(alpha), float(res_alpha), act_id(act), bool(glu), None, 1, -1,
+              float(rms_eps) if rms_eps is not None else -1.0)
     return y.view(*lead, Nout)
 
 
@@ -260,6 +265,23 @@ def rope(x, positions, cos, sin, rot_dim: Optional[int] = None, neox: bool = Tru
         return ref.rope(x, positions, cos, sin, rot, neox)
     _K().rope(x, _i32(positions), cos, sin, int(rot), bool(neox))
     return x
+
+
+def rope_qkv_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, heads: int, kv_heads: int):
+    """Packed QKV rows [T, (H + 2Hkv) * D]: NeoX RoPE on q in place, rotated k and v written to the paged
+    caches [blocks, Hkv, 64, D] at ``slots`` (-1 = skip).  One fused kernel on the GPU."""
+    T = qkv.shape[0]
+    D = k_cache.shape[-1]
+    if not _gpu(qkv):
+        q = qkv[:, : heads * D].view(T, heads, D)
+        k = qkv[:, heads * D:(heads + kv_heads) * D].view(T, kv_heads, D)
+        v = qkv[:, (heads + kv_heads) * D:].view(T, kv_heads, D)
+        ref.rope(q, positions, cos, sin, D, True)
+        ref.rope(k, positions, cos, sin, D, True)
+        ref.kv_write(k, v, k_cache, v_cache, slots)
+        return qkv
+    _K().rope_qkv_cache(qkv, _i32(positions), cos, sin, k_cache, v_cache, _i32(slots), int(heads), int(kv_heads))
+    return qkv
 
 
 def rope_pairs(x, cos, sin):

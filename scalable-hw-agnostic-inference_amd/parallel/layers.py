@@ -61,8 +61,8 @@ class ColumnParallelLinear(_ShardLoadMixin, nn.Module):
     def _shard(self, name, full):
         return full.narrow(0, self.tp_rank * self.out_local, self.out_local).contiguous()
 
-    def forward(self, x, act=None):
-        y = ops.linear(x, self.weight, self.bias, act=act)
+    def forward(self, x, act=None, rms_eps=None):
+        y = ops.linear(x, self.weight, self.bias, act=act, rms_eps=rms_eps)
         return comm.all_gather_last(y) if self.gather_output else y
 
 
@@ -122,8 +122,8 @@ class QKVParallelLinear(_ShardLoadMixin, nn.Module):
         vs = v.narrow(0, kv_idx * self.kv_local * hd, self.kv_local * hd)
         return torch.cat([qs, ks, vs], 0).contiguous()
 
-    def forward(self, x):
-        return ops.linear(x, self.weight, self.bias)
+    def forward(self, x, rms_eps=None):
+        return ops.linear(x, self.weight, self.bias, rms_eps=rms_eps)
 
 
 class GLUParallelLinear(_ShardLoadMixin, nn.Module):
@@ -142,8 +142,8 @@ class GLUParallelLinear(_ShardLoadMixin, nn.Module):
     def _shard(self, name, full):
         return full.narrow(0, self.tp_rank * 2 * self.i_local, 2 * self.i_local).contiguous()
 
-    def forward(self, x):
-        return ops.linear(x, self.weight, self.bias, act=self.act, glu=True)
+    def forward(self, x, rms_eps=None):
+        return ops.linear(x, self.weight, self.bias, act=self.act, glu=True, rms_eps=rms_eps)
 
 
 class VocabParallelEmbedding(_ShardLoadMixin, nn.Module):
@@ -173,8 +173,8 @@ class VocabParallelEmbedding(_ShardLoadMixin, nn.Module):
 
 
 class ParallelLMHead(VocabParallelEmbedding):
-    def logits(self, x):
-        y = ops.linear(x, self.weight)
+    def logits(self, x, rms_eps=None):
+        y = ops.linear(x, self.weight, rms_eps=rms_eps)
         if self.tp_size > 1:
             y = comm.all_gather_last(y)
         return y[..., : self.vocab]

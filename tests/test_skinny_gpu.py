@@ -9,7 +9,8 @@ SKINNY = 1000
 
 
 def _rel(a, b):
-    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-6)).item()
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-6)).item()
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (7, 6144, 4096), (32, 4096, 14336), (32, 28672, 4096),
@@ -70,3 +71,44 @@ def test_autotuned_decode_shapes(cuda):
         w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
         y = ops.linear(x, w)
         assert _rel(y, x.float() @ w.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(32, 6144, 4096), (5, 4096, 4096), (32, 28672, 4096), (64, 512, 1024)])
+def test_folded_rmsnorm_linear(cuda, M, N, K):
+    """linear(x, W * diag(g), rms_eps) == rmsnorm(x, g) @ W^T (fused in the skinny kernel for M <= 32,
+    explicit unweighted norm + GEMM otherwise)."""
+    from shai_amd.ops import reference as ref
+    x = (torch.randn(M, K, device=cuda) * 3).bfloat16()
+    g = (1 + 0.2 * torch.randn(K, device=cuda)).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
+    wf = (w.float() * g.float()[None]).bfloat16()
+    glu = N == 28672
+    y = ops.linear(x, wf, act="silu" if glu else None, glu=glu, rms_eps=1e-5)
+    xn = ref.rmsnorm(x.float(), g.float(), 1e-5)[0]
+    want = xn @ w.float().t()
+    if glu:
+        want = want[:, 0::2] * torch.nn.functional.silu(want[:, 1::2])
+    assert _rel(y, want) < 2e-2
+
+
+def test_rope_qkv_cache(cuda):
+    from shai_amd.ops import reference as ref
+    T, H, Hk, D, nb = 37, 8, 2, 128, 6
+    qkv = torch.randn(T, (H + 2 * Hk) * D, device=cuda).bfloat16()
+    pos = torch.randint(0, 300, (T,), device=cuda, dtype=torch.int32)
+    ang = torch.rand(512, D // 2, device=cuda) * 3
+    cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
+    slots = torch.randperm(nb * 64, device=cuda)[:T].int()
+    slots[3] = -1
+    kc = torch.zeros(nb, Hk, 64, D, device=cuda).bfloat16()
+    vc = torch.zeros_like(kc)
+    kc2, vc2, qkv2 = kc.clone().cpu(), vc.clone().cpu(), qkv.clone().cpu()
+    ops.rope_qkv_cache(qkv, pos, cos, sin, kc, vc, slots, H, Hk)
+    q = qkv2[:, :H * D].view(T, H, D)
+    k = qkv2[:, H * D:(H + Hk) * D].view(T, Hk, D)
+    v = qkv2[:, (H + Hk) * D:].view(T, Hk, D)
+    ref.rope(q, pos.cpu(), cos.cpu(), sin.cpu(), D, True)
+    ref.rope(k, pos.cpu(), cos.cpu(), sin.cpu(), D, True)
+    ref.kv_write(k, v, kc2, vc2, slots.cpu())
+    assert _rel(qkv[:, :H * D], qkv2[:, :H * D]) < 1e-2
+    assert _rel(kc, kc2) < 1e-2 and torch.equal(vc.cpu(), vc2)

@@ -47,6 +47,39 @@ def bench_gemm(rows):
                          shai_tflops=f / t_s / 1e12, torch_tflops=f / t_t / 1e12))
 
 
+def bench_decode(rows):
+    """Decode-shaped GEMMs (Mistral-7B TP1, batch M): skinny kernel vs each tile config vs hipBLASLt,
+    reported as achieved weight bandwidth."""
+    cfgs = int(os.environ.get("SHAI_NUM_CFGS", "5"))
+    for M in (1, 8, 32):
+        for N, K in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (32768, 4096)]:
+            # rotate over enough weight copies to defeat the 256 MB Infinity Cache (decode streams
+            # 14.5 GB of weights per token, so every GEMM reads HBM)
+            ncopy = max(2, min(16, (768 << 20) // (N * K * 2) + 1))
+            a = rnd(M, K)
+            ws = [rnd(N, K) * 0.02 for _ in range(ncopy)]
+            out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            it = [0]
+
+            def nxt():
+                it[0] = (it[0] + 1) % ncopy
+                return ws[it[0]]
+            res = {}
+            for c in list(range(cfgs)) + [1000]:
+                try:
+                    res[c] = timeit(lambda: ops.gemm_into(a, nxt(), out, force_cfg=c), iters=48)
+                except Exception as e:  # noqa
+                    res[c] = float("nan")
+            t_t = timeit(lambda: torch.matmul(a, nxt().t()), iters=48)
+            t_tuned = timeit(lambda: ops.linear(a, nxt()), iters=48)
+            del ws
+            gb = N * K * 2 / 1e9
+            rows.append(dict(op="decode_gemm", shape=f"{M}x{N}x{K}", skinny_us=res[1000] * 1e6,
+                             best_tile_us=min(v for k, v in res.items() if k != 1000) * 1e6,
+                             tuned_us=t_tuned * 1e6, torch_us=t_t * 1e6,
+                             skinny_TBps=gb / res[1000] / 1e3, torch_TBps=gb / t_t / 1e3))
+
+
 def bench_conv(rows):
     shapes = [(8, 64, 320, 320, 3), (8, 32, 640, 640, 3), (8, 16, 1280, 1280, 3), (8, 8, 1280, 1280, 3),
               (8, 64, 640, 320, 3), (1, 256, 256, 128, 3), (1, 512, 128, 128, 3), (8, 64, 320, 320, 1)]
@@ -103,7 +136,8 @@ def main():
     rows = []
     with torch.inference_mode():
         for name in a.only.split(","):
-            {"gemm": bench_gemm, "conv": bench_conv, "attn": bench_attn, "norm": bench_norm}[name](rows)
+            {"gemm": bench_gemm, "conv": bench_conv, "attn": bench_attn, "norm": bench_norm,
+             "decode": bench_decode}[name](rows)
     for r in rows:
         print("  ".join(f"{k}={v:.1f}" if isinstance(v, float) else f"{k}={v}" for k, v in r.items()), flush=True)
     if a.json:

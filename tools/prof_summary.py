@@ -1,20 +1,44 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 --kernel-trace --stats CSV directory into a markdown table."""
+"""Summarise a rocprofv3 --kernel-trace --stats output directory into a markdown table.
+
+Accepts the CSV layout (``--output-format csv``: run_kernel_stats.csv) or the
+default rocpd SQLite database (``*_results.db``)."""
 import csv
+import glob
+import os
+import sqlite3
 import sys
 
 
+def _rows(d):
+    """-> list of (name, calls, total_ns, avg_ns)."""
+    p = os.path.join(d, "run_kernel_stats.csv")
+    if os.path.exists(p):
+        return [(r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]), float(r["AverageNs"]))
+                for r in csv.DictReader(open(p))]
+    dbs = glob.glob(os.path.join(d, "**", "*.db"), recursive=True)
+    if not dbs:
+        raise SystemExit(f"no run_kernel_stats.csv or *.db under {d}")
+    out = {}
+    for db in dbs:
+        c = sqlite3.connect(db)
+        for name, n, tot in c.execute("select name, count(*), sum(duration) from kernels group by name"):
+            a = out.setdefault(name, [0, 0.0])
+            a[0] += n
+            a[1] += float(tot)
+    return [(k, v[0], v[1], v[1] / max(1, v[0])) for k, v in out.items()]
+
+
 def main(d, top=30, title=None):
-    rows = list(csv.DictReader(open(f"{d}/run_kernel_stats.csv")))
-    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    rows = _rows(d)
+    tot = sum(r[2] for r in rows)
     out = [f"### {title or d}", "", f"Total kernel time: {tot / 1e6:.2f} ms", "",
            "| ms | calls | % | avg us | kernel |", "|---:|---:|---:|---:|---|"]
-    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:top]:
-        name = r["Name"].replace("|", "/")
+    for name, calls, t, avg in sorted(rows, key=lambda r: -r[2])[:top]:
+        name = name.replace("|", "/")
         if len(name) > 100:
             name = name[:100] + "..."
-        out.append(f"| {float(r['TotalDurationNs']) / 1e6:.2f} | {r['Calls']} | {float(r['Percentage']):.1f} | "
-                   f"{float(r['AverageNs']) / 1e3:.1f} | `{name}` |")
+        out.append(f"| {t / 1e6:.2f} | {calls} | {100 * t / tot:.1f} | {avg / 1e3:.1f} | `{name}` |")
     return "\n".join(out)
 
 
