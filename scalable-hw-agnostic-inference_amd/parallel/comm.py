@@ -52,8 +52,9 @@ def all_gather_last(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) 
         return x
     n = st.size if group is None else dist.get_world_size(g)
     x = x.contiguous()
-    out = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, x, group=g)
+    flat = torch.empty((n * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(flat, x, group=g)   # rank-major concat along dim 0
+    out = flat.view((n,) + tuple(x.shape))
     return out.movedim(0, -2).reshape(*x.shape[:-1], n * x.shape[-1])
 
 
