@@ -32,8 +32,9 @@ bool use_v2(const shai::GemmArgs& g, long a_bytes, long w_bytes, long a2_bytes) 
   if (force_v1 || g.in_scale != nullptr) return false;
   const long lim = 0x7fffffffL - 64;
   if (a_bytes > lim || w_bytes > lim || a2_bytes > lim) return false;
-  if (g.conv && g.A2 != nullptr && (g.Cin % 64 != 0 || g.Cin1 % 64 != 0)) return false;
-  return true;
+  for (int c = 0; c < shai::gemm2_num_cfgs(); ++c)
+    if (shai::gemm2_cfg_supported(g, c)) return true;
+  return false;
 }
 
 // ---- GEMM autotuner: the first eager call of a problem shape times every
@@ -118,8 +119,10 @@ Choice tune(const shai::GemmArgs& g_real, const Tensor& like) {
   shai::gemm2_plan(g, &def.cfg, &def.splits);
   const int ms = max_splits_for(g);
   std::vector<Choice> cands;
-  for (int c = 0; c < shai::gemm2_num_cfgs(); ++c)
+  for (int c = 0; c < shai::gemm2_num_cfgs(); ++c) {
+    if (!shai::gemm2_cfg_supported(g, c)) continue;
     for (int s = 1; s <= ms; s *= 2) cands.push_back({c, s});
+  }
   if (shai::skinny_supported(g)) cands.push_back({kSkinnyCfg, 1});
   hipStream_t st = stream();
   hipEvent_t e0, e1;
@@ -146,9 +149,17 @@ Choice tune(const shai::GemmArgs& g_real, const Tensor& like) {
 }
 
 void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_bytes, long a2_bytes) {
+  static const int forced = [] {  // tests / tools: pin one config for every supported GEMM/conv
+    const char* e = getenv("SHAI_GEMM_FORCE");
+    return e ? atoi(e) : -1;
+  }();
   if (!use_v2(g, a_bytes, w_bytes, a2_bytes)) {
     SHAI_CHECK(g.gate == nullptr, "gated GEMM epilogue needs the v2 kernel (operands < 2 GiB, SHAI_GEMM_V1 unset)");
     shai::launch_gemm(g, stream());
+    return;
+  }
+  if (forced >= 0 && forced < shai::gemm2_num_cfgs() && shai::gemm2_cfg_supported(g, forced)) {
+    launch_choice(g, like, Choice{forced, 1});
     return;
   }
   const std::string key = gemm_key(g);
@@ -166,8 +177,12 @@ void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_
       std::lock_guard<std::mutex> lk(g_tune_mu);
       g_tuned[key] = c;
     } else {
-      if (shai::skinny_supported(g)) c = Choice{kSkinnyCfg, 1};
-      else shai::gemm2_plan(g, &c.cfg, &c.splits);
+      if (shai::skinny_supported(g)) {
+        c = Choice{kSkinnyCfg, 1};
+      } else {
+        shai::gemm2_plan(g, &c.cfg, &c.splits);
+        if (!shai::gemm2_cfg_supported(g, c.cfg)) c = Choice{shai::gemm2_num_cfgs() - 1, 1};
+      }
     }
   }
   launch_choice(g, like, c);
@@ -451,7 +466,7 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
     if (force_cfg == kSkinnyCfg) {
       SHAI_CHECK(shai::skinny_supported(g), "skinny kernel does not support this problem");
     } else {
-      SHAI_CHECK(force_cfg < shai::gemm2_num_cfgs(), "bad force_cfg");
+      SHAI_CHECK(force_cfg < shai::gemm2_num_cfgs() && shai::gemm2_cfg_supported(g, force_cfg), "bad force_cfg");
     }
     launch_choice(g, a, Choice{(int)force_cfg, 1});
     return;
@@ -476,11 +491,17 @@ void conv2d(const Tensor& x, const optional<Tensor>& x2, const Tensor& w, const 
   g.Wd = x.size(2);
   g.Cin1 = x.size(3);
   g.Cin = g.Cin1;
+  Tensor xcat;  // concat fallback: the fused two-source gather needs the split at a multiple of 32 channels
   if (x2) {
     check_bf16(*x2, "x2");
     SHAI_CHECK(x2->is_contiguous() && x2->size(0) == g.Nimg && x2->size(1) == g.H && x2->size(2) == g.Wd, "x2 shape");
-    g.A2 = cptr(*x2);
-    g.Cin += x2->size(3);
+    if (g.Cin1 % 32 != 0 || x2->size(3) % 32 != 0) {
+      xcat = at::cat({x, *x2}, 3);
+      g.Cin1 = g.Cin = xcat.size(3);
+    } else {
+      g.A2 = cptr(*x2);
+      g.Cin += x2->size(3);
+    }
   }
   SHAI_CHECK(g.Cin % 8 == 0 && g.Cin1 % 8 == 0, "conv2d: input channels must be multiples of 8");
   g.KH = kh;
@@ -498,7 +519,7 @@ void conv2d(const Tensor& x, const optional<Tensor>& x2, const Tensor& w, const 
   g.K = kh * kw * g.Cin;
   SHAI_CHECK(w.size(0) == g.N && w.numel() == (long)g.N * g.K, "conv2d weight must be [Cout, KH*KW*Cin]");
   g.M = g.Nimg * g.OH * g.OW;
-  g.A = cptr(x);
+  g.A = xcat.defined() ? cptr(xcat) : cptr(x);
   g.W = cptr(w);
   g.C = mptr(out);
   g.lda = g.K;
@@ -533,7 +554,8 @@ void conv2d(const Tensor& x, const optional<Tensor>& x2, const Tensor& w, const 
     g.in_shift = in_shift->data_ptr<float>();
     g.in_act = in_act;
   }
-  run_gemm(g, x, x.numel() * 2, w.numel() * 2, x2 ? x2->numel() * 2 : 0);
+  run_gemm(g, x, xcat.defined() ? xcat.numel() * 2 : x.numel() * 2, w.numel() * 2,
+           (x2 && !xcat.defined()) ? x2->numel() * 2 : 0);
 }
 
 // ---------------------------------------------------------------- attention

@@ -20,6 +20,7 @@
 // XCD-aware bijective block remap + grouped ordering along M.
 #include "common.h"
 #include "launchers.h"
+#include "gemm_epilogue.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -40,78 +41,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
 
 __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, bf16_t* lds_wave_base, uint32_t voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_wave_base, 16, voff, 0, 0, 0);
-}
-
-// Apply the epilogue to 4 consecutive columns n..n+3 of row m and store.
-template <bool GLU, int ACT>
-__device__ __forceinline__ void epilogue4(const GemmArgs& p, bf16_t* C, const bf16_t* R, int m, int n, float v[4],
-                                          int b = 0) {
-  const bool full = n + 3 < p.N && (p.ldc & 3) == 0 && (p.ldr & 3) == 0;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) v[e] *= p.alpha;
-  if (p.bias) {
-    if (full) {
-      const uint2_ bb = *reinterpret_cast<const uint2_*>(p.bias + n);
-      v[0] += bf2f(bb[0] & 0xffff); v[1] += bf2f(bb[0] >> 16);
-      v[2] += bf2f(bb[1] & 0xffff); v[3] += bf2f(bb[1] >> 16);
-    } else {
-      for (int e = 0; e < 4 && n + e < p.N; ++e) v[e] += bf2f(p.bias[n + e]);
-    }
-  }
-  if (p.bias2d) {
-    const bf16_t* b2 = p.bias2d + (long)(m / p.rows_per_bias2d) * p.N;
-    if (full && (p.N & 3) == 0) {
-      const uint2_ bb = *reinterpret_cast<const uint2_*>(b2 + n);
-      v[0] += bf2f(bb[0] & 0xffff); v[1] += bf2f(bb[0] >> 16);
-      v[2] += bf2f(bb[1] & 0xffff); v[3] += bf2f(bb[1] >> 16);
-    } else {
-      for (int e = 0; e < 4 && n + e < p.N; ++e) v[e] += bf2f(b2[n + e]);
-    }
-  }
-  const bf16_t* gr = p.gate ? p.gate + ((long)b * p.M + m) / p.rows_per_gate * p.gate_stride : nullptr;
-  if constexpr (GLU) {
-    float o0 = v[0] * apply_act<ACT>(v[1]);
-    float o1 = v[2] * apply_act<ACT>(v[3]);
-    const int nc = n >> 1;
-    if (gr) {
-      o0 *= bf2f(gr[nc]);
-      o1 *= bf2f(gr[nc + 1]);
-    }
-    float r0 = 0.f, r1 = 0.f;
-    if (R) {
-      r0 = bf2f(R[(long)m * p.ldr + nc]) * p.res_alpha;
-      r1 = bf2f(R[(long)m * p.ldr + nc + 1]) * p.res_alpha;
-    }
-    if (((p.ldc | nc) & 1) == 0) {
-      *reinterpret_cast<uint32_t*>(C + (long)m * p.ldc + nc) = pack2(o0 + r0, o1 + r1);
-    } else {
-      C[(long)m * p.ldc + nc] = f2bf(o0 + r0);
-      C[(long)m * p.ldc + nc + 1] = f2bf(o1 + r1);
-    }
-  } else {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = apply_act<ACT>(v[e]);
-    if (gr) {
-      for (int e = 0; e < 4 && n + e < p.N; ++e) v[e] *= bf2f(gr[n + e]);
-    }
-    if (full) {
-      if (R) {
-        const uint2_ rr = *reinterpret_cast<const uint2_*>(R + (long)m * p.ldr + n);
-        v[0] += bf2f(rr[0] & 0xffff) * p.res_alpha; v[1] += bf2f(rr[0] >> 16) * p.res_alpha;
-        v[2] += bf2f(rr[1] & 0xffff) * p.res_alpha; v[3] += bf2f(rr[1] >> 16) * p.res_alpha;
-      }
-      uint2_ o;
-      o[0] = pack2(v[0], v[1]);
-      o[1] = pack2(v[2], v[3]);
-      *reinterpret_cast<uint2_*>(C + (long)m * p.ldc + n) = o;
-    } else {
-      for (int e = 0; e < 4 && n + e < p.N; ++e) {
-        float x = v[e];
-        if (R) x += bf2f(R[(long)m * p.ldr + n + e]) * p.res_alpha;
-        C[(long)m * p.ldc + n + e] = f2bf(x);
-      }
-    }
-  }
 }
 
 template <int BM, int BN, int WM, int WN, bool CONV, bool FAST, bool GLU, int ACT, bool SPLITK, int STAGES>
@@ -523,6 +452,10 @@ static void launch_all(const GemmArgs& a, float* ws, int cfg, int splits, hipStr
 }
 
 void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStream_t s) {
+  if (cfg >= kNumCfgs) {  // pipelined 256x256 kernel (gemm_pipe.hip): 4-stage / 2-stage ring
+    launch_gemm3(a, ws, splits, cfg == kNumCfgs ? 4 : 2, s);
+    return;
+  }
   if (!a.conv) {
     launch_all<false, false>(a, ws, cfg, splits, s);
   } else {
@@ -550,9 +483,21 @@ void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipS
   }
 }
 
-int gemm2_num_cfgs() { return kNumCfgs; }
+int gemm2_num_cfgs() { return kNumCfgs + 2; }
+
+bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
+  if (cfg >= kNumCfgs) return cfg < kNumCfgs + 2 && gemm3_supported(a);
+  if (a.in_scale != nullptr) return false;
+  if (a.conv && a.A2 != nullptr && (a.Cin % 64 != 0 || a.Cin1 % 64 != 0)) return false;  // 64-wide K tiles
+  return cfg >= 0 && cfg < kNumCfgs;
+}
 
 void gemm2_cfg_info(int cfg, int* bm, int* bn) {
+  if (cfg >= kNumCfgs) {
+    *bm = cfg == kNumCfgs ? 4 : 2;  // pipelined v3 kernel: stages
+    *bn = -256;
+    return;
+  }
   *bm = kCfgs[cfg].bm;
   *bn = kCfgs[cfg].bn;
 }

@@ -1,0 +1,85 @@
+"""Pipelined 256x256 GEMM / conv kernel (config 5, gemm_pipe.hip) vs fp32 PyTorch."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from shai_amd import ops
+
+pytestmark = pytest.mark.gpu
+CFG = 5
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-6)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 4096), (300, 520, 200), (1000, 256, 96), (257, 1024, 2048),
+                                   (65536, 320, 320)])
+def test_gemm3_plain_bias_residual(cuda, M, N, K):
+    torch.manual_seed(M)
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device=cuda).bfloat16()
+    r = torch.randn(M, N, device=cuda).bfloat16()
+    out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    ops.gemm_into(a, w, out, bias, residual=r, force_cfg=CFG)
+    assert _rel(out, a.float() @ w.float().t() + bias.float() + r.float()) < 1e-2
+
+
+@pytest.mark.parametrize("act", ["gelu", "silu"])
+def test_gemm3_glu(cuda, act):
+    M, N, K = 2048, 2560, 320
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
+    out = torch.empty(M, N // 2, device=cuda, dtype=torch.bfloat16)
+    ops.gemm_into(a, w, out, act=act, glu=True, force_cfg=CFG)
+    y = a.float() @ w.float().t()
+    f = torch.nn.functional.gelu if act == "gelu" else torch.nn.functional.silu
+    assert _rel(out, y[:, 0::2] * f(y[:, 1::2])) < 1e-2
+
+
+def test_gemm3_batched_strided(cuda):
+    B, M, N, K = 3, 300, 384, 256
+    a = torch.randn(B, M, K, device=cuda).bfloat16()
+    w = torch.randn(N, K, device=cuda).bfloat16()
+    j = torch.zeros(B, M + 40, N, device=cuda).bfloat16()
+    ops.gemm_into(a, w, j[:, 40:], force_cfg=CFG)
+    assert _rel(j[:, 40:], a.float() @ w.float().t()) < 1e-2 and j[:, :40].abs().sum().item() == 0
+
+
+CONV_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+import shai_amd.ops as ops
+from shai_amd.ops import reference as ref
+torch.manual_seed(0)
+cases = [(2, 32, 32, 64, 128, 3, 1, 1, False, 0), (2, 16, 16, 320, 320, 3, 1, 1, False, 0),
+         (1, 16, 16, 64, 96, 3, 2, 1, False, 0), (2, 8, 8, 128, 64, 3, 1, 1, True, 0),
+         (2, 16, 16, 96, 64, 3, 1, 1, False, 64), (2, 16, 16, 64, 64, 1, 1, 0, False, 0)]
+worst = 0.0
+for N, H, C, Co, k, stride, pad, up, c2 in [(c[0], c[1], c[3], c[4], c[5], c[6], c[7], c[8], c[9]) for c in cases]:
+    x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+    x2 = torch.randn(N, H, H, c2, device="cuda").bfloat16() if c2 else None
+    cin = C + c2
+    w = (torch.randn(Co, cin, k, k, device="cuda") / (cin * k * k) ** 0.5).bfloat16()
+    wp = ops.pack_conv_weight(w)
+    b = torch.randn(Co, device="cuda").bfloat16()
+    y = ops.conv2d(x, wp, b, k, k, stride, pad, upsample=up, x2=x2, act="silu")
+    yr = ref.conv2d(x.cpu(), wp.cpu(), b.cpu(), k, k, stride, pad, upsample=up, x2=x2.cpu() if x2 is not None else None, act="silu")
+    rel = ((y.float().cpu() - yr.float()).norm() / yr.float().norm()).item()
+    worst = max(worst, rel)
+print("WORST", worst)
+assert worst < 2e-2, worst
+"""
+
+
+def test_gemm3_conv_forced(cuda):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SHAI_GEMM_FORCE=str(CFG))
+    r = subprocess.run([sys.executable, "-c", CONV_SCRIPT.format(root=root)], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]

@@ -80,6 +80,27 @@ def bench_decode(rows):
                              skinny_TBps=gb / res[1000] / 1e3, torch_TBps=gb / t_t / 1e3))
 
 
+def bench_sdgemm(rows):
+    """SD2.1 batch-8 (CFG 16) transformer GEMMs: every tile config (forced) vs the tuned choice vs hipBLASLt."""
+    shapes = [("sq4096", 4096, 4096, 4096, False), ("sq8192", 8192, 8192, 8192, False),
+              ("geglu_L1", 65536, 2560, 320, True), ("ffdown_L1", 65536, 320, 1280, False),
+              ("qkv_L1", 65536, 960, 320, False), ("proj_L1", 65536, 320, 320, False),
+              ("geglu_L2", 16384, 5120, 640, True), ("ffdown_L2", 16384, 640, 2560, False),
+              ("geglu_L3", 4096, 10240, 1280, True), ("ffdown_L3", 4096, 1280, 5120, False)]
+    for name, M, N, K, glu in shapes:
+        a, w = rnd(M, K), rnd(N, K) * (1 / math.sqrt(K))
+        out = torch.empty(M, N // 2 if glu else N, device="cuda", dtype=torch.bfloat16)
+        res = {}
+        for c in range(7):
+            res[c] = timeit(lambda: ops.gemm_into(a, w, out, act="gelu" if glu else None, glu=glu, force_cfg=c))
+        t_tuned = timeit(lambda: ops.linear(a, w, act="gelu" if glu else None, glu=glu))
+        t_t = timeit(lambda: torch.matmul(a, w.t()))
+        f = 2 * M * N * K
+        rows.append(dict(op=name, shape=f"{M}x{N}x{K}", **{f"cfg{c}_us": v * 1e6 for c, v in res.items()},
+                         tuned_us=t_tuned * 1e6, torch_us=t_t * 1e6, tuned_tflops=f / t_tuned / 1e12,
+                         torch_tflops=f / t_t / 1e12))
+
+
 def bench_conv(rows):
     shapes = [(8, 64, 320, 320, 3), (8, 32, 640, 640, 3), (8, 16, 1280, 1280, 3), (8, 8, 1280, 1280, 3),
               (8, 64, 640, 320, 3), (1, 256, 256, 128, 3), (1, 512, 128, 128, 3), (8, 64, 320, 320, 1)]
@@ -137,7 +158,7 @@ def main():
     with torch.inference_mode():
         for name in a.only.split(","):
             {"gemm": bench_gemm, "conv": bench_conv, "attn": bench_attn, "norm": bench_norm,
-             "decode": bench_decode}[name](rows)
+             "decode": bench_decode, "sdgemm": bench_sdgemm}[name](rows)
     for r in rows:
         print("  ".join(f"{k}={v:.1f}" if isinstance(v, float) else f"{k}={v}" for k, v in r.items()), flush=True)
     if a.json:
