@@ -728,6 +728,25 @@ void rope_qkv_cache(const Tensor& qkv, const Tensor& positions, const Tensor& co
                               D, stream());
 }
 
+void sample(const Tensor& logits, const Tensor& temps, const Tensor& top_k, const Tensor& top_p,
+            const Tensor& uniforms, const Tensor& out) {
+  SHAI_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits must be a 2D GPU tensor");
+  const bool bf16 = logits.scalar_type() == at::kBFloat16;
+  SHAI_CHECK(bf16 || logits.scalar_type() == at::kFloat, "logits must be bf16 or fp32");
+  const int B = logits.size(0);
+  check_f32(temps, "temps");
+  check_f32(top_p, "top_p");
+  check_f32(uniforms, "uniforms");
+  check_i32(top_k, "top_k");
+  check_i32(out, "out");
+  SHAI_CHECK(temps.numel() == B && top_p.numel() == B && uniforms.numel() == B && top_k.numel() == B &&
+                 out.numel() == B,
+             "per-row parameter sizes");
+  shai::launch_sample(logits.data_ptr(), bf16, logits.stride(0), B, logits.size(1), temps.data_ptr<float>(),
+                      top_k.data_ptr<int>(), top_p.data_ptr<float>(), uniforms.data_ptr<float>(),
+                      out.data_ptr<int>(), stream());
+}
+
 void rope_pairs(const Tensor& x, const Tensor& cos, const Tensor& sin) {
   check_bf16(x, "x");
   check_f32(cos, "cos");
@@ -807,6 +826,7 @@ TORCH_LIBRARY(shai, m) {
   m.def("bias_act(Tensor x, Tensor? bias, Tensor? residual, Tensor(a!) out, int act, float alpha) -> ()");
   m.def("rope(Tensor(a!) x, Tensor positions, Tensor cos, Tensor sin, int rot_dim, bool neox) -> ()");
   m.def("rope_pairs(Tensor(a!) x, Tensor cos, Tensor sin) -> ()");
+  m.def("sample(Tensor logits, Tensor temps, Tensor top_k, Tensor top_p, Tensor uniforms, Tensor(a!) out) -> ()");
   m.def("rope_qkv_cache(Tensor(a!) qkv, Tensor positions, Tensor cos, Tensor sin, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor slots, int H, int Hkv) -> ()");
   m.def("sched_step(Tensor model_out, Tensor(a!) latents, bool cfg, float guidance, int pred_type, float a_t, float a_prev, float dt) -> ()");
   m.def("softmax_(Tensor(a!) x, float scale) -> ()");
@@ -832,6 +852,7 @@ TORCH_LIBRARY_IMPL(shai, CUDA, m) {
   m.impl("bias_act", &bias_act);
   m.impl("rope", &rope);
   m.impl("rope_pairs", &rope_pairs);
+  m.impl("sample", &sample);
   m.impl("rope_qkv_cache", &rope_qkv_cache);
   m.impl("sched_step", &sched_step);
   m.impl("softmax_", &softmax_);

@@ -1,0 +1,188 @@
+// One-shot all-reduce over xGMI peer memory for small, latency-bound tensor-parallel
+// messages (LLM decode: [B, 4096] bf16 after o_proj / down_proj, a few KB to ~1 MB).
+//
+// RCCL's ring/tree all-reduce pays several link latencies per call; on a fully
+// connected 8x MI355X node every GPU can instead READ every peer's buffer
+// directly over its own xGMI link.  Each rank exposes one uncached device buffer
+// through a HIP IPC handle (exchanged once over torch.distributed); per call:
+//   1. every workgroup copies its slice of the local input into the local buffer,
+//   2. cross-GPU start barrier per workgroup (system-scope flag stores into each
+//      peer's signal area, spin on the local one -- epochs count calls, so the
+//      flags never need resetting and the kernel is HIP-graph replay safe),
+//   3. it sums the same slice from all `world` buffers (fp32 accumulate) into the
+//      output, 4. an end barrier so nobody overwrites a slice a peer still reads.
+// The buffer is allocated uncached (hipDeviceMallocUncached), so peer data and
+// flags are never served stale from an L2.  Spins are bounded: a missing peer
+// ends the call with a flagged error instead of hanging the GPU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+namespace {
+
+constexpr int kMaxRanks = 8;
+constexpr int kMaxBlocks = 256;
+constexpr long kSpinLimit = 1L << 27;
+
+struct Layout {  // signal area at the start of each rank's buffer
+  // flags[phase][block][src_rank] = epoch written by src_rank
+  uint32_t flags[2][kMaxBlocks][kMaxRanks];
+  uint32_t epoch[kMaxBlocks];  // local per-block call counter
+  uint32_t error;
+  uint32_t pad[63];
+};
+constexpr size_t kDataOff = (sizeof(Layout) + 4095) & ~size_t(4095);
+
+struct Peers {
+  char* base[kMaxRanks];
+};
+
+__device__ __forceinline__ void barrier_phase(const Peers& P, Layout* me, int phase, int rank, int world,
+                                              uint32_t epoch) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (t < world) {
+    Layout* peer = reinterpret_cast<Layout*>(P.base[t]);
+    __hip_atomic_store(&peer->flags[phase][b][rank], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    long spins = 0;
+    while (__hip_atomic_load(&me->flags[phase][b][t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+      if (++spins > kSpinLimit) {
+        __hip_atomic_store(&me->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(512) p2p_one_shot(Peers P, int rank, int world, const uint4* in,
+                                                    uint4* out, long n16) {
+  __shared__ uint32_t s_epoch;
+  Layout* me = reinterpret_cast<Layout*>(P.base[rank]);
+  if (threadIdx.x == 0) {
+    const uint32_t e = me->epoch[blockIdx.x] + 1;
+    me->epoch[blockIdx.x] = e;
+    s_epoch = e;
+  }
+  __syncthreads();
+  const uint32_t epoch = s_epoch;
+  uint4* mine = reinterpret_cast<uint4*>(P.base[rank] + kDataOff);
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) mine[i] = in[i];
+  __threadfence_system();
+  __syncthreads();
+  barrier_phase(P, me, 0, rank, world, epoch);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < world; ++r) {
+      const uint4 v = reinterpret_cast<const uint4*>(P.base[r] + kDataOff)[i];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[2 * e] += __uint_as_float(w[e] << 16);
+        acc[2 * e + 1] += __uint_as_float(w[e] & 0xffff0000u);
+      }
+    }
+    uint32_t o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      // round-to-nearest-even to bf16
+      uint32_t lo = __float_as_uint(acc[2 * e]), hi = __float_as_uint(acc[2 * e + 1]);
+      lo = (lo + 0x7fffu + ((lo >> 16) & 1u)) >> 16;
+      hi = (hi + 0x7fffu + ((hi >> 16) & 1u)) >> 16;
+      o[e] = lo | (hi << 16);
+    }
+    out[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  __syncthreads();
+  barrier_phase(P, me, 1, rank, world, epoch);
+}
+
+struct Ctx {
+  int rank, world, device;
+  size_t max_bytes;
+  char* local;
+  Peers peers;
+  bool opened[kMaxRanks];
+};
+
+}  // namespace
+
+extern "C" {
+
+// Returns nullptr on failure.  handle_out receives the 64-byte hipIpcMemHandle_t.
+void* shai_p2p_create(int rank, int world, size_t max_bytes, char* handle_out) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world) return nullptr;
+  Ctx* c = new Ctx();
+  c->rank = rank;
+  c->world = world;
+  c->max_bytes = max_bytes;
+  hipGetDevice(&c->device);
+  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->local), kDataOff + max_bytes, hipDeviceMallocUncached) !=
+      hipSuccess) {
+    delete c;
+    return nullptr;
+  }
+  (void)hipMemset(c->local, 0, kDataOff);
+  (void)hipDeviceSynchronize();
+  hipIpcMemHandle_t h;
+  if (hipIpcGetMemHandle(&h, c->local) != hipSuccess) {
+    (void)hipFree(c->local);
+    delete c;
+    return nullptr;
+  }
+  memcpy(handle_out, &h, sizeof(h));
+  memset(&c->peers, 0, sizeof(c->peers));
+  c->peers.base[rank] = c->local;
+  return c;
+}
+
+int shai_p2p_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+// handles: world consecutive 64-byte handles (own entry ignored).  0 on success.
+int shai_p2p_open(void* ctx, const char* handles) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  for (int r = 0; r < c->world; ++r) {
+    if (r == c->rank) continue;
+    hipIpcMemHandle_t h;
+    memcpy(&h, handles + (size_t)r * sizeof(h), sizeof(h));
+    void* p = nullptr;
+    if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -1 - r;
+    c->peers.base[r] = static_cast<char*>(p);
+    c->opened[r] = true;
+  }
+  return 0;
+}
+
+// bf16 sum of `bytes` (multiple of 16, <= max_bytes) from in into out (may alias) on stream.
+int shai_p2p_allreduce_bf16(void* ctx, const void* in, void* out, size_t bytes, hipStream_t stream) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (bytes % 16 != 0 || bytes > c->max_bytes) return -1;
+  const long n16 = (long)(bytes / 16);
+  int blocks = (int)((n16 + 511) / 512);
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  if (blocks < 1) blocks = 1;
+  // every rank must use the same grid: it is a function of bytes only
+  hipLaunchKernelGGL(p2p_one_shot, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world,
+                     static_cast<const uint4*>(in), static_cast<uint4*>(out), n16);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// 1 if any spin timed out since creation (a peer did not arrive).
+int shai_p2p_error(void* ctx) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  uint32_t e = 0;
+  (void)hipMemcpy(&e, c->local + offsetof(Layout, error), 4, hipMemcpyDeviceToHost);
+  return (int)e;
+}
+
+void shai_p2p_destroy(void* ctx) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return;
+  for (int r = 0; r < c->world; ++r)
+    if (c->opened[r]) (void)hipIpcCloseMemHandle(c->peers.base[r]);
+  (void)hipFree(c->local);
+  delete c;
+}
+
+}  // extern "C"

@@ -170,7 +170,7 @@ void launch_kv_write(const bf16_t* k, const bf16_t* v, bf16_t* k_cache, bf16_t* 
                      int T, int Hkv, int D, long k_ts, long v_ts, hipStream_t s);
 
 // ---------------------------------------------------------------- sampling
-// Per-row temperature / top-k / top-p sampling from fp32 or bf16 logits.
-void launch_sample(const float* logits, int rows, int V, const float* temperature, const int* top_k,
-                   const float* top_p, const float* uniform, int* out, float* ws, hipStream_t s);
+// Per-row temperature / top-k (<= 1024 candidates) / top-p sampling from bf16 or fp32 logits [B, ld].
+void launch_sample(const void* logits, bool bf16, long ld, int B, int V, const float* temps, const int* top_k,
+                   const float* top_p, const float* uniforms, int* out, hipStream_t s);
 }  // namespace shai

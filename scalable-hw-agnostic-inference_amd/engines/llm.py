@@ -80,6 +80,16 @@ def sample(logits: torch.Tensor, temps: torch.Tensor, top_k: torch.Tensor, top_p
            gen: Optional[torch.Generator] = None, all_greedy: Optional[bool] = None) -> torch.Tensor:
     """Temperature / top-k / top-p sampling; rows with temperature 0 are greedy (an all-greedy batch
     skips the sort / multinomial path entirely)."""
+    if all_greedy:
+        return logits.float().argmax(-1)
+    if logits.is_cuda and logits.dim() == 2 and os.environ.get("SHAI_TORCH_SAMPLER", "0") != "1":
+        # (top_k <= 0 / > 1024 rows keep their 1024 most likely tokens before the top-p cut)
+        # fused on-device sampler (csrc/kernels/sampling.hip); uniforms from the engine's generator
+        u = torch.rand(logits.shape[0], device=logits.device, generator=gen)
+        out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)
+        ops.sample(logits.contiguous(), temps.float().contiguous(), top_k.int().contiguous(),
+                   top_p.float().contiguous(), u, out)
+        return out.long()
     lf = logits.float()
     greedy = lf.argmax(-1)
     if all_greedy is None:

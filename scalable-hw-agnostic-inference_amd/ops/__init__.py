@@ -284,6 +284,12 @@ def rope_qkv_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, heads: int
     return qkv
 
 
+def sample(logits, temps, top_k, top_p, uniforms, out):
+    """Fused temperature / top-k / top-p sampling (GPU only; one workgroup per row)."""
+    _K().sample(logits, temps, top_k, top_p, uniforms, out)
+    return out
+
+
 def rope_pairs(x, cos, sin):
     """In-place Flux RoPE on x [B, T, H, Dh] with cos/sin [T, Dh/2]."""
     if not _gpu(x):

@@ -64,3 +64,58 @@ def broadcast_object(obj, src: int = 0):
     lst = [obj]
     dist.broadcast_object_list(lst, src=src)
     return lst[0]
+
+
+class P2PAllReduce:
+    """One-shot bf16 all-reduce over IPC-mapped peer buffers (csrc/comm/p2p_allreduce.hip).
+
+    Built once per TP group (handles exchanged with ``all_gather_object``), then used by
+    :func:`all_reduce` for contiguous bf16 messages up to ``max_bytes`` once registered with
+    :func:`enable_p2p` (``SHAI_P2P_ALLREDUCE=1`` in the engine).  Everything larger, or any
+    other dtype, goes to RCCL."""
+
+    def __init__(self, group: Optional[dist.ProcessGroup] = None, max_bytes: int = P2P_MAX_BYTES):
+        import ctypes
+        from .. import native
+        self.lib = native.comm()
+        self.lib.shai_p2p_create.restype = ctypes.c_void_p
+        self.lib.shai_p2p_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_char_p]
+        self.lib.shai_p2p_open.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+        self.lib.shai_p2p_allreduce_bf16.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                      ctypes.c_size_t, ctypes.c_void_p]
+        self.lib.shai_p2p_error.argtypes = [ctypes.c_void_p]
+        self.lib.shai_p2p_destroy.argtypes = [ctypes.c_void_p]
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.max_bytes = max_bytes
+        hs = self.lib.shai_p2p_handle_size()
+        buf = ctypes.create_string_buffer(hs)
+        self.ctx = self.lib.shai_p2p_create(self.rank, self.world, max_bytes, buf)
+        if not self.ctx:
+            raise RuntimeError("P2P all-reduce buffer allocation / IPC export failed")
+        handles = [None] * self.world
+        dist.all_gather_object(handles, bytes(buf.raw), group=group)
+        rc = self.lib.shai_p2p_open(self.ctx, b"".join(handles))
+        if rc != 0:
+            raise RuntimeError(f"hipIpcOpenMemHandle failed for peer {-rc - 1}")
+        dist.barrier(group=group)
+
+    def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        nbytes = x.numel() * x.element_size()
+        if x.dtype != torch.bfloat16 or not x.is_contiguous() or nbytes % 16 or nbytes > self.max_bytes:
+            dist.all_reduce(x, group=self.group)
+            return x
+        st = torch.cuda.current_stream(x.device).cuda_stream
+        rc = self.lib.shai_p2p_allreduce_bf16(self.ctx, x.data_ptr(), x.data_ptr(), nbytes, st)
+        if rc != 0:
+            raise RuntimeError(f"p2p all-reduce launch failed ({rc})")
+        return x
+
+    def error(self) -> bool:
+        return bool(self.lib.shai_p2p_error(self.ctx))
+
+    def close(self):
+        if self.ctx:
+            self.lib.shai_p2p_destroy(self.ctx)
+            self.ctx = None

@@ -1,0 +1,49 @@
+"""Two ranks on ONE GPU (gloo for the handle exchange): the IPC-mapped one-shot all-reduce
+must equal the sum of both ranks' tensors, repeatedly and inside a HIP graph."""
+import os
+
+import torch
+
+
+def run(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    from shai_amd.parallel.comm import P2PAllReduce
+    ar = P2PAllReduce(None, max_bytes=1 << 20)
+    for n in (8, 4096 * 32, 1 << 19):
+        for it in range(3):
+            torch.manual_seed(100 * it + n)
+            full = [torch.randn(n, device="cuda").bfloat16() for _ in range(world)]
+            x = full[rank].clone()
+            ar.all_reduce(x)
+            torch.cuda.synchronize()
+            want = sum(f.float() for f in full)
+            err = ((x.float() - want).abs().max() / want.abs().max()).item()
+            assert err < 2e-2, (n, it, err)
+            dist.barrier()
+    # graph replay
+    x = torch.ones(4096, device="cuda").bfloat16() * (rank + 1)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        ar.all_reduce(x.clone())
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    dist.barrier()
+    y = x.clone()
+    with torch.cuda.graph(g):
+        ar.all_reduce(y)
+    for it in range(3):
+        y.copy_(x)
+        dist.barrier()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.allclose(y.float(), torch.full_like(y.float(), 3.0)), y[:4]
+        dist.barrier()
+    assert not ar.error()
+    dist.barrier()
+    ar.close()
+    dist.destroy_process_group()

@@ -112,3 +112,30 @@ def test_rope_qkv_cache(cuda):
     ref.kv_write(k, v, kc2, vc2, slots.cpu())
     assert _rel(qkv[:, :H * D], qkv2[:, :H * D]) < 1e-2
     assert _rel(kc, kc2) < 1e-2 and torch.equal(vc.cpu(), vc2)
+
+
+def test_fused_sampler_distribution(cuda):
+    """Fused top-k/top-p sampler: greedy rows exact; sampled tokens follow the truncated distribution."""
+    from shai_amd.engines.llm import sample
+    torch.manual_seed(0)
+    B, V = 4, 32768
+    logits = torch.randn(B, V, device=cuda) * 2
+    logits[0, 123] = 50.0
+    temps = torch.tensor([0.0, 0.7, 1.0, 0.7], device=cuda)
+    tk = torch.tensor([50, 50, 5, 0], device=cuda)
+    tp = torch.tensor([0.9, 0.9, 1.0, 0.5], device=cuda)
+    g = torch.Generator(device=cuda)
+    g.manual_seed(1)
+    counts = torch.zeros(B, V)
+    for _ in range(400):
+        t = sample(logits.bfloat16(), temps, tk, tp, g, all_greedy=False).cpu()
+        counts[torch.arange(B), t] += 1
+    assert counts[0, 123] == 400
+    lb = logits.bfloat16().float().cpu()
+    top5 = lb[2].topk(5).indices
+    assert counts[2, top5].sum() == 400                     # top-k 5 respected
+    top50 = lb[1].topk(50).indices
+    assert counts[1, top50].sum() == 400
+    # row 2: empirical vs softmax over top-5 at T=1
+    p = torch.softmax(lb[2, top5], 0)
+    assert (counts[2, top5] / 400 - p).abs().max() < 0.1
