@@ -175,6 +175,70 @@ def bench_flux(args, rank, world):
     }
 
 
+REF_MLLAMA_CAPTION_S = 5.70   # cova/README.md:98 (Llama-3.2-11B-Vision caption, trn1, vLLM TP32)
+
+
+def bench_mllama(args, rank, world):
+    """Llama-3.2-11B-Vision image captioning (the cova caption stage): one 4-tile image + instruct prompt per
+    request, ``gen_len`` sampled tokens; captions/s over ``batch`` concurrent requests + p50 bs1 latency."""
+    import numpy as np
+    import torch
+    from shai_amd.engines.llm import LLMEngine, SamplingParams
+    from shai_amd.models.mllama import MllamaConfig, preprocess_image
+    from shai_amd.parallel.state import init_distributed
+    init_distributed(tp_size=world)
+    mc = MllamaConfig.llama32_11b_vision()
+    B, G = max(1, args.batch), args.gen_len
+    eng = LLMEngine(mc, device=f"cuda:{torch.cuda.current_device()}", max_num_seqs=B, max_model_len=64 + G + 64,
+                    enable_prefix_caching=False)
+    rng = np.random.default_rng(rank)
+    img = (rng.random((1024, 1024, 3)) * 255).astype(np.uint8)            # -> 2x2 tiles of 560^2
+    pre = preprocess_image(img, mc.vision, eng.device)
+    t = mc.text
+    prompt = [t.bos_token_id, mc.image_token_index] + rng.integers(1000, 100000, 24).tolist()
+    params = SamplingParams(temperature=0.7, top_k=50, top_p=0.9, max_tokens=G, ignore_eos=True)
+    for _ in range(max(1, args.warmup)):
+        for _ in range(B):
+            eng.add_request(prompt, params, image=pre)
+        while eng.has_work():
+            eng.step()
+    lat = []
+    for _ in range(args.latency_runs):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        s = eng.add_request(prompt, params, image=pre)
+        while not s.finished:
+            eng.step()
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t0)
+    _barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        for _ in range(B):
+            eng.add_request(prompt, params, image=pre)
+        while eng.has_work():
+            eng.step()
+    torch.cuda.synchronize()
+    _barrier(world)
+    el = _max_over_ranks(time.perf_counter() - t0, world)
+    p50 = statistics.median(lat) if lat else None
+    n = B * args.steps
+    return {
+        "metric": "Llama-3.2-11B-Vision captions/sec (4-tile image, %d tokens)" % G,
+        "value": round(n / el, 4), "unit": "captions/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 2), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": round(REF_MLLAMA_CAPTION_S / p50, 3) if p50 else None,
+        "dtype": "bf16", "data": "synthetic image + prompt, random-init weights (full Llama-3.2-11B-Vision)",
+        "config": {"model": "meta-llama/Llama-3.2-11B-Vision-Instruct (architecture)", "global_batch": B,
+                   "seq_len": len(prompt) + G, "gen_len": G, "image_tiles": pre["num_tiles"],
+                   "parallelism": f"tp{world}"},
+        "p50_latency_ms_bs1": round(1000 * p50, 1) if p50 else None,
+        "tokens_per_s": round(n * G / el, 1),
+        "baseline_note": "vs_baseline = 5.70 s (reference mllama caption latency, cova/README.md:98) / our p50 "
+                         "single-request latency",
+    }
+
+
 def bench_mistral(args, rank, world):
     import torch
     from shai_amd.engines.llm import bench_decode_throughput
@@ -186,7 +250,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="sd21", choices=["sd21", "mistral", "flux"])
+    ap.add_argument("--workload", default="sd21", choices=["sd21", "mistral", "flux", "mllama"])
     ap.add_argument("--batch", type=int, default=8, help="images per GPU per step (sd21) / sequences (mistral)")
     ap.add_argument("--inference-steps", type=int, default=50)
     ap.add_argument("--height", type=int, default=512)
@@ -199,7 +263,8 @@ def main():
     import torch
     rank, world, local = _dist_init(args.gpus)
     with torch.inference_mode():
-        fn = {"sd21": bench_sd21, "mistral": bench_mistral, "flux": bench_flux}[args.workload]
+        fn = {"sd21": bench_sd21, "mistral": bench_mistral, "flux": bench_flux,
+              "mllama": bench_mllama}[args.workload]
         res = fn(args, rank, world)
     if rank == 0:
         print(json.dumps(res), flush=True)

@@ -339,7 +339,7 @@ void groupnorm_stats(const Tensor& x, const optional<Tensor>& gamma, const optio
   check_f32(shift, "shift");
   const int N = x.size(0), HW = x.size(1), C = x.size(2);
   SHAI_CHECK(C % 8 == 0 && C % G == 0 && C <= 4096 && G <= 128, "groupnorm: bad C/G");
-  SHAI_CHECK(partials.numel() >= (long)N * shai::gn_num_blocks(HW) * G * 2, "partials too small");
+  SHAI_CHECK(partials.numel() >= (long)N * shai::gn_num_blocks(N, HW, C) * G * 2, "partials too small");
   SHAI_CHECK(scale.numel() >= (long)N * C && shift.numel() >= (long)N * C, "scale/shift too small");
   shai::GroupNormArgs a{};
   a.x = cptr(x);

@@ -38,7 +38,7 @@ struct GroupNormArgs {
   float eps;
   int silu;
 };
-int gn_num_blocks(int HW);
+int gn_num_blocks(int N, int HW, int C);
 void launch_groupnorm_stats(const GroupNormArgs& a, hipStream_t s);
 void launch_groupnorm_apply(const GroupNormArgs& a, hipStream_t s);
 

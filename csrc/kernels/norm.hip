@@ -309,16 +309,22 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
-int gn_num_blocks(int HW) {
-  // ~256 pixels per block (one partial slot each), at most 256 slots per sample
-  int nb = (HW + 255) / 256;
+int gn_num_blocks(int N, int HW, int C) {
+  // Enough blocks to cover the chip (>= ~2048 workgroups over 256 CUs; 256 pixels/block left the
+  // 16x16x1280 UNet levels on 16 CUs), but each block still reduces >= 16 KB so the per-block LDS
+  // reduction stays amortised.  At most 256 partial slots per sample (finalize / workspace bound).
+  const long bytes = (long)HW * C * 2;
+  int by_size = (int)(bytes / (16 << 10));
+  int want = (2048 + N - 1) / N;
+  int nb = want < by_size ? want : by_size;
+  if (nb > HW) nb = HW;
   if (nb > 256) nb = 256;
   if (nb < 1) nb = 1;
   return nb;
 }
 
 void launch_groupnorm_stats(const GroupNormArgs& a, hipStream_t s) {
-  const int NB = gn_num_blocks(a.HW);
+  const int NB = gn_num_blocks(a.N, a.HW, a.C);
   const int ppb = (a.HW + NB - 1) / NB;
   const int C8 = a.C / 8;
   const int P = C8 <= 256 ? 256 / C8 : 1;

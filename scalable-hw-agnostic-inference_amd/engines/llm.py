@@ -54,6 +54,9 @@ class Sequence_:
     output: List[int] = field(default_factory=list)
     blocks: List[int] = field(default_factory=list)
     n_cached: int = 0        # tokens whose K/V are in the cache
+    image: Optional[dict] = None                                 # preprocessed image (multimodal models)
+    img_pos: int = -1                                            # index of <|image|> in the prompt
+    cross_blocks: List[int] = field(default_factory=list)        # paged blocks holding the image K/V
     arrival: float = field(default_factory=time.perf_counter)
     first_token_time: Optional[float] = None
     finish_time: Optional[float] = None
@@ -114,7 +117,7 @@ def sample(logits: torch.Tensor, temps: torch.Tensor, top_k: torch.Tensor, top_p
 
 
 class _DecodeGraph:
-    def __init__(self, engine: "LLMEngine", Bc: int):
+    def __init__(self, engine: "LLMEngine", Bc: int, cross: bool = False):
         self.Bc = Bc
         dev = engine.device
         mb = engine.max_blocks
@@ -125,6 +128,14 @@ class _DecodeGraph:
         self.bt = torch.zeros(Bc, mb, dtype=torch.int32, device=dev)
         self.splits = ops.decode_splits(Bc, engine.model.kv_heads_local, engine.max_model_len)
         self.batch = Batch(self.ids, self.pos, self.slots, self.bt, self.lens, None, Bc, 1, False, self.splits)
+        self.cross = cross
+        if cross:  # static image-K/V inputs of the cross-attention layers
+            b = self.batch
+            b.cross_bt = torch.zeros(Bc, engine.max_cross_blocks, dtype=torch.int32, device=dev)
+            b.cross_lens = torch.ones(Bc, dtype=torch.int32, device=dev)
+            b.cross_attn_rows = torch.zeros(Bc, dtype=torch.bool, device=dev)
+            b.cross_mlp_rows = torch.zeros(Bc, dtype=torch.bool, device=dev)
+            b.cross_splits = ops.decode_splits(Bc, engine.model.kv_heads_local, engine.cross_tokens)
         self.graph = None
         self.engine = engine
         if engine.use_graphs:
@@ -138,7 +149,7 @@ class _DecodeGraph:
             with torch.cuda.graph(self.graph):
                 self.logits = engine.model(self.batch, engine.kv)
 
-    def run(self, ids, pos, slots, lens, bt):
+    def run(self, ids, pos, slots, lens, bt, cross=None):
         B = len(ids)
         self.ids[:B].copy_(torch.from_numpy(np.asarray(ids, dtype=np.int32)), non_blocking=True)
         self.pos[:B].copy_(torch.from_numpy(pos), non_blocking=True)
@@ -149,6 +160,19 @@ class _DecodeGraph:
             self.slots[B:].fill_(-1)
             self.lens[B:].fill_(1)
             self.bt[B:].zero_()
+        if self.cross:
+            cbt, clens, has = cross
+            b = self.batch
+            b.cross_bt[:B].copy_(torch.from_numpy(cbt), non_blocking=True)
+            b.cross_lens[:B].copy_(torch.from_numpy(clens), non_blocking=True)
+            hb = torch.from_numpy(has)
+            b.cross_attn_rows[:B].copy_(hb, non_blocking=True)
+            b.cross_mlp_rows[:B].copy_(hb, non_blocking=True)
+            if B < self.Bc:
+                b.cross_bt[B:].zero_()
+                b.cross_lens[B:].fill_(1)
+                b.cross_attn_rows[B:].fill_(False)
+                b.cross_mlp_rows[B:].fill_(False)
         if self.graph is not None:
             self.graph.replay()
             return self.logits[:B]
@@ -160,26 +184,34 @@ class LLMEngine:
                  max_num_seqs: int = 64, max_model_len: int = 4096, num_kv_blocks: Optional[int] = None,
                  gpu_memory_utilization: float = 0.85, prefill_token_budget: int = 8192, use_graphs: bool = True,
                  enable_prefix_caching: bool = True):
+        from ..models.mllama import MllamaConfig, MllamaForConditionalGeneration
         from ..runtime import BlockManager
+        self.mcfg = cfg if isinstance(cfg, MllamaConfig) else None
+        if self.mcfg is not None:
+            cfg = self.mcfg.text
         self.cfg = cfg
         self.device = torch.device(device)
         with torch.device(self.device):
-            self.model = LlamaForCausalLM(cfg)
+            self.model = (MllamaForConditionalGeneration(self.mcfg) if self.mcfg is not None
+                          else LlamaForCausalLM(cfg))
         materialize(self.model, self.device, model_path, None, seed)
         self.model.fold_norms()  # before any graph capture (re-folded lazily after a later load)
         self.weights = self.model._shai_weights
         self.max_num_seqs = max_num_seqs
         self.max_model_len = min(max_model_len, cfg.max_position_embeddings)
         self.max_blocks = (self.max_model_len + KV_BLOCK - 1) // KV_BLOCK
+        self.cross_tokens = self.model.tokens_per_image if self.mcfg is not None else 0
+        self.max_cross_blocks = (self.cross_tokens + KV_BLOCK - 1) // KV_BLOCK
         hk = self.model.kv_heads_local
+        per_seq = self.max_blocks + self.max_cross_blocks
         if num_kv_blocks is None:
             if self.device.type == "cuda":
                 free, total = torch.cuda.mem_get_info(self.device)
                 budget = free - (1 - gpu_memory_utilization) * total
                 num_kv_blocks = int(max(budget, 0) // kv_bytes_per_block(cfg, hk))
-                num_kv_blocks = max(16, min(num_kv_blocks, max_num_seqs * self.max_blocks + 64))
+                num_kv_blocks = max(16, min(num_kv_blocks, max_num_seqs * per_seq + 64))
             else:
-                num_kv_blocks = max_num_seqs * self.max_blocks + 8
+                num_kv_blocks = max_num_seqs * per_seq + 8
         self.num_kv_blocks = num_kv_blocks
         self.kv_buf, self.kv = allocate_kv_cache(cfg, hk, num_kv_blocks, self.device)
         self.bm = BlockManager(num_kv_blocks)
@@ -189,17 +221,31 @@ class LLMEngine:
         self.waiting: List[Sequence_] = []
         self.running: List[Sequence_] = []
         self._ids = itertools.count()
-        self._graphs: Dict[int, _DecodeGraph] = {}
+        self._graphs: Dict[tuple, _DecodeGraph] = {}
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "steps": 0, "prefix_hit_tokens": 0}
         self.eos = {cfg.eos_token_id}
 
     # ------------------------------------------------------------------ requests
-    def add_request(self, prompt: Sequence[int], params: Optional[SamplingParams] = None) -> Sequence_:
+    def add_request(self, prompt: Sequence[int], params: Optional[SamplingParams] = None, image=None) -> Sequence_:
+        """image: PIL image / HWC uint8 array / preprocess_image() dict (multimodal models only); the prompt
+        gets an ``<|image|>`` token after BOS if it has none."""
         params = params or SamplingParams()
         prompt = list(prompt)[-(self.max_model_len - 1):] or [self.cfg.bos_token_id]
-        s = Sequence_(next(self._ids), prompt, params)
+        img = None
+        pos = -1
+        if image is not None:
+            if self.mcfg is None:
+                raise ValueError("this model has no vision tower; drop the image or load Llama-3.2-Vision")
+            from ..models.mllama import preprocess_image
+            img = image if isinstance(image, dict) else preprocess_image(image, self.mcfg.vision, self.device)
+            itok = self.mcfg.image_token_index
+            if itok not in prompt:
+                at = 1 if prompt and prompt[0] == self.cfg.bos_token_id else 0
+                prompt = prompt[:at] + [itok] + prompt[at:]
+            pos = prompt.index(itok)
+        s = Sequence_(next(self._ids), prompt, params, image=img, img_pos=pos)
         self.waiting.append(s)
         return s
 
@@ -217,8 +263,9 @@ class LLMEngine:
         return True
 
     def _free(self, s: Sequence_):
-        self.bm.release(s.blocks)
+        self.bm.release(s.blocks + s.cross_blocks)
         s.blocks = []
+        s.cross_blocks = []
 
     def _prefix_hashes(self, toks: Sequence[int], n_full: int) -> List[int]:
         hs, h = [], 0
@@ -235,13 +282,25 @@ class LLMEngine:
         watermark = max(1, len(self.running))
         n = sched_admit([len(s.prompt) for s in self.waiting], self.bm.num_free, len(self.running),
                         self.max_num_seqs, self.prefill_token_budget, watermark)
+        if self.mcfg is not None:  # image K/V blocks are outside the native scheduler's block budget
+            free, k = self.bm.num_free - watermark, 0
+            for s in self.waiting[:n]:
+                need = (len(s.prompt) + KV_BLOCK) // KV_BLOCK + (self.max_cross_blocks if s.image is not None else 0)
+                if need > free:
+                    break
+                free -= need
+                k += 1
+            if k == 0 and n > 0 and not self.running:
+                raise MemoryError("KV block pool too small for one multimodal request")
+            n = k
         adm = self.waiting[:n]
         del self.waiting[:n]
         return adm
 
     def _prefill(self, seqs: List[Sequence_]):
         for s in seqs:
-            if self.prefix_caching:
+            s._hashes = []
+            if self.prefix_caching and s.image is None:  # image prompts: K/V depend on the image, not cached
                 n_full = (len(s.prompt) - 1) // KV_BLOCK
                 hs = self._prefix_hashes(s.prompt, n_full)
                 got = self.bm.lookup_prefix(hs)
@@ -251,6 +310,8 @@ class LLMEngine:
                 self.stats["prefix_hit_tokens"] += s.n_cached
             ok = self._ensure_blocks(s, len(s.prompt) + 1)
             assert ok, "scheduler admitted a prompt without blocks"
+            if s.image is not None and not s.cross_blocks:
+                s.cross_blocks = self.bm.allocate(self.max_cross_blocks)
         S = max(len(s.prompt) - s.n_cached for s in seqs)
         from ..runtime import build_prefill
         pos, slots, lens, qlens, bt, last = build_prefill([s.n_cached for s in seqs],
@@ -263,6 +324,9 @@ class LLMEngine:
         d = self.device
         t = lambda a: torch.from_numpy(a).to(d, non_blocking=True)
         batch = Batch(t(ids), t(pos), t(slots), t(bt), t(lens), t(qlens), len(seqs), S, True, 1, t(last).long())
+        if any(s.image is not None for s in seqs):
+            self._encode_images([s for s in seqs if s.image is not None])
+            self._attach_cross_prefill(batch, seqs, S)
         logits = self.model(batch, self.kv)
         self.stats["prefill_tokens"] += int(sum(len(s.prompt) - s.n_cached for s in seqs))
         for s in seqs:
@@ -271,6 +335,45 @@ class LLMEngine:
                 for i, h in enumerate(s._hashes):
                     self.bm.register(s.blocks[i], h)
         self._sample_and_append(seqs, logits)
+
+    # ------------------------------------------------------------------ images (multimodal models)
+    def _encode_images(self, seqs: List[Sequence_]):
+        """Vision tower + projector for every new image, then each cross layer's K/V into the sequence's
+        image blocks (once per request; decode steps only read them)."""
+        d = self.device
+        px = torch.stack([s.image["pixel_values"].to(d) for s in seqs])
+        ar = torch.tensor([s.image["aspect_ratio_id"] for s in seqs], device=d)
+        states = self.model.encode_images(px, ar, [s.image["num_tiles"] for s in seqs])
+        nv = np.arange(self.cross_tokens)
+        slots = np.concatenate([np.asarray(s.cross_blocks, np.int64)[nv // KV_BLOCK] * KV_BLOCK + nv % KV_BLOCK
+                                for s in seqs]).astype(np.int32)
+        self.model.write_cross_kv(states.reshape(-1, states.shape[-1]), self.kv, torch.from_numpy(slots).to(d))
+
+    def _cross_tables(self, seqs: List[Sequence_]):
+        B, P = len(seqs), self.mcfg.vision.num_patches
+        cbt = np.zeros((B, self.max_cross_blocks), np.int32)
+        clens = np.ones(B, np.int32)
+        has = np.zeros(B, bool)
+        for i, s in enumerate(seqs):
+            if s.cross_blocks:
+                cbt[i] = s.cross_blocks
+                clens[i] = s.image["num_tiles"] * P
+                has[i] = True
+        return cbt, clens, has
+
+    def _attach_cross_prefill(self, batch: Batch, seqs: List[Sequence_], S: int):
+        cbt, clens, has = self._cross_tables(seqs)
+        full = np.where(has, self.cross_tokens, 1).astype(np.int32)
+        pre = np.asarray([max(0, s.img_pos - s.n_cached) if s.cross_blocks else 0 for s in seqs], np.int32)
+        pre_rows = (np.arange(S)[None, :] < pre[:, None]) & has[:, None]
+        attn_rows = np.repeat(has[:, None], S, axis=1)
+        d = self.device
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(d, non_blocking=True)
+        batch.cross_bt, batch.cross_lens, batch.cross_full_lens = t(cbt), t(clens), t(full)
+        batch.cross_pre_lens = t(pre) if pre.any() else None
+        batch.cross_pre_rows = t(pre_rows.reshape(-1))
+        batch.cross_attn_rows = t(attn_rows.reshape(-1))
+        batch.cross_mlp_rows = t((attn_rows & ~pre_rows).reshape(-1))
 
     def _decode(self, seqs: List[Sequence_]):
         from ..runtime import build_decode
@@ -290,10 +393,12 @@ class LLMEngine:
         pos, slots, lens, bt = build_decode([s.length - 1 for s in seqs], [s.blocks for s in seqs], self.max_blocks)
         ids = [s.tokens[-1] for s in seqs]
         Bc = 1 << max(0, math.ceil(math.log2(B)))
-        g = self._graphs.get(Bc)
+        cross = self._cross_tables(seqs) if any(s.cross_blocks for s in seqs) else None
+        key = (Bc, cross is not None)
+        g = self._graphs.get(key)
         if g is None:
-            g = self._graphs[Bc] = _DecodeGraph(self, Bc)
-        logits = g.run(ids, pos, slots, lens, bt)
+            g = self._graphs[key] = _DecodeGraph(self, Bc, cross=cross is not None)
+        logits = g.run(ids, pos, slots, lens, bt, cross)
         self.stats["decode_tokens"] += B
         for s in seqs:
             s.n_cached = s.length
@@ -421,8 +526,12 @@ class LLMService:
                 while True:
                     item = self._q.get(block=block, timeout=None if block else 0)
                     block = False
-                    ids, params, fut = item
-                    s = self.engine.add_request(ids, params)
+                    ids, params, fut, image = item
+                    try:
+                        s = self.engine.add_request(ids, params, image=image)
+                    except Exception as e:  # bad request (e.g. image for a text-only model)
+                        fut.set_exception(e)
+                        continue
                     self._futs[s.seq_id] = (s, fut)
             except queue.Empty:
                 pass
@@ -442,11 +551,15 @@ class LLMService:
                 if ent is not None:
                     ent[1].set_result(s)
 
-    def submit_ids(self, ids, params: SamplingParams):
+    def submit_ids(self, ids, params: SamplingParams, image=None):
         from concurrent.futures import Future
         f = Future()
-        self._q.put((list(ids), params, f))
+        self._q.put((list(ids), params, f, image))
         return f
+
+    @property
+    def multimodal(self) -> bool:
+        return self.engine.mcfg is not None
 
     def encode(self, text: str):
         if self.tokenizer is None:
@@ -456,23 +569,29 @@ class LLMService:
         ids = ids[0] if hasattr(ids, "dim") and ids.dim() == 2 else ids
         return [int(i) for i in (ids.tolist() if hasattr(ids, "tolist") else ids)]
 
-    def generate_text(self, prompt: str, params: SamplingParams, timeout: Optional[float] = None):
+    def generate_text(self, prompt: str, params: SamplingParams, timeout: Optional[float] = None, image=None):
         t0 = time.time()
-        s = self.submit_ids(self.encode(prompt), params).result(timeout)
+        s = self.submit_ids(self.encode(prompt), params, image).result(timeout)
         text = self.tokenizer.decode(s.output, skip_special_tokens=True)
         return text, time.time() - t0, s
 
 
 def llama_config_for(model_id: str, model_path: Optional[str] = None, size: str = "") -> LlamaConfig:
     import json
+    from ..models.mllama import MllamaConfig
     if model_path and os.path.exists(os.path.join(model_path, "config.json")):
         with open(os.path.join(model_path, "config.json")) as f:
             d = json.load(f)
+        if "vision_config" in d and "text_config" in d:
+            return MllamaConfig.from_hf(d)
         d = d.get("text_config", d)
         return LlamaConfig.from_hf(d)
     m = (model_id or "").lower()
+    vision = "vision" in m or "mllama" in m
     if size == "tiny":
-        return LlamaConfig.tiny()
+        return MllamaConfig.tiny() if vision else LlamaConfig.tiny()
+    if vision:
+        return MllamaConfig.llama32_11b_vision()
     if "70b" in m or "deepseek" in m:
         return LlamaConfig.deepseek_r1_distill_70b() if "deepseek" in m else LlamaConfig.llama3_70b()
     if "llama" in m:

@@ -125,6 +125,15 @@ class Batch:
     is_prefill: bool
     num_splits: int = 1             # decode split-K
     last_index: Optional[torch.Tensor] = None  # [B] flat index of each sequence's last token (prefill)
+    # cross-attention to image K/V (Llama-3.2-Vision; see models/mllama.py), None for text-only steps
+    cross_bt: Optional[torch.Tensor] = None         # [B, max_cross_blocks] int32 image K/V blocks
+    cross_lens: Optional[torch.Tensor] = None       # [B] int32 valid-tile image tokens (>= 1)
+    cross_full_lens: Optional[torch.Tensor] = None  # [B] int32 all-tile image tokens (rows before <|image|>)
+    cross_pre_lens: Optional[torch.Tensor] = None   # [B] int32 rows before <|image|> (prefill; None if none)
+    cross_pre_rows: Optional[torch.Tensor] = None   # [T] bool row is before <|image|>
+    cross_attn_rows: Optional[torch.Tensor] = None  # [T] bool row's sequence has an image
+    cross_mlp_rows: Optional[torch.Tensor] = None   # [T] bool cross MLP applies (image, at/after <|image|>)
+    cross_splits: int = 1
 
 
 class LlamaAttention(nn.Module):

@@ -13,8 +13,10 @@ is honoured (the _m variant's behaviour).  Engine kwargs can come from a
 /vllm_config.yaml-style file (``VLLM_CONFIG``): tensor_parallel_size,
 max_num_seqs, max_model_len, block_size (rounded to 64-token KV blocks).
 
-``image``: decoded and validated; the Llama-3.2-Vision cross-attention tower is
-not implemented, so the image is acknowledged but not attended to (see README).
+``image``: with a Llama-3.2-Vision model (``MODEL_ID`` containing "vision", or a
+local checkpoint with a ``vision_config``) the image goes through the native
+vision tower and the decoder's cross-attention layers (models/mllama.py); a
+text-only model validates and acknowledges it without attending to it.
 """
 
 import base64
@@ -40,12 +42,16 @@ def build_service(env: ServerEnv):
     from ..tokenizers import load_tokenizer
     vc = load_vllm_config(os.environ.get("VLLM_CONFIG", "/vllm_config.yaml"))
     cfg = llama_config_for(env.model_id, env.model_path, env.config)
+    text = getattr(cfg, "text", cfg)   # MllamaConfig (vision) or LlamaConfig
     eng = LLMEngine(cfg, device=env.torch_device, model_path=env.model_path,
                     max_num_seqs=int(vc.get("max_num_seqs", 64)),
-                    max_model_len=int(vc.get("max_model_len", min(8192, cfg.max_position_embeddings))),
+                    max_model_len=int(vc.get("max_model_len", min(8192, text.max_position_embeddings))),
                     enable_prefix_caching=True)
-    tok = load_tokenizer(env.model_path, vocab_size=cfg.vocab_size, bos_id=cfg.bos_token_id, eos_id=cfg.eos_token_id,
-                         pad_id=0, model_max_length=eng.max_model_len)
+    specials = {"<|begin_of_text|>": text.bos_token_id}
+    if text is not cfg:
+        specials["<|image|>"] = cfg.image_token_index
+    tok = load_tokenizer(env.model_path, vocab_size=text.vocab_size, bos_id=text.bos_token_id,
+                         eos_id=text.eos_token_id, pad_id=0, model_max_length=eng.max_model_len, specials=specials)
     return LLMService(eng, tok)
 
 
@@ -53,6 +59,14 @@ def _decode_image(b64: str):
     from PIL import Image
     raw = base64.b64decode(b64.split(",", 1)[-1])
     return Image.open(io.BytesIO(raw)).convert("RGB")
+
+
+def add_instruct(prompt: str, has_image: bool) -> str:
+    """Llama-3 instruct turn around the user prompt, with the image placeholder first when an image is
+    attached (the formatting app/vllm_model_api_m.py:47 applies through NxDI's ``add_instruct``)."""
+    img = "<|image|>" if has_image else ""
+    return (f"<|begin_of_text|><|start_header_id|>user<|end_header_id|>\n\n{img}{prompt}<|eot_id|>"
+            f"<|start_header_id|>assistant<|end_header_id|>\n\n")
 
 
 def create_app(service=None, env: Optional[ServerEnv] = None):
@@ -83,11 +97,16 @@ def create_app(service=None, env: Optional[ServerEnv] = None):
     def params(n):
         return SamplingParams(temperature=0.7, top_k=50, top_p=0.9, max_tokens=max(1, int(n)))
 
+    multimodal = bool(getattr(service, "multimodal", False))
+
     def gentext(prompt: str, max_new_tokens: int, image_b64: Optional[str] = None):
+        image = None
         if image_b64:
-            _decode_image(image_b64)  # validate; vision tower not implemented (see module doc)
-            prompt = "<|image|>" + prompt
-        text, secs, _ = service.generate_text(prompt, params(max_new_tokens))
+            image = _decode_image(image_b64)
+            prompt = add_instruct(prompt, True)
+            if not multimodal:
+                image = None  # text-only model: the image is validated and acknowledged, not attended to
+        text, secs, _ = service.generate_text(prompt, params(max_new_tokens), image=image)
         return text, secs
 
     def bench(n_runs, test_name, prompt, max_new_tokens):

@@ -25,24 +25,37 @@ class HashTokenizer:
     """Deterministic offline tokenizer: word -> crc32 bucket in [n_special, vocab)."""
 
     def __init__(self, vocab_size: int, bos_id: Optional[int] = None, eos_id: Optional[int] = None, pad_id: int = 0,
-                 model_max_length: int = 77, n_special: int = 256):
+                 model_max_length: int = 77, n_special: int = 256, specials: Optional[dict] = None):
         self.vocab_size = vocab_size
         self.bos_token_id, self.eos_token_id, self.pad_token_id = bos_id, eos_id, pad_id
         self.model_max_length = model_max_length
         self.n_special = min(n_special, vocab_size // 4)
-        specials = {i for i in (bos_id, eos_id, pad_id) if i is not None}
+        # literal special-token strings (e.g. "<|image|>") -> fixed ids, matched before word splitting
+        self.specials = dict(specials or {})
+        self._special_re = (re.compile("(" + "|".join(re.escape(s) for s in sorted(self.specials, key=len,
+                                                                                    reverse=True)) + ")")
+                            if self.specials else None)
+        fixed = {i for i in (bos_id, eos_id, pad_id) if i is not None}
         self._hi = vocab_size
-        while self._hi - 1 in specials:
+        while self._hi - 1 in fixed:
             self._hi -= 1
 
     def _tok(self, w: str) -> int:
         span = max(1, self._hi - self.n_special)
         return self.n_special + zlib.crc32(w.encode()) % span
 
+    def _words(self, text: str) -> List[int]:
+        return [self._tok(w) for w in re.findall(r"\w+|[^\w\s]", text.lower())]
+
     def encode(self, text: str, add_special_tokens: bool = True) -> List[int]:
-        ids = [self._tok(w) for w in re.findall(r"\w+|[^\w\s]", text.lower())]
+        if self._special_re is None:
+            ids = self._words(text)
+        else:
+            ids = []
+            for part in self._special_re.split(text):
+                ids += [self.specials[part]] if part in self.specials else self._words(part)
         if add_special_tokens:
-            if self.bos_token_id is not None:
+            if self.bos_token_id is not None and not (ids and ids[0] == self.bos_token_id):
                 ids = [self.bos_token_id] + ids
             if self.eos_token_id is not None:
                 ids = ids + [self.eos_token_id]
@@ -84,7 +97,7 @@ class HashTokenizer:
 
 
 def load_tokenizer(path: Optional[str], *, vocab_size: int, bos_id=None, eos_id=None, pad_id=0,
-                   model_max_length: int = 77, subfolder: Optional[str] = None):
+                   model_max_length: int = 77, subfolder: Optional[str] = None, specials: Optional[dict] = None):
     """HF fast tokenizer from a local directory if available, else HashTokenizer."""
     if path:
         d = os.path.join(path, subfolder) if subfolder else path
@@ -96,4 +109,4 @@ def load_tokenizer(path: Optional[str], *, vocab_size: int, bos_id=None, eos_id=
                 return tok
             except Exception:  # pragma: no cover - depends on local files
                 pass
-    return HashTokenizer(vocab_size, bos_id, eos_id, pad_id, model_max_length)
+    return HashTokenizer(vocab_size, bos_id, eos_id, pad_id, model_max_length, specials=specials)

@@ -72,6 +72,19 @@ def test_llm_api_server():
     assert rep.startswith("RESULT FOR benchmark:mistral on mi355x with 4 output tokens: Latency P0=")
 
 
+def test_llm_api_multimodal_server():
+    """Llama-3.2-Vision (tiny) behind the vllm_model_api_m.py schema: the image is attended to."""
+    from shai_amd.serving import llm_api
+    c = TestClient(llm_api.create_app(env=env(app="mllama", model_id="meta-llama/Llama-3.2-11B-Vision-Instruct")))
+    svc = c.app.state.service
+    assert svc.multimodal
+    r = c.post("/generate", json={"prompt": "Describe this image", "max_new_tokens": 3, "image": _img_b64()})
+    assert r.status_code == 200 and set(r.json()) == {"text", "execution_time"}
+    ids = svc.encode(llm_api.add_instruct("Describe this image", True))
+    assert ids.count(svc.engine.mcfg.image_token_index) == 1 and ids[0] == svc.engine.cfg.bos_token_id
+    assert svc.engine.bm.num_free == svc.engine.num_kv_blocks
+
+
 def test_llm_gradio_server():
     from shai_amd.serving import llm_gradio
     c = TestClient(llm_gradio.create_app(env=env(app="llama")))
