@@ -45,9 +45,16 @@ def _load_kernels() -> None:
             _kernels_error = e
 
 
+DEFAULT_TUNE_FILE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "config",
+                                 "gemm_tuning_mi355x.json")
+
+
 def _autoload_tuning() -> None:
-    path = os.environ.get("SHAI_GEMM_TUNE_FILE")
-    if path and os.path.exists(path):
+    """Pre-load GEMM tile/split-K choices measured on MI355X (config/gemm_tuning_mi355x.json, or
+    ``SHAI_GEMM_TUNE_FILE``; "none" disables) so serving warm-up skips the per-shape autotune sweep.
+    Shapes missing from the file are still autotuned on first use."""
+    path = os.environ.get("SHAI_GEMM_TUNE_FILE", DEFAULT_TUNE_FILE)
+    if path and path != "none" and os.path.exists(path):
         load_gemm_tuning(path)
 
 
