@@ -1,5 +1,6 @@
-// One-shot all-reduce over xGMI peer memory for small, latency-bound tensor-parallel
-// messages (LLM decode: [B, 4096] bf16 after o_proj / down_proj, a few KB to ~1 MB).
+// All-reduce over xGMI peer memory for tensor-parallel messages: a one-shot kernel for small,
+// latency-bound ones (LLM decode: [B, 4096] bf16 after o_proj / down_proj, a few KB to ~1 MB) and a
+// two-shot reduce-scatter + all-gather kernel (p2p_two_shot, below) for mid-size ones (Flux / prefill).
 //
 // RCCL's ring/tree all-reduce pays several link latencies per call; on a fully
 // connected 8x MI355X node every GPU can instead READ every peer's buffer
@@ -98,6 +99,78 @@ __global__ void __launch_bounds__(512) p2p_one_shot(Peers P, int rank, int world
   barrier_phase(P, me, 1, rank, world, epoch);
 }
 
+__device__ __forceinline__ uint4 pack_bf16x8(const float acc[8]) {
+  uint32_t o[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {  // round-to-nearest-even to bf16
+    uint32_t lo = __float_as_uint(acc[2 * e]), hi = __float_as_uint(acc[2 * e + 1]);
+    lo = (lo + 0x7fffu + ((lo >> 16) & 1u)) >> 16;
+    hi = (hi + 0x7fffu + ((hi >> 16) & 1u)) >> 16;
+    o[e] = lo | (hi << 16);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// Two-shot (reduce-scatter + all-gather) all-reduce for mid-size messages (Flux / prefill row-parallel
+// outputs, 0.5-64 MiB).  The message is cut into `world` segments; rank r owns segment r.
+//   phase 0: copy the input into the local staging slot A (only the positions this block will hand out),
+//   barrier, phase 1: sum segment r over every rank's slot A (world-1 remote reads of M/world each, all xGMI
+//   links busy at once) into the local slot B, barrier, phase 2: gather every segment s from rank s's slot B
+//   into the output.  Per rank (world-1)/world * M crosses the links twice, vs 2 (world-1)/world * M through
+//   ONE link per direction for a single ring.  Block b of every rank touches the same positions in every
+//   phase, so the per-block flag barriers order all the hand-offs (no grid-wide barrier); the next call's
+//   first barrier protects slot B from being overwritten while a peer still gathers it.
+__global__ void __launch_bounds__(512) p2p_two_shot(Peers P, int rank, int world, const uint4* in, uint4* out,
+                                                    long n16, size_t slot_bytes) {
+  __shared__ uint32_t s_epoch;
+  Layout* me = reinterpret_cast<Layout*>(P.base[rank]);
+  if (threadIdx.x == 0) {
+    const uint32_t e = me->epoch[blockIdx.x] + 1;
+    me->epoch[blockIdx.x] = e;
+    s_epoch = e;
+  }
+  __syncthreads();
+  const uint32_t epoch = s_epoch;
+  const long seg = (n16 + world - 1) / world;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  uint4* slotA = reinterpret_cast<uint4*>(P.base[rank] + kDataOff);
+  uint4* slotB = reinterpret_cast<uint4*>(P.base[rank] + kDataOff + slot_bytes);
+  for (int s = 0; s < world; ++s) {
+    const long beg = s * seg, end = min(n16, beg + seg);
+    for (long i = beg + t0; i < end; i += stride) slotA[i] = in[i];
+  }
+  __threadfence_system();
+  __syncthreads();
+  barrier_phase(P, me, 0, rank, world, epoch);
+  {
+    const long beg = rank * seg, end = min(n16, beg + seg);
+    for (long i = beg + t0; i < end; i += stride) {
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int r = 0; r < world; ++r) {
+        const int src = (rank + r) % world;  // stagger the peers so the links are loaded evenly
+        const uint4 v = reinterpret_cast<const uint4*>(P.base[src] + kDataOff)[i];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[2 * e] += __uint_as_float(w[e] << 16);
+          acc[2 * e + 1] += __uint_as_float(w[e] & 0xffff0000u);
+        }
+      }
+      slotB[i] = pack_bf16x8(acc);
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  barrier_phase(P, me, 1, rank, world, epoch);
+  for (int r = 0; r < world; ++r) {
+    const int s = (rank + r) % world;
+    const uint4* src = reinterpret_cast<const uint4*>(P.base[s] + kDataOff + slot_bytes);
+    const long beg = s * seg, end = min(n16, beg + seg);
+    for (long i = beg + t0; i < end; i += stride) out[i] = src[i];
+  }
+}
+
 struct Ctx {
   int rank, world, device;
   size_t max_bytes;
@@ -118,8 +191,9 @@ void* shai_p2p_create(int rank, int world, size_t max_bytes, char* handle_out) {
   c->world = world;
   c->max_bytes = max_bytes;
   hipGetDevice(&c->device);
-  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->local), kDataOff + max_bytes, hipDeviceMallocUncached) !=
-      hipSuccess) {
+  // signal area | slot A (staging, both algorithms) | slot B (two-shot reduced segments)
+  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->local), kDataOff + 2 * max_bytes,
+                            hipDeviceMallocUncached) != hipSuccess) {
     delete c;
     return nullptr;
   }
@@ -165,6 +239,20 @@ int shai_p2p_allreduce_bf16(void* ctx, const void* in, void* out, size_t bytes, 
   // every rank must use the same grid: it is a function of bytes only
   hipLaunchKernelGGL(p2p_one_shot, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world,
                      static_cast<const uint4*>(in), static_cast<uint4*>(out), n16);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// Two-shot (reduce-scatter + all-gather) bf16 sum for mid-size messages; same contract as above.
+int shai_p2p_allreduce2_bf16(void* ctx, const void* in, void* out, size_t bytes, hipStream_t stream) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (bytes % 16 != 0 || bytes > c->max_bytes) return -1;
+  const long n16 = (long)(bytes / 16);
+  const long per_rank = (n16 + c->world - 1) / c->world;
+  int blocks = (int)((per_rank + 511) / 512);
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(p2p_two_shot, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world,
+                     static_cast<const uint4*>(in), static_cast<uint4*>(out), n16, c->max_bytes);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -9,7 +9,9 @@ Per engine step (one call to :meth:`LLMEngine.step`):
   1. the native scheduler (csrc/runtime/scheduler.cpp) admits waiting prompts
      FCFS under KV-block / sequence / token budgets;
   2. admitted prompts run as one padded prefill batch (prefix-cached blocks are
-     reused via the native block manager's content hashes);
+     reused via the native block manager's content hashes); prompts longer than
+     ``prefill_chunk`` are prefilled chunk by chunk, the chunks alternating with
+     decode steps so running sequences keep streaming (chunked prefill);
   3. otherwise every running sequence decodes one token -- the decode forward
      for each batch-size bucket is captured once into a HIP graph and replayed;
   4. sampling (temperature / top-k / top-p; greedy at temperature 0) on device.
@@ -57,6 +59,7 @@ class Sequence_:
     image: Optional[dict] = None                                 # preprocessed image (multimodal models)
     img_pos: int = -1                                            # index of <|image|> in the prompt
     cross_blocks: List[int] = field(default_factory=list)        # paged blocks holding the image K/V
+    prefill_started: bool = False                                # first prefill chunk done (blocks held)
     arrival: float = field(default_factory=time.perf_counter)
     first_token_time: Optional[float] = None
     finish_time: Optional[float] = None
@@ -183,7 +186,7 @@ class LLMEngine:
     def __init__(self, cfg: LlamaConfig, device="cuda", model_path: Optional[str] = None, seed: int = 0,
                  max_num_seqs: int = 64, max_model_len: int = 4096, num_kv_blocks: Optional[int] = None,
                  gpu_memory_utilization: float = 0.85, prefill_token_budget: int = 8192, use_graphs: bool = True,
-                 enable_prefix_caching: bool = True):
+                 enable_prefix_caching: bool = True, prefill_chunk: Optional[int] = None):
         from ..models.mllama import MllamaConfig, MllamaForConditionalGeneration
         from ..runtime import BlockManager
         self.mcfg = cfg if isinstance(cfg, MllamaConfig) else None
@@ -216,6 +219,9 @@ class LLMEngine:
         self.kv_buf, self.kv = allocate_kv_cache(cfg, hk, num_kv_blocks, self.device)
         self.bm = BlockManager(num_kv_blocks)
         self.prefill_token_budget = prefill_token_budget
+        # longest prompt slice one prefill step processes (chunked prefill; SURVEY 5.7: <= 8k tokens)
+        self.prefill_chunk = max(KV_BLOCK, prefill_chunk or prefill_token_budget)
+        self._last_step = "decode"
         self.prefix_caching = enable_prefix_caching
         self.use_graphs = use_graphs and self.device.type == "cuda"
         self.waiting: List[Sequence_] = []
@@ -298,7 +304,14 @@ class LLMEngine:
         return adm
 
     def _prefill(self, seqs: List[Sequence_]):
+        """One prefill chunk for each of ``seqs``: at most ``prefill_chunk`` new prompt tokens per sequence
+        (chunked prefill -- a long prompt spans several engine steps that alternate with decode steps of
+        the running batch).  The first chunk looks up cached prefix blocks and allocates the sequence's KV
+        (and image) blocks; only sequences whose prompt is complete sample their first token."""
         for s in seqs:
+            if s.prefill_started:
+                continue
+            s.prefill_started = True
             s._hashes = []
             if self.prefix_caching and s.image is None:  # image prompts: K/V depend on the image, not cached
                 n_full = (len(s.prompt) - 1) // KV_BLOCK
@@ -312,29 +325,39 @@ class LLMEngine:
             assert ok, "scheduler admitted a prompt without blocks"
             if s.image is not None and not s.cross_blocks:
                 s.cross_blocks = self.bm.allocate(self.max_cross_blocks)
-        S = max(len(s.prompt) - s.n_cached for s in seqs)
+                s._img_encoded = False
+        news = [min(len(s.prompt) - s.n_cached, self.prefill_chunk) for s in seqs]
+        S = max(news)
         from ..runtime import build_prefill
-        pos, slots, lens, qlens, bt, last = build_prefill([s.n_cached for s in seqs],
-                                                          [len(s.prompt) - s.n_cached for s in seqs],
+        pos, slots, lens, qlens, bt, last = build_prefill([s.n_cached for s in seqs], news,
                                                           [s.blocks for s in seqs], S, self.max_blocks)
         ids = np.zeros(len(seqs) * S, dtype=np.int32)
-        for i, s in enumerate(seqs):
-            new = s.prompt[s.n_cached:]
-            ids[i * S:i * S + len(new)] = new
+        for i, (s, n) in enumerate(zip(seqs, news)):
+            ids[i * S:i * S + n] = s.prompt[s.n_cached:s.n_cached + n]
         d = self.device
         t = lambda a: torch.from_numpy(a).to(d, non_blocking=True)
         batch = Batch(t(ids), t(pos), t(slots), t(bt), t(lens), t(qlens), len(seqs), S, True, 1, t(last).long())
-        if any(s.image is not None for s in seqs):
-            self._encode_images([s for s in seqs if s.image is not None])
-            self._attach_cross_prefill(batch, seqs, S)
+        if any(s.cross_blocks for s in seqs):
+            fresh = [s for s in seqs if s.cross_blocks and not s._img_encoded]
+            if fresh:
+                self._encode_images(fresh)
+                for s in fresh:
+                    s._img_encoded = True
+            self._attach_cross_prefill(batch, seqs, S, news)
         logits = self.model(batch, self.kv)
-        self.stats["prefill_tokens"] += int(sum(len(s.prompt) - s.n_cached for s in seqs))
-        for s in seqs:
-            s.n_cached = len(s.prompt)
+        self.stats["prefill_tokens"] += int(sum(news))
+        done = []
+        for i, (s, n) in enumerate(zip(seqs, news)):
+            s.n_cached += n
+            if s.n_cached < len(s.prompt):
+                continue
+            done.append(i)
             if self.prefix_caching:
-                for i, h in enumerate(s._hashes):
-                    self.bm.register(s.blocks[i], h)
-        self._sample_and_append(seqs, logits)
+                for j, h in enumerate(s._hashes):
+                    self.bm.register(s.blocks[j], h)
+        if done:
+            sel = logits if len(done) == len(seqs) else logits.index_select(0, torch.tensor(done, device=d))
+            self._sample_and_append([seqs[i] for i in done], sel)
 
     # ------------------------------------------------------------------ images (multimodal models)
     def _encode_images(self, seqs: List[Sequence_]):
@@ -361,10 +384,12 @@ class LLMEngine:
                 has[i] = True
         return cbt, clens, has
 
-    def _attach_cross_prefill(self, batch: Batch, seqs: List[Sequence_], S: int):
+    def _attach_cross_prefill(self, batch: Batch, seqs: List[Sequence_], S: int, news: List[int]):
         cbt, clens, has = self._cross_tables(seqs)
         full = np.where(has, self.cross_tokens, 1).astype(np.int32)
-        pre = np.asarray([max(0, s.img_pos - s.n_cached) if s.cross_blocks else 0 for s in seqs], np.int32)
+        # rows of this chunk that lie before <|image|>
+        pre = np.asarray([min(n, max(0, s.img_pos - s.n_cached)) if s.cross_blocks else 0
+                          for s, n in zip(seqs, news)], np.int32)
         pre_rows = (np.arange(S)[None, :] < pre[:, None]) & has[:, None]
         attn_rows = np.repeat(has[:, None], S, axis=1)
         d = self.device
@@ -382,6 +407,7 @@ class LLMEngine:
                 # preempt (recompute later): free blocks, requeue at the front
                 self._free(s)
                 s.n_cached = 0
+                s.prefill_started = False
                 s.prompt = s.prompt + s.output
                 s.output = []
                 self.running.remove(s)
@@ -428,11 +454,16 @@ class LLMEngine:
         """Run one engine iteration; returns sequences that finished in it."""
         self.stats["steps"] += 1
         adm = self._admit()
-        if adm:
+        pending = [s for s in self.running if s.n_cached < len(s.prompt)]     # mid chunked prefill
+        decodable = [s for s in self.running if s.n_cached >= len(s.prompt)]
+        # new prompts and remaining prefill chunks alternate with decode steps of the running batch
+        if adm or (pending and (not decodable or self._last_step != "prefill")):
             self.running += adm
-            self._prefill(adm)
-        elif self.running:
-            self._decode(list(self.running))
+            self._prefill(pending + adm)
+            self._last_step = "prefill"
+        elif decodable:
+            self._decode(decodable)
+            self._last_step = "decode"
         done = [s for s in self.running if s.finished]
         for s in done:
             self._free(s)

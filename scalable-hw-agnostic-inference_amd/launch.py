@@ -15,6 +15,7 @@ from .controller.failover import FailoverController
 from .router import Router, create_app
 from .serving.common import run
 from .supervisor import GPUInventory, Supervisor, WorkerSpec
+from .supervisor.health import GPUHealthMonitor
 
 
 def spec_factory(dep: dict):
@@ -59,6 +60,9 @@ def main():
         sup.wait_ready(name)
     router.apply_efficiency_weights()
     sup.monitor()
+    hc = cfg.get("health", {})
+    GPUHealthMonitor(sup, max_temp_c=float(hc.get("max_temp_c", 105)),
+                     hang_timeout_s=float(hc.get("hang_timeout_s", 120))).run(float(hc.get("interval_s", 10)))
     fo.run(float(cfg.get("failover", {}).get("interval_s", 300)))
 
     import threading

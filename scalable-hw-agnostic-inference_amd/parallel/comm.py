@@ -24,7 +24,8 @@ import torch.distributed as dist
 from .state import tp
 
 _P2P = None
-P2P_MAX_BYTES = int(os.environ.get("SHAI_P2P_MAX_BYTES", str(512 * 1024)))
+P2P_ONE_SHOT_MAX = int(os.environ.get("SHAI_P2P_ONE_SHOT_MAX", str(512 * 1024)))
+P2P_MAX_BYTES = int(os.environ.get("SHAI_P2P_MAX_BYTES", str(64 << 20)))
 
 
 def enable_p2p(p2p) -> None:
@@ -38,7 +39,7 @@ def all_reduce(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> to
     g = group if group is not None else st.group
     if st.size == 1 and group is None:
         return x
-    if _P2P is not None and x.is_cuda and x.numel() * x.element_size() <= P2P_MAX_BYTES and x.is_contiguous():
+    if _P2P is not None and x.is_cuda and x.numel() * x.element_size() <= _P2P.max_bytes and x.is_contiguous():
         return _P2P.all_reduce(x)
     dist.all_reduce(x, group=g)
     return x
@@ -67,22 +68,25 @@ def broadcast_object(obj, src: int = 0):
 
 
 class P2PAllReduce:
-    """One-shot bf16 all-reduce over IPC-mapped peer buffers (csrc/comm/p2p_allreduce.hip).
+    """bf16 all-reduce over IPC-mapped peer buffers (csrc/comm/p2p_allreduce.hip): one-shot (every rank
+    reads every peer's whole message) up to ``one_shot_max`` bytes, two-shot (reduce-scatter + all-gather
+    over all xGMI links at once) up to ``max_bytes``.
 
     Built once per TP group (handles exchanged with ``all_gather_object``), then used by
-    :func:`all_reduce` for contiguous bf16 messages up to ``max_bytes`` once registered with
-    :func:`enable_p2p` (``SHAI_P2P_ALLREDUCE=1`` in the engine).  Everything larger, or any
-    other dtype, goes to RCCL."""
+    :func:`all_reduce` for contiguous bf16 messages once registered with :func:`enable_p2p`
+    (``SHAI_P2P_ALLREDUCE=1`` in the engine).  Everything larger, or any other dtype, goes to RCCL."""
 
-    def __init__(self, group: Optional[dist.ProcessGroup] = None, max_bytes: int = P2P_MAX_BYTES):
+    def __init__(self, group: Optional[dist.ProcessGroup] = None, max_bytes: int = P2P_MAX_BYTES,
+                 one_shot_max: int = P2P_ONE_SHOT_MAX):
         import ctypes
         from .. import native
         self.lib = native.comm()
         self.lib.shai_p2p_create.restype = ctypes.c_void_p
         self.lib.shai_p2p_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_char_p]
         self.lib.shai_p2p_open.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
-        self.lib.shai_p2p_allreduce_bf16.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                                      ctypes.c_size_t, ctypes.c_void_p]
+        for fn in (self.lib.shai_p2p_allreduce_bf16, self.lib.shai_p2p_allreduce2_bf16):
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        self.one_shot_max = one_shot_max
         self.lib.shai_p2p_error.argtypes = [ctypes.c_void_p]
         self.lib.shai_p2p_destroy.argtypes = [ctypes.c_void_p]
         self.group = group
@@ -107,7 +111,8 @@ class P2PAllReduce:
             dist.all_reduce(x, group=self.group)
             return x
         st = torch.cuda.current_stream(x.device).cuda_stream
-        rc = self.lib.shai_p2p_allreduce_bf16(self.ctx, x.data_ptr(), x.data_ptr(), nbytes, st)
+        fn = self.lib.shai_p2p_allreduce_bf16 if nbytes <= self.one_shot_max else self.lib.shai_p2p_allreduce2_bf16
+        rc = fn(self.ctx, x.data_ptr(), x.data_ptr(), nbytes, st)
         if rc != 0:
             raise RuntimeError(f"p2p all-reduce launch failed ({rc})")
         return x

@@ -56,6 +56,10 @@ def init_distributed(backend: Optional[str] = None, tp_size: Optional[int] = Non
             if rank in ranks:
                 group = g
     _TP = TPState(rank % tp if tp > 1 else 0, tp, group, device)
+    if tp > 1 and use_gpu and os.environ.get("SHAI_P2P_ALLREDUCE", "0") == "1":
+        # custom xGMI peer all-reduce (one-shot / two-shot) for the TP group; RCCL stays the fallback
+        from .comm import P2PAllReduce, enable_p2p
+        enable_p2p(P2PAllReduce(group))
     return _TP
 
 

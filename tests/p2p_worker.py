@@ -1,5 +1,5 @@
-"""Two ranks on ONE GPU (gloo for the handle exchange): the IPC-mapped one-shot all-reduce
-must equal the sum of both ranks' tensors, repeatedly and inside a HIP graph."""
+"""Two ranks on ONE GPU (gloo for the handle exchange): the IPC-mapped one-shot and two-shot all-reduces
+must equal the sum of both ranks' tensors, repeatedly, at mixed sizes and inside a HIP graph."""
 import os
 
 import torch
@@ -11,8 +11,9 @@ def run(rank, world, port):
     dist.init_process_group("gloo")
     torch.cuda.set_device(0)
     from shai_amd.parallel.comm import P2PAllReduce
-    ar = P2PAllReduce(None, max_bytes=1 << 20)
-    for n in (8, 4096 * 32, 1 << 19):
+    ar = P2PAllReduce(None, max_bytes=8 << 20, one_shot_max=512 << 10)
+    # one-shot sizes, then two-shot (reduce-scatter + all-gather) sizes incl. an uneven segmentation
+    for n in (8, 4096 * 32, 1 << 18, 1 << 19, (3 << 20) + 8, 4 << 20):
         for it in range(3):
             torch.manual_seed(100 * it + n)
             full = [torch.randn(n, device="cuda").bfloat16() for _ in range(world)]

@@ -196,3 +196,48 @@ def test_orchestrator_uis_and_launch(tmp_path):
         assert load_models(str(mf))[0]["url"] == "http://10.0.0.1:9000"
     finally:
         sup.shutdown()
+
+
+def test_gpu_health_monitor_faults_and_recovery():
+    """ECC growth / overheating / a vanished device fail the slot (replica killed, not restarted there);
+    clean polls bring it back; a worker whose /health stays silent is killed by the hang watchdog."""
+    from shai_amd.supervisor import GPUInventory, Supervisor
+    from shai_amd.supervisor.health import GPUHealthMonitor
+
+    class P:  # stand-in process handle
+        def poll(self):
+            return None
+
+    sup = Supervisor(None, GPUInventory([0, 1, 2]))
+    killed = []
+    sup.kill = lambda name, sig=9: killed.append(name)
+    readings = {"recs": [{"gpu": 0, "temp_c": 60.0, "ecc_uncorrectable": 2},
+                         {"gpu": 1, "temp_c": 55.0, "ecc_uncorrectable": 0},
+                         {"gpu": 2, "temp_c": 50.0, "ecc_uncorrectable": 0}]}
+    healthy = {"ok": True}
+    mon = GPUHealthMonitor(sup, probe=lambda: readings["recs"], recover_after=2, hang_timeout_s=30,
+                           http_get=lambda url, t: healthy["ok"])
+    from shai_amd.supervisor import WorkerSpec
+    sup.specs["w1"] = WorkerSpec("w1", "m", gpus=[1], port=1234)
+    sup.procs["w1"] = P()
+    mon.check_devices()
+    assert not sup.inv.failed                       # baseline ECC counts are not faults
+    readings["recs"][0]["ecc_uncorrectable"] = 3    # new uncorrectable error on GPU 0
+    readings["recs"][1]["temp_c"] = 120.0           # GPU 1 overheating -> its worker is killed
+    readings["recs"] = readings["recs"][:2]         # GPU 2 vanished
+    mon.check_devices()
+    assert sup.inv.failed == {0, 1, 2} and "w1" in killed
+    assert sup.inv.allocate(1, "x") is None
+    readings["recs"] = [{"gpu": 0, "temp_c": 60.0, "ecc_uncorrectable": 3},
+                        {"gpu": 1, "temp_c": 70.0, "ecc_uncorrectable": 0}]
+    mon.check_devices()
+    mon.check_devices()
+    assert sup.inv.failed == {2}                    # two clean polls -> back in the inventory
+    assert [e[1] for e in sup.events].count("gpu_recover") == 2
+    # hang watchdog
+    killed.clear()
+    assert mon.check_workers(now=100.0) == []
+    healthy["ok"] = False
+    assert mon.check_workers(now=110.0) == []
+    assert mon.check_workers(now=140.5) == ["w1"] and killed == ["w1"]
+    assert GPUHealthMonitor(sup, probe=lambda: None).check_devices() == {}   # no library: no verdicts

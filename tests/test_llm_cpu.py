@@ -89,3 +89,26 @@ def test_sampling():
     t = torch.tensor([0.0, 1.0, 0.7])
     out = sample(logits, t, torch.tensor([50, 1, 0]), torch.tensor([0.9, 0.9, 1.0]))
     assert out.tolist()[0] == 42 and out.tolist()[1] == 42
+
+
+def test_chunked_prefill_matches_and_interleaves():
+    """A 300-token prompt prefilled in 64-token chunks gives the same greedy tokens as one-shot prefill,
+    and a sequence already decoding keeps producing tokens between the chunks."""
+    c = LlamaConfig.tiny()
+    p = SamplingParams(max_tokens=5, temperature=0.0, ignore_eos=True)
+    long = [(7 * i) % 500 + 3 for i in range(300)]
+    ref = LLMEngine(c, device="cpu", max_num_seqs=4, max_model_len=512, enable_prefix_caching=False)
+    want = ref.generate([long], p)[0].output
+    eng = LLMEngine(c, device="cpu", max_num_seqs=4, max_model_len=512, enable_prefix_caching=False,
+                    prefill_chunk=64)
+    short = eng.add_request([5, 6, 7], SamplingParams(max_tokens=40, temperature=0.0, ignore_eos=True))
+    eng.step()                      # short prompt prefilled
+    s = eng.add_request(long, p)
+    lens = []
+    while not s.finished:
+        eng.step()
+        lens.append(len(short.output))
+    assert s.output == want
+    # decode of the short sequence advanced while the long prompt was still being prefilled
+    assert lens[4] > lens[0]
+    assert eng.stats["prefill_tokens"] >= 300

@@ -105,10 +105,16 @@ def test_vision_tower_matches_transformers():
     assert err < 3e-2, float(err)
 
 
-@pytest.mark.parametrize("prompt", [[1, 512, 17, 99, 250, 7], [1, 33, 44, 512, 17, 99, 250, 7, 8]])
-def test_image_generation_matches_transformers(prompt):
+LONG = [1] + [(13 * i) % 400 + 20 for i in range(70)] + [512] + [(5 * i) % 400 + 20 for i in range(80)]
+
+
+@pytest.mark.parametrize("prompt,chunk", [([1, 512, 17, 99, 250, 7], None),
+                                          ([1, 33, 44, 512, 17, 99, 250, 7, 8], None),
+                                          (LONG, 64)])    # chunked prefill; <|image|> in the 2nd chunk
+def test_image_generation_matches_transformers(prompt, chunk):
     c, hf = _hf_tiny()
     eng = _engine(c, hf)
+    eng.prefill_chunk = chunk or eng.prefill_chunk
     pre = preprocess_image(_image(), c.vision)
     inp = _hf_inputs(c, pre, prompt)
     with torch.no_grad():
