@@ -51,7 +51,7 @@ std::string gemm_key(const shai::GemmArgs& g) {
   char buf[256];
   snprintf(buf, sizeof(buf), "%d:%d,%d,%d,b%d,g%d|%d,%d,%d,%d,%d,%d,%d,%d,%d", g.conv, g.M, g.N, g.K, g.batch, g.glu,
            g.Nimg, g.H, g.Wd, g.Cin, g.Cin1, g.KH, g.stride, g.upsample, g.A2 != nullptr);
-  return buf;
+  return g.rms ? std::string(buf) + "|rms" : std::string(buf);
 }
 
 bool autotune_enabled() {
@@ -71,7 +71,8 @@ int max_splits_for(const shai::GemmArgs& g) {
   return s;
 }
 
-constexpr int kSkinnyCfg = 1000;  // Choice.cfg of the skinny streaming kernel (csrc/kernels/gemv.hip)
+// Choice.cfg of the skinny streaming kernel (csrc/kernels/gemv.hip); Choice.splits = its K-group count
+constexpr int kSkinnyCfg = 1000;
 
 bool stream_capturing() {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -79,20 +80,20 @@ bool stream_capturing() {
   return cs != hipStreamCaptureStatusNone;
 }
 
-void launch_skinny_choice(const shai::GemmArgs& g, const Tensor& like) {
+void launch_skinny_choice(const shai::GemmArgs& g, const Tensor& like, int kg) {
   Tensor ws;
   float* wsp = nullptr;
-  const size_t bytes = shai::skinny_workspace_bytes(g);
+  const size_t bytes = shai::skinny_workspace_bytes_kg(g, kg);
   if (bytes > 0) {
     ws = at::empty({(long)(bytes / sizeof(float))}, like.options().dtype(at::kFloat));
     wsp = ws.data_ptr<float>();
   }
-  shai::launch_skinny(g, wsp, stream());
+  shai::launch_skinny_kg(g, wsp, kg, stream());
 }
 
 void launch_choice(const shai::GemmArgs& g, const Tensor& like, Choice c) {
   if (c.cfg == kSkinnyCfg) {
-    launch_skinny_choice(g, like);
+    launch_skinny_choice(g, like, c.splits);
     return;
   }
   Tensor ws;
@@ -106,8 +107,9 @@ void launch_choice(const shai::GemmArgs& g, const Tensor& like, Choice c) {
 
 // Candidates are timed into a scratch output so that in-place epilogues (C aliasing
 // the residual, e.g. x = x + gate * f(x)) are applied exactly once, by the caller's
-// final launch.
-Choice tune(const shai::GemmArgs& g_real, const Tensor& like) {
+// final launch.  skinny_only: the problem has an epilogue only the skinny kernel implements
+// (folded RMSNorm), so only its K-group counts are candidates.
+Choice tune(const shai::GemmArgs& g_real, const Tensor& like, bool skinny_only = false) {
   shai::GemmArgs g = g_real;
   const long n_out = g.glu ? g.N / 2 : g.N;
   const int nb = g.batch > 0 ? g.batch : 1;
@@ -115,15 +117,18 @@ Choice tune(const shai::GemmArgs& g_real, const Tensor& like) {
   g.C = reinterpret_cast<shai::bf16_t*>(scratch.data_ptr());
   g.ldc = n_out;
   g.batch_c = (long)g.M * n_out;
-  Choice def;
-  shai::gemm2_plan(g, &def.cfg, &def.splits);
-  const int ms = max_splits_for(g);
+  Choice def{kSkinnyCfg, shai::skinny_kgroups(g)};
   std::vector<Choice> cands;
-  for (int c = 0; c < shai::gemm2_num_cfgs(); ++c) {
-    if (!shai::gemm2_cfg_supported(g, c)) continue;
-    for (int s = 1; s <= ms; s *= 2) cands.push_back({c, s});
+  if (!skinny_only) {
+    shai::gemm2_plan(g, &def.cfg, &def.splits);
+    const int ms = max_splits_for(g);
+    for (int c = 0; c < shai::gemm2_num_cfgs(); ++c) {
+      if (!shai::gemm2_cfg_supported(g, c)) continue;
+      for (int s = 1; s <= ms; s *= 2) cands.push_back({c, s});
+    }
   }
-  if (shai::skinny_supported(g)) cands.push_back({kSkinnyCfg, 1});
+  if (shai::skinny_supported(g))
+    for (int kg = 1; kg <= shai::skinny_max_kgroups(g); kg *= 2) cands.push_back({kSkinnyCfg, kg});
   hipStream_t st = stream();
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
@@ -146,6 +151,27 @@ Choice tune(const shai::GemmArgs& g_real, const Tensor& like) {
   hipEventDestroy(e0);
   hipEventDestroy(e1);
   return best;
+}
+
+// Skinny-kernel-only problems (folded RMSNorm epilogue): tuned over the K-group count.
+void run_skinny(const shai::GemmArgs& g, const Tensor& like) {
+  const std::string key = gemm_key(g);
+  Choice c{-1, 1};
+  {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    auto it = g_tuned.find(key);
+    if (it != g_tuned.end() && it->second.cfg == kSkinnyCfg) c = it->second;
+  }
+  if (c.cfg < 0) {
+    if (!stream_capturing() && autotune_enabled()) {
+      c = tune(g, like, true);
+      std::lock_guard<std::mutex> lk(g_tune_mu);
+      g_tuned[key] = c;
+    } else {
+      c = Choice{kSkinnyCfg, shai::skinny_kgroups(g)};
+    }
+  }
+  launch_choice(g, like, c);
 }
 
 void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_bytes, long a2_bytes) {
@@ -178,7 +204,7 @@ void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_
       g_tuned[key] = c;
     } else {
       if (shai::skinny_supported(g)) {
-        c = Choice{kSkinnyCfg, 1};
+        c = Choice{kSkinnyCfg, shai::skinny_kgroups(g)};
       } else {
         shai::gemm2_plan(g, &c.cfg, &c.splits);
         if (!shai::gemm2_cfg_supported(g, c.cfg)) c = Choice{shai::gemm2_num_cfgs() - 1, 1};
@@ -193,7 +219,7 @@ std::vector<std::string> gemm_tuning_table() {
   std::vector<std::string> out;
   for (auto& kv : g_tuned) {
     if (kv.second.cfg == kSkinnyCfg) {
-      out.push_back(kv.first + " -> skinny");
+      out.push_back(kv.first + " -> skinny kg=" + std::to_string(kv.second.splits));
       continue;
     }
     int bm, bn;
@@ -436,14 +462,19 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
   g.act = act;
   g.glu = glu;
   const long a_bytes = (batched ? (long)a.size(0) * a.stride(0) : (long)g.M * g.lda) * 2;
+  // tests / tools bypass the tuner: force_cfg = gemm2 config, 1000 = skinny kernel (heuristic K groups),
+  // 1000 + kg = skinny kernel with kg K groups
+  const bool force_skinny = force_cfg >= kSkinnyCfg;
+  const int force_kg = force_cfg > kSkinnyCfg ? (int)(force_cfg - kSkinnyCfg) : shai::skinny_kgroups(g);
   if (rms_eps >= 0) {
     // RMSNorm(a) folded in (norm gain pre-multiplied into w): fused into the skinny kernel for
     // decode-shaped problems, otherwise an explicit unweighted RMSNorm pass feeds the GEMM.
     SHAI_CHECK(!batched, "folded RMSNorm needs a 2D activation");
-    if (shai::skinny_supported(g) && force_cfg < 0) {
+    if (shai::skinny_supported(g) && (force_cfg < 0 || force_skinny)) {
       g.rms = 1;
       g.rms_eps = (float)rms_eps;
-      launch_choice(g, a, Choice{kSkinnyCfg, 1});
+      if (force_skinny) launch_choice(g, a, Choice{kSkinnyCfg, force_kg});
+      else run_skinny(g, a);
       return;
     }
     Tensor xn = at::empty({g.M, g.K}, a.options());
@@ -462,13 +493,15 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
     run_gemm(g, xn, (long)g.M * g.K * 2, (long)g.N * g.ldw * 2, 0);
     return;
   }
-  if (force_cfg >= 0) {  // tests / tools: bypass the tuner (1000 = skinny kernel)
-    if (force_cfg == kSkinnyCfg) {
-      SHAI_CHECK(shai::skinny_supported(g), "skinny kernel does not support this problem");
+  if (force_cfg >= 0) {
+    if (force_skinny) {
+      SHAI_CHECK(shai::skinny_supported(g) && force_kg >= 1 && force_kg <= 64,
+                 "skinny kernel does not support this problem");
+      launch_choice(g, a, Choice{kSkinnyCfg, force_kg});
     } else {
       SHAI_CHECK(force_cfg < shai::gemm2_num_cfgs() && shai::gemm2_cfg_supported(g, force_cfg), "bad force_cfg");
+      launch_choice(g, a, Choice{(int)force_cfg, 1});
     }
-    launch_choice(g, a, Choice{(int)force_cfg, 1});
     return;
   }
   run_gemm(g, a, a_bytes, (long)g.N * g.ldw * 2, 0);

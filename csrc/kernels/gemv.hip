@@ -1,4 +1,4 @@
-// Skinny GEMM for decode-shaped problems (M <= 32 activation rows: LLM decode
+// Skinny GEMM for decode-shaped problems (M <= 64 activation rows: LLM decode
 // batches, per-request modulation GEMMs):
 //
 //   C[m, n] = act(alpha * sum_k X[m, k] * W[n, k] + bias[n]) (+ res_alpha * R[m, n]),  GLU optional
@@ -7,19 +7,23 @@
 // in flight per CU to cover HBM latency" (Little's law: ~8 TB/s x ~2 us over 256
 // CUs is ~64 KB per CU), with every global load fully coalesced:
 //
-// * Workgroup = 4 waves, tile = 64 W rows (n) x all M <= 32 rows of X, walking
-//   its K range in 64-wide steps.  Each step's W tile (8 KB) and X tile (4 KB)
-//   move global -> LDS with buffer_load ... lds DMA (8 full 128 B rows per wave
-//   instruction; range check = zero fill for X rows >= M / W rows >= N), through
-//   a SK_STAGES-deep ring (6 x 12 KB), so 5 steps are always in flight while one
-//   is consumed.  Counted vmcnt + one s_barrier per step (same protocol as the
-//   3-stage GEMM in gemm_lds.hip, generalised to S stages).
-// * Wave w consumes the 16-wide K slice [16w, 16w + 16) of each step: two
-//   32x32x16 MFMAs (W rows 0-31 and 32-63 as A, X^T as B).  XOR-swizzled LDS
-//   image (source-side swizzle, conflict-free ds_read_b128).
-// * Cross-wave reduction through LDS, fused epilogue.  When N/64 tiles cannot
-//   fill the chip, K is additionally split over KG workgroups writing fp32
-//   partials that the shared split-K fold (gemm_lds.hip) reduces + epilogues.
+// * Workgroup = 4 waves, tile = 64 W rows (n) x all M rows of X (one 32-row
+//   group for M <= 32, two for M <= 64), walking its K range in 64-wide steps.
+//   Each step's W tile (8 KB) and X tile (4 / 8 KB) move global -> LDS with
+//   buffer_load ... lds DMA (8 full 128 B rows per wave instruction; range
+//   check = zero fill for X rows >= M / W rows >= N), through a ring of
+//   6 x 12 KB (MB = 32) or 4 x 16 KB (MB = 64, two workgroups per CU), so
+//   several steps are always in flight while one is consumed.  Counted vmcnt +
+//   one s_barrier per step (same protocol as the GEMM in gemm_lds.hip).
+// * Wave w consumes the 16-wide K slice [16w, 16w + 16) of each step: 32x32x16
+//   MFMAs with W rows 0-31 / 32-63 as A and each 32-row X group (transposed) as
+//   B, so one W fragment feeds both X groups -- at M = 64 the weights are still
+//   streamed exactly once.  XOR-swizzled LDS image (source-side swizzle,
+//   conflict-free ds_read_b128).
+// * Cross-wave reduction through LDS, fused epilogue (bias / act / GLU /
+//   residual / folded RMSNorm).  When N/64 tiles cannot fill the chip, K is
+//   additionally split over KG workgroups writing fp32 partials that the shared
+//   split-K fold (gemm_lds.hip) reduces + epilogues.
 #include "common.h"
 #include "launchers.h"
 
@@ -31,10 +35,19 @@ typedef __attribute__((address_space(3))) void sk_lds_void;
 constexpr int SK_BN = 64;       // W rows per workgroup
 constexpr int SK_BK = 64;       // K per step
 constexpr int SK_WAVES = 4;
-constexpr int SK_STAGES = 6;
-constexpr int SK_STAGE_ELEMS = (SK_BN + 32) * SK_BK;   // W tile then X tile
-constexpr int SK_PER = 3;       // DMA instructions per wave per step (2 for W, 1 for X)
 constexpr uint32_t SK_OOB = 0x80000000u;
+
+template <int MB>
+struct SkGeom {
+  static constexpr int XG = MB / 32;                    // 32-row X groups
+  static constexpr int STAGES = MB == 32 ? 6 : 4;
+  static constexpr int STAGE_ELEMS = (SK_BN + MB) * SK_BK;  // W tile then X tile
+  static constexpr int PER = 2 + XG;                    // DMA instructions per wave per step
+  static constexpr int RP = MB + 1;                     // padded row of the reduction image
+  static constexpr size_t LDS = (size_t)STAGES * STAGE_ELEMS * 2 > (size_t)SK_WAVES * SK_BN * RP * 4
+                                    ? (size_t)STAGES * STAGE_ELEMS * 2
+                                    : (size_t)SK_WAVES * SK_BN * RP * 4;
+};
 
 __device__ __forceinline__ int sk_swz(int row, int ch) { return row * SK_BK + ((ch ^ ((row >> 1) & 7)) << 3); }
 
@@ -42,14 +55,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t sk_rsrc(const void* base, uint
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-template <int N>
+template <int PER, int N>
 __device__ __forceinline__ void sk_wait_upto(int pending) {
-  // s_waitcnt needs an immediate: allow `pending` DMA groups (of SK_PER loads) to stay in flight
+  // s_waitcnt needs an immediate: allow `pending` DMA groups (of PER loads) to stay in flight
   if constexpr (N == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
-    if (pending >= N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N * SK_PER) : "memory");
-    else sk_wait_upto<N - 1>(pending);
+    if (pending >= N) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N * PER) : "memory");
+    else sk_wait_upto<PER, N - 1>(pending);
   }
 }
 
@@ -70,21 +83,21 @@ __device__ __forceinline__ void sk_store(const GemmArgs& p, int n, int m, float 
   }
 }
 
-// Epilogue over a reduced 64 (n) x 32 (m) tile held as get(nl, m).
-template <bool GLU, int ACT, typename Get>
+// Epilogue over a reduced 64 (n) x MB (m) tile held as get(nl, m).
+template <int MB, bool GLU, int ACT, typename Get>
 __device__ __forceinline__ void sk_epilogue(const GemmArgs& p, int n0, Get get) {
   const int tid = threadIdx.x;
   if constexpr (GLU) {
-    // 32 pairs x 32 m = 1024 outputs, 4 per thread; consecutive threads -> consecutive pairs
+    // 32 pairs x MB m, consecutive threads -> consecutive pairs
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
+    for (int it = 0; it < 32 * MB / 256; ++it) {
       const int idx = tid + it * 256;
       const int m = idx >> 5, pr = idx & 31;
       if (m < p.M) sk_store<GLU, ACT>(p, n0 + 2 * pr, m, get(2 * pr, m), get(2 * pr + 1, m));
     }
   } else {
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
+    for (int it = 0; it < 64 * MB / 256; ++it) {
       const int idx = tid + it * 256;
       const int m = idx >> 6, nl = idx & 63;
       if (m < p.M) sk_store<GLU, ACT>(p, n0 + nl, m, get(nl, m), 0.f);
@@ -92,12 +105,14 @@ __device__ __forceinline__ void sk_epilogue(const GemmArgs& p, int n0, Get get) 
   }
 }
 
-template <bool GLU, int ACT, bool RMS>
+template <int MB, bool GLU, int ACT, bool RMS>
 __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmArgs p, float* __restrict__ ws,
                                                                     int kg_steps) {
+  using G = SkGeom<MB>;
+  constexpr int XG = G::XG;
   extern __shared__ __attribute__((aligned(16))) bf16_t sk_smem[];
-  __shared__ float ss_red[SK_WAVES][64];
-  __shared__ float rstd_s[32];
+  __shared__ float ss_red[SK_WAVES][64 * XG];
+  __shared__ float rstd_s[MB];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tile = blockIdx.x, kg = blockIdx.y, KG = gridDim.y;
@@ -119,11 +134,11 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
     wr[j] = (w * 2 + j) * 8 + lrow;
     wc[j] = lpos ^ ((wr[j] >> 1) & 7);
   }
-  const int xr = w * 8 + lrow;
-  const int xc = lpos ^ ((xr >> 1) & 7);
+  const int xr = w * 8 + lrow;                 // X rows xr (+ 32 for the second group)
+  const int xc = lpos ^ ((xr >> 1) & 7);       // (xr + 32) has the same swizzle
 
   auto stage = [&](int buf, int step) {
-    bf16_t* sw = sk_smem + buf * SK_STAGE_ELEMS;
+    bf16_t* sw = sk_smem + buf * G::STAGE_ELEMS;
     bf16_t* sx = sw + SK_BN * SK_BK;
     const int k0 = (t0 + step) * SK_BK;
 #pragma unroll
@@ -132,64 +147,87 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
       const uint32_t off = (n < p.N && k < p.K) ? (uint32_t)(((long)n * p.ldw + k) * 2) : SK_OOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (sk_lds_void*)(sw + (w * 2 + j) * 8 * SK_BK), 16, off, 0, 0, 0);
     }
-    const int k = k0 + xc * 8;
-    const uint32_t off = (xr < p.M && k < p.K) ? (uint32_t)(((long)xr * p.lda + k) * 2) : SK_OOB;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (sk_lds_void*)(sx + w * 8 * SK_BK), 16, off, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < XG; ++j) {
+      const int r = xr + 32 * j, k = k0 + xc * 8;
+      const uint32_t off = (r < p.M && k < p.K) ? (uint32_t)(((long)r * p.lda + k) * 2) : SK_OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (sk_lds_void*)(sx + (32 * j + w * 8) * SK_BK), 16, off, 0, 0,
+                                               0);
+    }
   };
 
-  float16_ acc0 = {}, acc1 = {};
-  float ss = 0.f;  // folded RMSNorm: this lane's share of sum_k X[m, k]^2 (the 4 waves x 2 halves
-                   // together read every X element of every step exactly once)
+  float16_ acc[2][XG];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < XG; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[h][j][i] = 0.f;
+  float ss[XG];  // folded RMSNorm: this lane's share of sum_k X[m, k]^2 (the 4 waves x 2 halves together
+                 // read every X element of every step exactly once)
+#pragma unroll
+  for (int j = 0; j < XG; ++j) ss[j] = 0.f;
   const int fr = lane & 31, fh = lane >> 5;
   const int ch = 2 * w + fh;  // this lane's 8-element chunk of the step's K range
 #pragma unroll
-  for (int i = 0; i < SK_STAGES - 1; ++i)
+  for (int i = 0; i < G::STAGES - 1; ++i)
     if (i < nk) stage(i, i);
   int buf = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    sk_wait_upto<SK_STAGES - 2>(min(SK_STAGES - 2, nk - 1 - kt));
+    sk_wait_upto<G::PER, G::STAGES - 2>(min(G::STAGES - 2, nk - 1 - kt));
     __builtin_amdgcn_s_barrier();
-    if (kt + SK_STAGES - 1 < nk) {
-      const int nb = buf == 0 ? SK_STAGES - 1 : buf - 1;  // buffer of step kt-1: every wave is past it
-      stage(nb, kt + SK_STAGES - 1);
+    if (kt + G::STAGES - 1 < nk) {
+      const int nb = buf == 0 ? G::STAGES - 1 : buf - 1;  // buffer of step kt-1: every wave is past it
+      stage(nb, kt + G::STAGES - 1);
     }
-    const bf16_t* sw = sk_smem + buf * SK_STAGE_ELEMS;
+    const bf16_t* sw = sk_smem + buf * G::STAGE_ELEMS;
     const bf16_t* sx = sw + SK_BN * SK_BK;
-    const bf16x8s xf = *reinterpret_cast<const bf16x8s*>(sx + sk_swz(fr, ch));
     const bf16x8s w0 = *reinterpret_cast<const bf16x8s*>(sw + sk_swz(fr, ch));
     const bf16x8s w1 = *reinterpret_cast<const bf16x8s*>(sw + sk_swz(32 + fr, ch));
-    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, xf, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, xf, acc1, 0, 0, 0);
-    if constexpr (RMS) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float f = (float)xf[e];
-        ss += f * f;
+    for (int j = 0; j < XG; ++j) {
+      const bf16x8s xf = *reinterpret_cast<const bf16x8s*>(sx + sk_swz(32 * j + fr, ch));
+      acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, xf, acc[0][j], 0, 0, 0);
+      acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, xf, acc[1][j], 0, 0, 0);
+      if constexpr (RMS) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = (float)xf[e];
+          ss[j] += f * f;
+        }
       }
     }
-    buf = buf == SK_STAGES - 1 ? 0 : buf + 1;
+    buf = buf == G::STAGES - 1 ? 0 : buf + 1;
   }
-  if constexpr (RMS) ss_red[w][lane] = ss;
+  if constexpr (RMS) {
+#pragma unroll
+    for (int j = 0; j < XG; ++j) ss_red[w][64 * j + lane] = ss[j];
+  }
 
   // ---- cross-wave reduction: red[w][nl][m] (padded), reusing the stage ring
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   float* red = reinterpret_cast<float*>(sk_smem);
-  constexpr int RP = 33;
+  constexpr int RP = G::RP;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int nl = (i & 3) + 8 * (i >> 2) + 4 * fh;
-    red[(w * SK_BN + nl) * RP + fr] = acc0[i];
-    red[(w * SK_BN + 32 + nl) * RP + fr] = acc1[i];
+#pragma unroll
+    for (int j = 0; j < XG; ++j) {
+      red[(w * SK_BN + nl) * RP + 32 * j + fr] = acc[0][j][i];
+      red[(w * SK_BN + 32 + nl) * RP + 32 * j + fr] = acc[1][j][i];
+    }
   }
   __syncthreads();
   auto row_ss = [&](int m) {
+    const int j = m >> 5, r = m & 31;
     float t = 0.f;
 #pragma unroll
-    for (int q = 0; q < SK_WAVES; ++q) t += ss_red[q][m] + ss_red[q][m + 32];
+    for (int q = 0; q < SK_WAVES; ++q) t += ss_red[q][64 * j + r] + ss_red[q][64 * j + 32 + r];
     return t;
   };
   if constexpr (RMS) {
-    if (KG == 1 && tid < 32) rstd_s[tid] = rsqrtf(row_ss(tid) / p.K + p.rms_eps);
+    if (KG == 1 && tid < MB) rstd_s[tid] = rsqrtf(row_ss(tid) / p.K + p.rms_eps);
     __syncthreads();
   }
   auto wsum = [&](int nl, int m) {
@@ -202,7 +240,7 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
     return v;
   };
   if (KG == 1) {
-    sk_epilogue<GLU, ACT>(p, n0, wsum);
+    sk_epilogue<MB, GLU, ACT>(p, n0, wsum);
     return;
   }
   if constexpr (RMS) {  // row sum-of-squares partials for the fold (one tile per K group writes them)
@@ -213,7 +251,7 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
   // L2 writeback on this chip, and measured ~5x slower than the separate fold.)
   float* part = ws + (long)kg * p.M * p.N;
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {
+  for (int it = 0; it < 64 * MB / 256; ++it) {
     const int idx = tid + it * 256;
     const int m = idx >> 6, nl = idx & 63;
     if (m < p.M && n0 + nl < p.N) part[(long)m * p.N + n0 + nl] = wsum(nl, m);
@@ -222,34 +260,43 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
 
 // ---------------------------------------------------------------------------- host side
 bool skinny_supported(const GemmArgs& a) {
-  return !a.conv && (a.batch <= 1) && a.M >= 1 && a.M <= 32 && a.K % 8 == 0 && a.N % 2 == 0 &&
+  return !a.conv && (a.batch <= 1) && a.M >= 1 && a.M <= 64 && a.K % 8 == 0 && a.N % 2 == 0 &&
          a.bias2d == nullptr && a.gate == nullptr && a.in_scale == nullptr && (a.lda % 8) == 0 &&
          (a.ldw % 8) == 0 && (long)a.N * a.ldw * 2 < 0x7fffffffL;
 }
 
 // K groups: enough workgroups for ~2 per CU, each group >= 2 pipeline depths of K steps.
 int skinny_kgroups(const GemmArgs& a) {
+  const int stages = a.M <= 32 ? SkGeom<32>::STAGES : SkGeom<64>::STAGES;
   const int tiles = (a.N + SK_BN - 1) / SK_BN, ksteps = (a.K + SK_BK - 1) / SK_BK;
   int kg = 1;
-  while (tiles * kg < 512 && ksteps / (kg * 2) >= SK_STAGES) kg *= 2;
+  while (tiles * kg < 512 && ksteps / (kg * 2) >= stages) kg *= 2;
   return kg;
 }
 
-size_t skinny_workspace_bytes(const GemmArgs& a) {
-  const int kg = skinny_kgroups(a);
+size_t skinny_workspace_bytes_kg(const GemmArgs& a, int kg) {
   return kg > 1 ? ((size_t)kg * a.M * a.N + (a.rms ? (size_t)kg * a.M : 0)) * sizeof(float) : 0;
 }
 
-void launch_skinny(const GemmArgs& a, float* ws, hipStream_t s) {
-  const int kg = ws != nullptr ? skinny_kgroups(a) : 1;
+size_t skinny_workspace_bytes(const GemmArgs& a) { return skinny_workspace_bytes_kg(a, skinny_kgroups(a)); }
+
+int skinny_max_kgroups(const GemmArgs& a) {
+  const int ksteps = (a.K + SK_BK - 1) / SK_BK;
+  int kg = 1;
+  while (kg < 16 && ksteps / (kg * 2) >= 2) kg *= 2;
+  return kg;
+}
+
+template <int MB>
+static void launch_skinny_mb(const GemmArgs& a, float* ws, int kg, hipStream_t s) {
   const int ksteps = (a.K + SK_BK - 1) / SK_BK;
   const int kg_steps = (ksteps + kg - 1) / kg;
   dim3 grid((a.N + SK_BN - 1) / SK_BN, kg), block(SK_WAVES * 64);
-  const size_t lds = (size_t)SK_STAGES * SK_STAGE_ELEMS * sizeof(bf16_t);
-#define SK(G, A)                                                               \
-  do {                                                                         \
-    if (a.rms) skinny_gemm_kernel<G, A, true><<<grid, block, lds, s>>>(a, ws, kg_steps);  \
-    else skinny_gemm_kernel<G, A, false><<<grid, block, lds, s>>>(a, ws, kg_steps);       \
+  const size_t lds = SkGeom<MB>::LDS;
+#define SK(G, A)                                                                         \
+  do {                                                                                   \
+    if (a.rms) skinny_gemm_kernel<MB, G, A, true><<<grid, block, lds, s>>>(a, ws, kg_steps);  \
+    else skinny_gemm_kernel<MB, G, A, false><<<grid, block, lds, s>>>(a, ws, kg_steps);       \
   } while (0)
 #define SK_ACT(G)                                      \
   switch (a.act) {                                     \
@@ -267,7 +314,20 @@ void launch_skinny(const GemmArgs& a, float* ws, hipStream_t s) {
   }
 #undef SK_ACT
 #undef SK
+}
+
+// kg K groups (split-K over workgroups; needs ws of skinny_workspace_bytes_kg, else kg = 1)
+void launch_skinny_kg(const GemmArgs& a, float* ws, int kg, hipStream_t s) {
+  const int ksteps = (a.K + SK_BK - 1) / SK_BK;
+  if (ws == nullptr || kg < 1) kg = 1;
+  if (kg > ksteps) kg = ksteps;
+  if (a.M <= 32) launch_skinny_mb<32>(a, ws, kg, s);
+  else launch_skinny_mb<64>(a, ws, kg, s);
   if (kg > 1) launch_splitk_epilogue(a, ws, kg, s);
+}
+
+void launch_skinny(const GemmArgs& a, float* ws, hipStream_t s) {
+  launch_skinny_kg(a, ws, ws != nullptr ? skinny_kgroups(a) : 1, s);
 }
 
 }  // namespace shai

@@ -122,11 +122,14 @@ bool gemm2_cfg_supported(const GemmArgs& a, int cfg);
 bool gemm3_supported(const GemmArgs& a);
 void launch_gemm3(const GemmArgs& a, float* ws, int splits, int stages, hipStream_t s);
 void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipStream_t s);
-// skinny (decode-shaped, M <= 32) streaming GEMM; ws: skinny_workspace_bytes (fp32 split-K partials)
+// skinny (decode-shaped, M <= 64) streaming GEMM; ws: skinny_workspace_bytes (fp32 split-K partials)
 bool skinny_supported(const GemmArgs& a);
-int skinny_kgroups(const GemmArgs& a);
+int skinny_kgroups(const GemmArgs& a);        // heuristic K-group count
+int skinny_max_kgroups(const GemmArgs& a);    // largest K-group count worth trying (autotuner)
 size_t skinny_workspace_bytes(const GemmArgs& a);
+size_t skinny_workspace_bytes_kg(const GemmArgs& a, int kg);
 void launch_skinny(const GemmArgs& a, float* ws, hipStream_t s);
+void launch_skinny_kg(const GemmArgs& a, float* ws, int kg, hipStream_t s);
 void gemm2_cfg_info(int cfg, int* bm, int* bn);
 
 // ---------------------------------------------------------------- attention

@@ -1,4 +1,4 @@
-"""Skinny (decode-shaped, M <= 32) streaming GEMM kernel vs fp32 PyTorch."""
+"""Skinny (decode-shaped, M <= 64) streaming GEMM kernel vs fp32 PyTorch."""
 import pytest
 import torch
 
@@ -14,7 +14,8 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (7, 6144, 4096), (32, 4096, 14336), (32, 28672, 4096),
-                                   (16, 1024, 512), (32, 32768, 4096), (3, 96, 64)])
+                                   (16, 1024, 512), (32, 32768, 4096), (3, 96, 64), (33, 4096, 4096),
+                                   (48, 6144, 4096), (64, 28672, 4096), (64, 4096, 14336), (64, 96, 64)])
 def test_skinny_plain(cuda, M, N, K):
     torch.manual_seed(M + N)
     x = torch.randn(M, K, device=cuda).bfloat16()
@@ -27,9 +28,9 @@ def test_skinny_plain(cuda, M, N, K):
     assert _rel(out, want) < 1e-2
 
 
-@pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
-def test_skinny_glu_and_act(cuda, act):
-    M, N, K = 32, 2 * 2048, 4096
+@pytest.mark.parametrize("act,M", [("silu", 32), ("gelu_tanh", 32), ("silu", 64), ("gelu_tanh", 40)])
+def test_skinny_glu_and_act(cuda, act, M):
+    N, K = 2 * 2048, 4096
     x = torch.randn(M, K, device=cuda).bfloat16()
     w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
     out = torch.empty(M, N // 2, device=cuda, dtype=torch.bfloat16)
@@ -42,9 +43,26 @@ def test_skinny_glu_and_act(cuda, act):
     assert _rel(out2, f(y)) < 1e-2
 
 
+@pytest.mark.parametrize("kg", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("M,N,K,rms", [(32, 4096, 4096, False), (64, 4096, 14336, False), (17, 6144, 4096, True),
+                                       (64, 28672, 4096, True)])
+def test_skinny_k_groups(cuda, kg, M, N, K, rms):
+    """Every K-group count the tuner may pick (force_cfg = 1000 + kg), incl. the folded-RMSNorm epilogue."""
+    torch.manual_seed(kg + M)
+    x = (torch.randn(M, K, device=cuda) * 2).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16()
+    out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    ops.gemm_into(x, w, out, b, force_cfg=SKINNY + kg, rms_eps=1e-5 if rms else -1.0)
+    xf = x.float()
+    if rms:
+        xf = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)
+    assert _rel(out, xf @ w.float().t() + b.float()) < 1e-2
+
+
 def test_skinny_graph_replay_rearms_tickets(cuda):
     """Split-K fixup tickets must re-arm so graph replays stay correct."""
-    M, N, K = 8, 1024, 8192   # few tiles, long K -> several K groups
+    M, N, K = 48, 1024, 8192   # few tiles, long K -> several K groups (two 32-row X groups)
     x = torch.randn(M, K, device=cuda).bfloat16()
     w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
     out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
@@ -66,16 +84,18 @@ def test_skinny_graph_replay_rearms_tickets(cuda):
 
 def test_autotuned_decode_shapes(cuda):
     """The tuner may pick skinny or a tile config; either way results are right."""
-    for M, N, K in [(32, 6144, 4096), (32, 4096, 4096), (32, 28672, 4096), (32, 4096, 14336)]:
+    for M, N, K in [(32, 6144, 4096), (32, 4096, 4096), (32, 28672, 4096), (32, 4096, 14336), (64, 6144, 4096),
+                    (64, 4096, 14336)]:
         x = torch.randn(M, K, device=cuda).bfloat16()
         w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
         y = ops.linear(x, w)
         assert _rel(y, x.float() @ w.float().t()) < 1e-2
 
 
-@pytest.mark.parametrize("M,N,K", [(32, 6144, 4096), (5, 4096, 4096), (32, 28672, 4096), (64, 512, 1024)])
+@pytest.mark.parametrize("M,N,K", [(32, 6144, 4096), (5, 4096, 4096), (32, 28672, 4096), (64, 512, 1024),
+                                   (64, 6144, 4096), (48, 28672, 4096), (96, 512, 1024)])
 def test_folded_rmsnorm_linear(cuda, M, N, K):
-    """linear(x, W * diag(g), rms_eps) == rmsnorm(x, g) @ W^T (fused in the skinny kernel for M <= 32,
+    """linear(x, W * diag(g), rms_eps) == rmsnorm(x, g) @ W^T (fused in the skinny kernel for M <= 64,
     explicit unweighted norm + GEMM otherwise)."""
     from shai_amd.ops import reference as ref
     x = (torch.randn(M, K, device=cuda) * 3).bfloat16()
