@@ -99,6 +99,7 @@ void shai_bm_fork(void* h, const int* blocks, int n) {
   std::lock_guard<std::mutex> g(m->mu);
   for (int i = 0; i < n; ++i) {
     int b = blocks[i];
+    if (b < 0 || b >= m->num_blocks) continue;
     if (m->in_lru[b]) {
       m->lru.erase(m->lru_it[b]);
       m->in_lru[b] = 0;
@@ -130,6 +131,7 @@ void shai_bm_release(void* h, const int* blocks, int n) {
 void shai_bm_register(void* h, int block, uint64_t content_hash) {
   auto* m = static_cast<BlockManager*>(h);
   std::lock_guard<std::mutex> g(m->mu);
+  if (block < 0 || block >= m->num_blocks) return;
   if (m->cache.count(content_hash)) return;  // another block already caches it
   m->drop_hash(block);
   m->hash[block] = content_hash;
@@ -168,6 +170,10 @@ void shai_bm_stats(void* h, int64_t* out) {
   out[3] = (int64_t)m->lru.size();
 }
 
-int shai_bm_refcount(void* h, int block) { return static_cast<BlockManager*>(h)->refcnt[block]; }
+int shai_bm_refcount(void* h, int block) {
+  auto* m = static_cast<BlockManager*>(h);
+  std::lock_guard<std::mutex> g(m->mu);
+  return (block < 0 || block >= m->num_blocks) ? -1 : m->refcnt[block];
+}
 
 }  // extern "C"

@@ -28,6 +28,7 @@ from ..models.unet2d import UNet2DConditionModel, UNetConfig
 from ..models.vae import AutoencoderKLDecoder, VAEConfig
 from ..schedulers import DDIMScheduler
 from ..tokenizers import load_tokenizer
+from ..utils import profiling as prof
 from ..weights import materialize
 
 
@@ -128,8 +129,14 @@ class StableDiffusionEngine:
         W = width or self.cfg.width
         B = len(prompts)
         h, w = H // 8, W // 8
-        ctx = self.encode_prompts(prompts, negative_prompts)
-        ctx_kv = self.unet.context_kv(ctx)
+        with prof.profile_session("sd_generate"):
+            return self._generate(prompts, negative_prompts, num_inference_steps, guidance_scale, B, h, w, seed,
+                                  output)
+
+    def _generate(self, prompts, negative_prompts, num_inference_steps, guidance_scale, B, h, w, seed, output):
+        with prof.range_("text_encode"):
+            ctx = self.encode_prompts(prompts, negative_prompts)
+            ctx_kv = self.unet.context_kv(ctx)
         gen = torch.Generator(device=self.device)
         gen.manual_seed(int(seed) if seed is not None else int(time.time_ns() % (2 ** 31)))
         lat = torch.randn(B, h, w, self.cfg.unet.in_channels, generator=gen, device=self.device,
@@ -142,14 +149,16 @@ class StableDiffusionEngine:
             g.lat.copy_(lat)
             lat = g.lat
             for sp in steps:
-                out = g.run(sp.t)
+                with prof.range_("unet_step"):
+                    out = g.run(sp.t)
                 ops.sched_step(out, lat, True, guidance_scale, self.scheduler.pred_type, sp.a_t, sp.a_prev)
         else:
             for sp in steps:
                 t = torch.full((1,), sp.t, dtype=torch.float32, device=self.device)
                 out = self.unet(torch.cat([lat, lat], 0), t, ctx_kv)
                 ops.sched_step(out, lat, True, guidance_scale, self.scheduler.pred_type, sp.a_t, sp.a_prev)
-        img = self.vae(lat)
+        with prof.range_("vae_decode"):
+            img = self.vae(lat)
         if output == "tensor":
             return img
         return AutoencoderKLDecoder.to_uint8(img).cpu()

@@ -25,6 +25,7 @@ from typing import Dict, Optional, Sequence, Tuple
 
 import torch
 
+from ..utils import profiling as prof
 from .. import ops
 from ..models.clip import CLIPTextConfig, CLIPTextModel
 from ..models.flux import FluxConfig, FluxTransformer2DModel, pack_latents, unpack_latents_nhwc
@@ -153,7 +154,8 @@ class FluxEngine:
         h, w = H // 8, W // 8
         h2, w2 = h // 2, w // 2
         g_scale = c.guidance_scale if guidance_scale is None else guidance_scale
-        pooled, states = self.encode_prompts(prompts, max_sequence_length)
+        with prof.range_("flux_text_encode"):
+            pooled, states = self.encode_prompts(prompts, max_sequence_length)
         Nt = states.shape[1]
         tr = self.transformer
         ctx = tr.context_embedder(states)

@@ -31,6 +31,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 import torch
 
+from ..utils import profiling as prof
 from .. import ops
 from ..models.llama import (KV_BLOCK, Batch, LlamaConfig, LlamaForCausalLM, allocate_kv_cache, kv_bytes_per_block)
 from ..parallel.state import tp
@@ -459,10 +460,12 @@ class LLMEngine:
         # new prompts and remaining prefill chunks alternate with decode steps of the running batch
         if adm or (pending and (not decodable or self._last_step != "prefill")):
             self.running += adm
-            self._prefill(pending + adm)
+            with prof.range_("llm_prefill"):
+                self._prefill(pending + adm)
             self._last_step = "prefill"
         elif decodable:
-            self._decode(decodable)
+            with prof.range_("llm_decode"):
+                self._decode(decodable)
             self._last_step = "decode"
         done = [s for s in self.running if s.finished]
         for s in done:

@@ -8,14 +8,13 @@ ScaledObjects + capacity checker.
 import argparse
 import time
 
-import yaml
-
 from .autoscaler import Autoscaler, ScaleTarget, router_rate_metric
 from .controller.failover import FailoverController
 from .router import Router, create_app
 from .serving.common import run
 from .supervisor import GPUInventory, Supervisor, WorkerSpec
 from .supervisor.health import GPUHealthMonitor
+from .utils.config import load_node_config
 
 
 def spec_factory(dep: dict):
@@ -53,8 +52,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="config/node.yaml")
     a = ap.parse_args()
-    with open(a.config) as f:
-        cfg = yaml.safe_load(f)
+    cfg = load_node_config(a.config).as_dict()   # validated (utils/config.py), SHAI_NODE__* env overrides
     router, sup, scaler, fo = build(cfg)
     for name in list(sup.specs):
         sup.wait_ready(name)

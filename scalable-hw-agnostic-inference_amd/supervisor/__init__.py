@@ -23,6 +23,9 @@ import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
+from ..utils.logging import get_logger
+
+_log = get_logger("supervisor")
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
@@ -119,6 +122,7 @@ class Supervisor:
 
     def log(self, kind, detail):
         self.events.append((time.time(), kind, detail))
+        _log.info(kind, extra={"event": kind, "detail": str(detail)})
 
     # ------------------------------------------------------------------ lifecycle
     def _cmd(self, spec: WorkerSpec) -> List[str]:
@@ -142,6 +146,7 @@ class Supervisor:
             env["PORT"] = str(spec.port)
             env["HOST"] = "127.0.0.1"
             env.setdefault("POD_NAME", spec.name)
+            env.setdefault("SHAI_LOG_FORMAT", "json")   # one JSON object per line in <log_dir>/<name>.log
             env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
             if spec.gpus:
                 env["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in spec.gpus)
