@@ -356,18 +356,41 @@ void qk_norm_rope(const Tensor& x, const optional<Tensor>& q_w, const optional<T
                             stream());
 }
 
-void groupnorm_stats(const Tensor& x, const optional<Tensor>& gamma, const optional<Tensor>& beta,
-                     const Tensor& partials, const Tensor& scale, const Tensor& shift, int64_t G, double eps) {
+// x [N, HW, C1] (+ x2 [N, HW, C - C1]: channels of a virtual concat); counters: optional zeroed int32 [>= N]
+// tickets -> finalize fused into the stats launch.
+static void gn_sources(const Tensor& x, const optional<Tensor>& x2, shai::GroupNormArgs& a, int* C) {
   check_bf16(x, "x");
   SHAI_CHECK(x.is_contiguous() && x.dim() == 3, "groupnorm x must be contiguous [N, HW, C]");
+  *C = x.size(2);
+  a.C1 = x.size(2);
+  if (x2.has_value()) {
+    check_bf16(*x2, "x2");
+    SHAI_CHECK(x2->is_contiguous() && x2->dim() == 3 && x2->size(0) == x.size(0) && x2->size(1) == x.size(1),
+               "groupnorm x2 must be contiguous [N, HW, C2] matching x");
+    SHAI_CHECK(x.size(2) % 8 == 0 && x2->size(2) % 8 == 0, "groupnorm concat halves need C % 8 == 0");
+    a.x2 = cptr(*x2);
+    *C += x2->size(2);
+  }
+}
+
+void groupnorm_stats(const Tensor& x, const optional<Tensor>& x2, const optional<Tensor>& gamma,
+                     const optional<Tensor>& beta, const Tensor& partials, const Tensor& scale, const Tensor& shift,
+                     const optional<Tensor>& counters, int64_t G, double eps) {
   check_f32(partials, "partials");
   check_f32(scale, "scale");
   check_f32(shift, "shift");
-  const int N = x.size(0), HW = x.size(1), C = x.size(2);
+  shai::GroupNormArgs a{};
+  int C;
+  gn_sources(x, x2, a, &C);
+  const int N = x.size(0), HW = x.size(1);
+  if (counters.has_value()) {
+    SHAI_CHECK(counters->is_cuda() && counters->scalar_type() == at::kInt && counters->numel() >= N,
+               "groupnorm counters must be int32 [>= N] on the device");
+    a.counters = reinterpret_cast<unsigned*>(counters->data_ptr<int>());
+  }
   SHAI_CHECK(C % 8 == 0 && C % G == 0 && C <= 4096 && G <= 128, "groupnorm: bad C/G");
   SHAI_CHECK(partials.numel() >= (long)N * shai::gn_num_blocks(N, HW, C) * G * 2, "partials too small");
   SHAI_CHECK(scale.numel() >= (long)N * C && shift.numel() >= (long)N * C, "scale/shift too small");
-  shai::GroupNormArgs a{};
   a.x = cptr(x);
   a.gamma = optr(gamma);
   a.beta = optr(beta);
@@ -382,20 +405,23 @@ void groupnorm_stats(const Tensor& x, const optional<Tensor>& gamma, const optio
   shai::launch_groupnorm_stats(a, stream());
 }
 
-void groupnorm_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const Tensor& out, bool silu) {
-  check_bf16(x, "x");
+void groupnorm_apply(const Tensor& x, const optional<Tensor>& x2, const Tensor& scale, const Tensor& shift,
+                     const Tensor& out, bool silu) {
   check_bf16(out, "out");
-  SHAI_CHECK(x.is_contiguous() && out.is_contiguous() && x.dim() == 3, "groupnorm_apply needs contiguous [N,HW,C]");
   check_f32(scale, "scale");
   check_f32(shift, "shift");
   shai::GroupNormArgs a{};
+  int C;
+  gn_sources(x, x2, a, &C);
+  SHAI_CHECK(out.is_contiguous() && out.numel() == x.size(0) * x.size(1) * (long)C, "groupnorm_apply out must be [N,HW,C]");
+  SHAI_CHECK(scale.numel() >= x.size(0) * (long)C && shift.numel() >= x.size(0) * (long)C, "scale/shift too small");
   a.x = cptr(x);
   a.scale = scale.data_ptr<float>();
   a.shift = shift.data_ptr<float>();
   a.out = mptr(out);
   a.N = x.size(0);
   a.HW = x.size(1);
-  a.C = x.size(2);
+  a.C = C;
   SHAI_CHECK(a.C % 8 == 0, "C % 8");
   a.silu = silu;
   shai::launch_groupnorm_apply(a, stream());
@@ -846,8 +872,8 @@ void embedding(const Tensor& ids, const Tensor& table, const Tensor& out) {
 TORCH_LIBRARY(shai, m) {
   m.def("rmsnorm(Tensor x, Tensor? w, Tensor(a!) out, Tensor? residual, Tensor(b!)? residual_out, float eps, float w_offset) -> ()");
   m.def("layernorm(Tensor x, Tensor? w, Tensor? b, Tensor(a!) out, Tensor? residual, Tensor(b!)? residual_out, float eps) -> ()");
-  m.def("groupnorm_stats(Tensor x, Tensor? gamma, Tensor? beta, Tensor(a!) partials, Tensor(b!) scale, Tensor(c!) shift, int G, float eps) -> ()");
-  m.def("groupnorm_apply(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, bool silu) -> ()");
+  m.def("groupnorm_stats(Tensor x, Tensor? x2, Tensor? gamma, Tensor? beta, Tensor(a!) partials, Tensor(b!) scale, Tensor(c!) shift, Tensor(d!)? counters, int G, float eps) -> ()");
+  m.def("groupnorm_apply(Tensor x, Tensor? x2, Tensor scale, Tensor shift, Tensor(a!) out, bool silu) -> ()");
   m.def("gemm(Tensor a, Tensor w, Tensor(a!) c, Tensor? bias, Tensor? bias2d, int rows_per_bias2d, Tensor? residual, float alpha, float res_alpha, int act, bool glu, Tensor? gate=None, int rows_per_gate=1, int force_cfg=-1, float rms_eps=-1.0) -> ()");
   m.def("layernorm_mod(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, int rows_per_mod, float eps) -> ()");
   m.def("qk_norm_rope(Tensor(a!) x, Tensor? q_w, Tensor? k_w, Tensor? cos, Tensor? sin, int H, int D, int S, float eps) -> ()");

@@ -175,10 +175,14 @@ __global__ void __launch_bounds__(256, 2) flash_fwd_kernel(const AttnArgs p) {
           sacc[kb][r] = bad ? -INFINITY : sacc[kb][r];
         }
     }
+    {  // 4 independent max chains (a single chain is 32 dependent v_max on the critical path)
+      float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) mloc = fmaxf(mloc, fmaxf(sacc[kb][r], sacc[kb][r + 1]));
+        for (int r = 0; r < 16; ++r) m4[r & 3] = fmaxf(m4[r & 3], sacc[kb][r]);
+      mloc = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+    }
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64)) * sl2;   // scale > 0: max commutes with scaling
     const float m_new = fmaxf(m_run, mloc);
     const float m_use = m_new == -INFINITY ? 0.f : m_new;
@@ -186,7 +190,7 @@ __global__ void __launch_bounds__(256, 2) flash_fwd_kernel(const AttnArgs p) {
     const bool grew = __any(m_new > m_run);
     const float alpha = grew ? __builtin_amdgcn_exp2f(m_run - m_use) : 1.f;
     m_run = m_new;
-    float lsum = 0.f;
+    float ls4[4] = {0.f, 0.f, 0.f, 0.f};  // independent partial row sums (ILP)
     bf16x8 pf[2][2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
@@ -194,7 +198,7 @@ __global__ void __launch_bounds__(256, 2) flash_fwd_kernel(const AttnArgs p) {
       for (int r = 0; r < 16; ++r) {
         const float e = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], sl2, -m_use));
         sacc[kb][r] = e;
-        lsum += e;
+        ls4[r & 3] += e;
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -204,6 +208,7 @@ __global__ void __launch_bounds__(256, 2) flash_fwd_kernel(const AttnArgs p) {
         pf[kb][s] = v;
       }
     }
+    const float lsum = (ls4[0] + ls4[1]) + (ls4[2] + ls4[3]);
     l_run = l_run * alpha + lsum;
     if (grew) {
 #pragma unroll

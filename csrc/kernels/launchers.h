@@ -37,6 +37,9 @@ struct GroupNormArgs {
   int N, HW, C, G;
   float eps;
   int silu;
+  const bf16_t* x2;  // optional second source: channels [C1, C) (fused concat; x then holds [0, C1))
+  int C1;
+  unsigned* counters;  // optional [N] zeroed tickets: finalize fused into the stats launch
 };
 int gn_num_blocks(int N, int HW, int C);
 void launch_groupnorm_stats(const GroupNormArgs& a, hipStream_t s);

@@ -123,12 +123,74 @@ void launch_layernorm(const RowNormArgs& a, hipStream_t s) { launch_row_norm<tru
 // GroupNorm over channels-last [N, HW, C] (C % 8 == 0, C <= 4096).
 // Pass 1: grid (N, NB); each block reduces a contiguous pixel range into
 //         per-group (sum, sumsq) partials  -> part[N][NB][G][2].
-// Pass 2: grid (N); reduce partials, emit scale/shift [N][C] (fp32) such that
+// Pass 2: grid (N) -- or fused into pass 1's last block per image (ticket counters) --
+//         reduce partials, emit scale/shift [N][C] (fp32) such that
 //         y = x * scale + shift  ==  (x - mean) * rstd * gamma + beta.
 // Pass 3 (optional): apply (+ SiLU) elementwise.
 // ----------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict__ x, float* __restrict__ part,
-                                                       int HW, int C, int G, int NB, int ppb) {
+// Per-(image, group) finalize shared by the fused path (last stats block of an image) and the
+// standalone kernel: reduce the NB partials of image n, emit scale/shift [C].
+__device__ void gn_finalize_image(const float* __restrict__ part, const bf16_t* __restrict__ gamma,
+                                  const bf16_t* __restrict__ beta, float* __restrict__ scale,
+                                  float* __restrict__ shift, int n, int HW, int C, int G, int NB, float eps,
+                                  bool coherent) {
+  __shared__ float mean_s[128], rstd_s[128];
+  __shared__ float red[2][256];
+  const int Cg = C / G;
+  // 256 threads = L lanes per group x G groups (L = 256 / G); lanes stride over the partials
+  const int L = 256 / G;
+  const int g0 = threadIdx.x % G, lane_k = threadIdx.x / G;
+  float a = 0.f, b = 0.f;
+  if (lane_k < L) {
+    for (int k = lane_k; k < NB; k += L) {
+      const float* src = part + (((long)n * NB + k) * G + g0) * 2;
+      if (coherent) {  // written by other workgroups (possibly other XCDs) of this launch
+        a += __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        b += __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        const float2 v = *reinterpret_cast<const float2*>(src);
+        a += v.x;
+        b += v.y;
+      }
+    }
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    double sa = 0.0, sb = 0.0;
+    for (int l = 0; l < L; ++l) {
+      sa += red[0][l * G + g];
+      sb += red[1][l * G + g];
+    }
+    const double cnt = (double)HW * Cg;
+    const double mean = sa / cnt;
+    double var = sb / cnt - mean * mean;
+    if (var < 0) var = 0;
+    mean_s[g] = (float)mean;
+    rstd_s[g] = (float)(1.0 / sqrt(var + (double)eps));
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int g = c / Cg;
+    const float ga = gamma ? bf2f(gamma[c]) : 1.f;
+    const float be = beta ? bf2f(beta[c]) : 0.f;
+    const float sc = rstd_s[g] * ga;
+    scale[(long)n * C + c] = sc;
+    shift[(long)n * C + c] = be - mean_s[g] * sc;
+  }
+}
+
+// Stats over channels-last [N, HW, C] whose channels [0, C1) come from x (row stride C1) and
+// [C1, C) from x2 (row stride C - C1): the UNet up-block skip concat is never materialised.
+// With `counters` the LAST block of image n (agent-scope ticket, self re-arming to 0 so a HIP
+// graph replays it) also runs the finalize: one launch instead of stats + finalize.
+__global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ x2,
+                                                       int C1, float* __restrict__ part, int HW, int C, int G, int NB,
+                                                       int ppb, unsigned* __restrict__ counters,
+                                                       const bf16_t* __restrict__ gamma,
+                                                       const bf16_t* __restrict__ beta, float* __restrict__ scale,
+                                                       float* __restrict__ shift, float eps) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [P][C] sums then [P][C] sumsq
   const int n = blockIdx.y, blk = blockIdx.x;
   const int C8 = C >> 3;
@@ -136,12 +198,28 @@ __global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict_
   const int P = C8 <= 256 ? 256 / C8 : 1;
   const int p0 = blk * ppb;
   const int p1 = min(HW, p0 + ppb);
-  const bf16_t* xn = x + (long)n * HW * C;
+  const int C2 = C - C1;
   // each thread: pixel lane pl, channel vectors cv0 (and cv0+256 when C8>256)
   const int pl = C8 <= 256 ? t / C8 : 0;
   const int cv0 = C8 <= 256 ? t % C8 : t;
   const bool active = C8 <= 256 ? (t < P * C8) : (t < C8);
   const bool second = C8 > 256 && (t + 256) < C8;
+  // per-thread source (x or x2) of its channel vector(s): base pointer + row stride
+  auto src_of = [&](int cv, const bf16_t*& base, int& ld) {
+    const int c = cv * 8;
+    if (c < C1) {
+      base = x + (long)n * HW * C1 + c;
+      ld = C1;
+    } else {
+      base = x2 + (long)n * HW * C2 + (c - C1);
+      ld = C2;
+    }
+  };
+  const bf16_t* b0 = x;
+  const bf16_t* b1 = x;
+  int ld0 = C, ld1 = C;
+  src_of(cv0, b0, ld0);
+  if (second) src_of(cv0 + 256, b1, ld1);
   float s0[8], q0[8], s1[8], q1[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) s0[i] = q0[i] = s1[i] = q1[i] = 0.f;
@@ -151,7 +229,7 @@ __global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict_
     for (; p + 3 * P < p1; p += 4 * P) {
       uint4_ v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4_*>(xn + (long)(p + u * P) * C + cv0 * 8);
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4_*>(b0 + (long)(p + u * P) * ld0);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         float f[8];
@@ -164,7 +242,7 @@ __global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict_
       }
       if (second) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4_*>(xn + (long)(p + u * P) * C + (cv0 + 256) * 8);
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4_*>(b1 + (long)(p + u * P) * ld1);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           float f[8];
@@ -178,16 +256,15 @@ __global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict_
       }
     }
     for (; p < p1; p += P) {
-      const bf16_t* xp = xn + (long)p * C;
       float f[8];
-      unpack8(*reinterpret_cast<const uint4_*>(xp + cv0 * 8), f);
+      unpack8(*reinterpret_cast<const uint4_*>(b0 + (long)p * ld0), f);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         s0[i] += f[i];
         q0[i] += f[i] * f[i];
       }
       if (second) {
-        unpack8(*reinterpret_cast<const uint4_*>(xp + (cv0 + 256) * 8), f);
+        unpack8(*reinterpret_cast<const uint4_*>(b1 + (long)p * ld1), f);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           s1[i] += f[i];
@@ -232,67 +309,51 @@ __global__ void __launch_bounds__(256) gn_stats_kernel(const bf16_t* __restrict_
       b += lq[g * Cg + c];
     }
     float* o = part + (((long)n * NB + blk) * G + g) * 2;
-    o[0] = a;
-    o[1] = b;
+    if (counters) {  // read back by another workgroup of this launch: store at agent scope
+      __hip_atomic_store(o, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      o[0] = a;
+      o[1] = b;
+    }
   }
+  if (!counters) return;
+  // Fence-free hand-off (MI355X_MICROARCH.md, sc1 hand-off table, row 1): partials stored sc1
+  // (agent-scope relaxed stores above), every storing wave waits for its stores, a barrier, then
+  // ONE lane's agent-scope add; the block whose add returns NB-1 reads every partial with sc1
+  // loads.  No buffer_wbl2 / buffer_inv (an acq_rel fence per block measured 2x slower).
+  __shared__ unsigned s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(counters + n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == (unsigned)(NB - 1);
+    if (s_last) __hip_atomic_store(counters + n, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  }
+  __syncthreads();
+  if (!s_last) return;
+  gn_finalize_image(part, gamma, beta, scale, shift, n, HW, C, G, NB, eps, true);
 }
 
 __global__ void __launch_bounds__(256) gn_finalize_kernel(const float* __restrict__ part, const bf16_t* __restrict__ gamma,
                                                           const bf16_t* __restrict__ beta, float* __restrict__ scale,
                                                           float* __restrict__ shift, int HW, int C, int G, int NB,
                                                           float eps) {
-  __shared__ float mean_s[128], rstd_s[128];
-  __shared__ float red[2][256];
-  const int n = blockIdx.x;
-  const int Cg = C / G;
-  // 256 threads = L lanes per group x G groups (L = 256 / G); lanes stride over the partials
-  const int L = 256 / G;
-  const int g0 = threadIdx.x % G, lane_k = threadIdx.x / G;
-  float a = 0.f, b = 0.f;
-  if (lane_k < L) {
-    for (int k = lane_k; k < NB; k += L) {
-      const float2 v = *reinterpret_cast<const float2*>(part + (((long)n * NB + k) * G + g0) * 2);
-      a += v.x;
-      b += v.y;
-    }
-  }
-  red[0][threadIdx.x] = a;
-  red[1][threadIdx.x] = b;
-  __syncthreads();
-  for (int g = threadIdx.x; g < G; g += blockDim.x) {
-    double sa = 0.0, sb = 0.0;
-    for (int l = 0; l < L; ++l) {
-      sa += red[0][l * G + g];
-      sb += red[1][l * G + g];
-    }
-    const double cnt = (double)HW * Cg;
-    const double mean = sa / cnt;
-    double var = sb / cnt - mean * mean;
-    if (var < 0) var = 0;
-    mean_s[g] = (float)mean;
-    rstd_s[g] = (float)(1.0 / sqrt(var + (double)eps));
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const int g = c / Cg;
-    const float ga = gamma ? bf2f(gamma[c]) : 1.f;
-    const float be = beta ? bf2f(beta[c]) : 0.f;
-    const float sc = rstd_s[g] * ga;
-    scale[(long)n * C + c] = sc;
-    shift[(long)n * C + c] = be - mean_s[g] * sc;
-  }
+  gn_finalize_image(part, gamma, beta, scale, shift, blockIdx.x, HW, C, G, NB, eps, false);
 }
 
-__global__ void __launch_bounds__(256) gn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
+__global__ void __launch_bounds__(256) gn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ x2,
+                                                       int C1, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, bf16_t* __restrict__ out,
                                                        long total8, int HW, int C, int silu) {
-  const int C8 = C >> 3;
+  const int C8 = C >> 3, C18 = C1 >> 3, C28 = (C - C1) >> 3;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total8; i += (long)gridDim.x * blockDim.x) {
     const long pix = i / C8;
     const int cv = (int)(i - pix * C8);
     const int n = (int)(pix / HW);
     float f[8];
-    unpack8(reinterpret_cast<const uint4_*>(x)[i], f);
+    if (cv < C18) unpack8(reinterpret_cast<const uint4_*>(x)[pix * C18 + cv], f);  // (x2 == null: C1 == C)
+    else unpack8(reinterpret_cast<const uint4_*>(x2)[pix * C28 + (cv - C18)], f);
     const float* sc = scale + (long)n * C + cv * 8;
     const float* sh = shift + (long)n * C + cv * 8;
     const float4_ a0 = *reinterpret_cast<const float4_*>(sc), a1 = *reinterpret_cast<const float4_*>(sc + 4);
@@ -329,15 +390,19 @@ void launch_groupnorm_stats(const GroupNormArgs& a, hipStream_t s) {
   const int C8 = a.C / 8;
   const int P = C8 <= 256 ? 256 / C8 : 1;
   const size_t lds = (size_t)2 * P * a.C * sizeof(float);
-  gn_stats_kernel<<<dim3(NB, a.N), 256, lds, s>>>(a.x, a.partials, a.HW, a.C, a.G, NB, ppb);
-  gn_finalize_kernel<<<a.N, 256, 0, s>>>(a.partials, a.gamma, a.beta, a.scale, a.shift, a.HW, a.C, a.G, NB, a.eps);
+  const int C1 = a.x2 ? a.C1 : a.C;
+  gn_stats_kernel<<<dim3(NB, a.N), 256, lds, s>>>(a.x, a.x2, C1, a.partials, a.HW, a.C, a.G, NB, ppb, a.counters,
+                                                  a.gamma, a.beta, a.scale, a.shift, a.eps);
+  if (!a.counters)
+    gn_finalize_kernel<<<a.N, 256, 0, s>>>(a.partials, a.gamma, a.beta, a.scale, a.shift, a.HW, a.C, a.G, NB, a.eps);
 }
 
 void launch_groupnorm_apply(const GroupNormArgs& a, hipStream_t s) {
   const long total8 = (long)a.N * a.HW * a.C / 8;
   long blocks = (total8 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  gn_apply_kernel<<<(int)blocks, 256, 0, s>>>(a.x, a.scale, a.shift, a.out, total8, a.HW, a.C, a.silu);
+  gn_apply_kernel<<<(int)blocks, 256, 0, s>>>(a.x, a.x2, a.x2 ? a.C1 : a.C, a.scale, a.shift, a.out, total8, a.HW,
+                                              a.C, a.silu);
 }
 
 }  // namespace shai

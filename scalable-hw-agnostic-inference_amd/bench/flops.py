@@ -67,15 +67,18 @@ def count_flops():
         fc.add("bmm", 2.0 * B * M * w.shape[-2] * K)
         return torch.empty(B, M, w.shape[-2], dtype=a.dtype, device=a.device)
 
-    def gn_stats(x, gamma, beta, groups, eps):
-        N, C = x.shape[0], x.shape[-1]
+    def gn_stats(x, gamma, beta, groups, eps, x2=None):
+        N, C = x.shape[0], x.shape[-1] + (x2.shape[-1] if x2 is not None else 0)
         return torch.ones(N, C), torch.zeros(N, C)
+
+    def gn_apply(x, scale, shift, silu=False, x2=None):
+        return x if x2 is None else torch.empty(*x.shape[:-1], x.shape[-1] + x2.shape[-1], dtype=x.dtype)
 
     def ln(x, w, b, eps=1e-5, residual=None):
         return x, residual
 
     for n, f in (("linear", linear), ("conv2d", conv2d), ("attention", attention), ("bmm", bmm),
-                 ("groupnorm_stats", gn_stats), ("layernorm", ln), ("groupnorm_apply", lambda x, *a, **k: x),
+                 ("groupnorm_stats", gn_stats), ("layernorm", ln), ("groupnorm_apply", gn_apply),
                  ("bias_act", lambda x, *a, **k: x), ("softmax_", lambda x, *a, **k: x)):
         setattr(ops, n, f)
     try:

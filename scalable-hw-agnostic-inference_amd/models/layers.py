@@ -114,13 +114,14 @@ class GroupNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(channels, dtype=dtype), requires_grad=False)
         self.bias = nn.Parameter(torch.zeros(channels, dtype=dtype), requires_grad=False)
 
-    def stats(self, x):
+    def stats(self, x, x2=None):
         """(scale, shift) fp32 [N, C]: fed to a consumer conv's fused prologue."""
-        return ops.groupnorm_stats(x, self.weight, self.bias, self.groups, self.eps)
+        return ops.groupnorm_stats(x, self.weight, self.bias, self.groups, self.eps, x2=x2)
 
-    def forward(self, x, silu: bool = False):
-        sc, sh = self.stats(x)
-        return ops.groupnorm_apply(x, sc, sh, silu)
+    def forward(self, x, silu: bool = False, x2=None):
+        """GroupNorm of x, or of cat([x, x2], -1) without materialising the concat."""
+        sc, sh = self.stats(x, x2)
+        return ops.groupnorm_apply(x, sc, sh, silu, x2=x2)
 
 
 class LayerNorm(nn.Module):

@@ -64,11 +64,16 @@ class ResnetBlock2D(nn.Module):
         self.conv2 = Conv2d(cout, cout, 3, padding=1)
         self.conv_shortcut = Conv2d(cin, cout, 1) if cin != cout else None
 
-    def forward(self, x, temb_proj=None):
+    def forward(self, x, temb_proj=None, x2=None):
+        """``x2``: up-block skip tensor -- the block's input is cat([x, x2], -1), read from the two
+        sources by GroupNorm and by the 1x1 shortcut conv (fused concat), never materialised."""
         # GroupNorm+SiLU as one memory-bound pass (normalising inside the 3x3 gather would
         # redo the transform 9x per N-tile: VALU-bound, measured 5x slower).
-        h = self.conv1(self.norm1(x, silu=True), temb=temb_proj)
-        skip = self.conv_shortcut(x) if self.conv_shortcut is not None else x
+        h = self.conv1(self.norm1(x, silu=True, x2=x2), temb=temb_proj)
+        if self.conv_shortcut is not None:
+            skip = self.conv_shortcut(x, x2=x2) if x2 is not None else self.conv_shortcut(x)
+        else:
+            skip = x if x2 is None else torch.cat([x, x2], dim=-1)
         return self.conv2(self.norm2(h, silu=True), residual=skip)
 
 
@@ -274,7 +279,7 @@ class UNet2DConditionModel(nn.Module):
         for blk in self.up_blocks:
             for i, r in enumerate(blk.resnets):
                 s = skips.pop()
-                x = r(torch.cat([x, s], dim=-1), next(ti))
+                x = r(x, next(ti), x2=s)
                 if blk.attentions is not None:
                     x = blk.attentions[i](x, next(kvi))
             if blk.upsamplers is not None:

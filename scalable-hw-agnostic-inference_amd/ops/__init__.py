@@ -11,6 +11,7 @@ captured into HIP graphs (``torch.cuda.CUDAGraph`` is hipGraph on ROCm).
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -70,32 +71,58 @@ def layernorm(x: torch.Tensor, w: Optional[torch.Tensor], b: Optional[torch.Tens
     return y.view(shape), (new_res.view(shape) if new_res is not None else None)
 
 
-def groupnorm_stats(x: torch.Tensor, gamma, beta, groups: int, eps: float):
-    """Channels-last GroupNorm statistics. x [N, ..., C] -> (scale, shift) fp32 [N, C]."""
-    N, C = x.shape[0], x.shape[-1]
-    x3 = x.reshape(N, -1, C)
+_GN_TICKETS: dict = {}
+# Finalize fused into the stats launch (last-block ticket) is opt-in: on MI355X the per-block
+# agent-scope add + vmcnt drain made GN+SiLU 1.3-1.45x SLOWER than a separate 8-block finalize
+# launch (8x4096x320: 40.6 vs 28.2 us), so the two-launch path stays the default.
+_GN_FUSED = os.environ.get("SHAI_GN_FUSED_FINALIZE", "0") == "1"
+
+
+def _gn_tickets(x: torch.Tensor, n: int) -> Optional[torch.Tensor]:
+    """Zeroed int32 tickets for the stats kernel's fused finalize, one set per (device, stream):
+    the kernel re-arms them to 0, so they stay valid across launches and HIP-graph replays."""
+    if not _GN_FUSED or n > 4096:
+        return None
+    key = (x.device.index, torch.cuda.current_stream(x.device).cuda_stream)
+    t = _GN_TICKETS.get(key)
+    if t is None:
+        t = _GN_TICKETS[key] = torch.zeros(4096, dtype=torch.int32, device=x.device)
+    return t
+
+
+def groupnorm_stats(x: torch.Tensor, gamma, beta, groups: int, eps: float, x2: Optional[torch.Tensor] = None):
+    """Channels-last GroupNorm statistics. x [N, ..., C] -> (scale, shift) fp32 [N, C].
+    With ``x2`` the statistics are those of ``cat([x, x2], -1)`` without materialising it."""
+    N = x.shape[0]
+    x3 = x.reshape(N, -1, x.shape[-1])
+    x23 = x2.reshape(N, -1, x2.shape[-1]) if x2 is not None else None
+    C = x3.shape[-1] + (x23.shape[-1] if x23 is not None else 0)
     if not _gpu(x):
-        return ref.groupnorm_stats(x3, gamma, beta, groups, eps)
-    HW = x3.shape[1]
+        xx = torch.cat([x3, x23], -1) if x23 is not None else x3
+        return ref.groupnorm_stats(xx, gamma, beta, groups, eps)
     part = torch.empty(N * 256 * groups * 2, dtype=torch.float32, device=x.device)
     scale = torch.empty(N, C, dtype=torch.float32, device=x.device)
     shift = torch.empty(N, C, dtype=torch.float32, device=x.device)
-    _K().groupnorm_stats(x3, gamma, beta, part, scale, shift, int(groups), float(eps))
+    _K().groupnorm_stats(x3, x23, gamma, beta, part, scale, shift, _gn_tickets(x, N), int(groups), float(eps))
     return scale, shift
 
 
-def groupnorm_apply(x: torch.Tensor, scale, shift, silu: bool = False) -> torch.Tensor:
+def groupnorm_apply(x: torch.Tensor, scale, shift, silu: bool = False, x2: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = (silu)(x * scale + shift); with ``x2`` the input is ``cat([x, x2], -1)`` (never materialised)."""
     if not _gpu(x):
-        return ref.groupnorm_apply(x, scale, shift, silu)
-    N, C = x.shape[0], x.shape[-1]
-    out = torch.empty_like(x)
-    _K().groupnorm_apply(x.reshape(N, -1, C), scale, shift, out.view(N, -1, C), bool(silu))
+        xx = torch.cat([x, x2], -1) if x2 is not None else x
+        return ref.groupnorm_apply(xx, scale, shift, silu)
+    N = x.shape[0]
+    C = x.shape[-1] + (x2.shape[-1] if x2 is not None else 0)
+    out = torch.empty(*x.shape[:-1], C, dtype=x.dtype, device=x.device)
+    _K().groupnorm_apply(x.reshape(N, -1, x.shape[-1]), x2.reshape(N, -1, x2.shape[-1]) if x2 is not None else None,
+                         scale, shift, out.view(N, -1, C), bool(silu))
     return out
 
 
-def groupnorm(x, gamma, beta, groups, eps, silu=False):
-    scale, shift = groupnorm_stats(x, gamma, beta, groups, eps)
-    return groupnorm_apply(x, scale, shift, silu)
+def groupnorm(x, gamma, beta, groups, eps, silu=False, x2=None):
+    scale, shift = groupnorm_stats(x, gamma, beta, groups, eps, x2=x2)
+    return groupnorm_apply(x, scale, shift, silu, x2=x2)
 
 
 # ----------------------------------------------------------------------------- GEMM / conv

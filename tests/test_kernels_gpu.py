@@ -61,6 +61,29 @@ def test_groupnorm(cuda, N, HW, C, G):
     close(ops.groupnorm_apply(x, sc, sh, True), ref.groupnorm_apply(x, scr, shr, True), 2e-2)
 
 
+@pytest.mark.parametrize("N,HW,C1,C2", [(2, 4096, 320, 320), (3, 64, 1280, 640), (1, 1000, 640, 320), (8, 256, 64, 256)])
+@pytest.mark.parametrize("fused", [True, False])
+def test_groupnorm_two_source(cuda, N, HW, C1, C2, fused, monkeypatch):
+    """GN of cat([x, x2], -1) read from the two sources (UNet up-block skip concat) with the
+    finalize fused into the stats launch (ticket counters) or as its own kernel; repeated calls
+    check that the tickets re-arm."""
+    monkeypatch.setattr(ops, "_GN_FUSED", fused)
+    torch.manual_seed(5)
+    x, x2 = rnd(N, HW, C1, scale=2.0) + 0.5, rnd(N, HW, C2) - 0.25
+    g, b = rnd(C1 + C2), rnd(C1 + C2)
+    xc = torch.cat([x, x2], -1)
+    scr, shr = ref.groupnorm_stats(xc, g, b, 32, 1e-5)
+    for _ in range(3):
+        sc, sh = ops.groupnorm_stats(x, g, b, 32, 1e-5, x2=x2)
+        torch.testing.assert_close(sc, scr, atol=1e-3, rtol=1e-3)
+        torch.testing.assert_close(sh, shr, atol=1e-3, rtol=1e-3)
+    y = ops.groupnorm_apply(x, sc, sh, True, x2=x2)
+    assert y.shape == (N, HW, C1 + C2)
+    close(y, ref.groupnorm_apply(xc, scr, shr, True), 2e-2)
+    if fused:
+        assert int(ops._gn_tickets(x, N)[:N].abs().sum()) == 0  # re-armed
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (1000, 320, 1280), (77, 1024, 1024), (8192, 640, 320),
                                    (5, 4096, 4096), (300, 96, 72)])
 @pytest.mark.parametrize("act", ["none", "silu", "gelu"])
