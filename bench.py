@@ -252,18 +252,20 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="sd21", choices=["sd21", "mistral", "flux", "mllama"])
     ap.add_argument("--batch", type=int, default=None,
-                    help="per-GPU batch: images per step (sd21: 16, flux: 1) / concurrent sequences (mistral: 64, "
+                    help="per-GPU batch: images per step (sd21: 32, flux: 1) / concurrent sequences (mistral: 64, "
                          "mllama: 8)")
     ap.add_argument("--inference-steps", type=int, default=50)
     ap.add_argument("--height", type=int, default=512)
     ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--quantization", default=None, choices=[None, "fp8"],
+                    help="mistral: fp8 e4m3 weight-only quantisation (NOT the bf16 headline config)")
     ap.add_argument("--latency-runs", type=int, default=3)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--gen-len", type=int, default=128)
     args = ap.parse_args()
     if args.batch is None:  # dynamic-batching caps a serving replica would use for each workload
-        args.batch = {"sd21": 16, "mistral": 64, "flux": 1, "mllama": 8}[args.workload]
+        args.batch = {"sd21": 32, "mistral": 64, "flux": 1, "mllama": 8}[args.workload]
     import torch
     rank, world, local = _dist_init(args.gpus)
     with torch.inference_mode():

@@ -51,7 +51,7 @@ std::string gemm_key(const shai::GemmArgs& g) {
   char buf[256];
   snprintf(buf, sizeof(buf), "%d:%d,%d,%d,b%d,g%d|%d,%d,%d,%d,%d,%d,%d,%d,%d", g.conv, g.M, g.N, g.K, g.batch, g.glu,
            g.Nimg, g.H, g.Wd, g.Cin, g.Cin1, g.KH, g.stride, g.upsample, g.A2 != nullptr);
-  return g.rms ? std::string(buf) + "|rms" : std::string(buf);
+  return std::string(buf) + (g.rms ? "|rms" : "") + (g.w_scale ? "|fp8w" : "");
 }
 
 bool autotune_enabled() {
@@ -432,9 +432,19 @@ void groupnorm_apply(const Tensor& x, const optional<Tensor>& x2, const Tensor& 
 void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tensor>& bias,
           const optional<Tensor>& bias2d, int64_t rows_per_bias2d, const optional<Tensor>& residual, double alpha,
           double res_alpha, int64_t act, bool glu, const optional<Tensor>& gate, int64_t rows_per_gate,
-          int64_t force_cfg, double rms_eps) {
+          int64_t force_cfg, double rms_eps, const optional<Tensor>& w_scale) {
   check_rows(a, "a");
-  check_rows(w, "w");
+  if (w_scale.has_value()) {  // fp8 (e4m3) weights + fp32 per-row scale: skinny (decode-shaped) kernel only
+    SHAI_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat8_e4m3fn && w.dim() == 2 && w.stride(1) == 1 &&
+                   w.stride(0) % 16 == 0,
+               "fp8 gemm: w must be a row-major float8_e4m3fn [N, K] matrix with 16-byte aligned rows");
+    check_f32(*w_scale, "w_scale");
+    SHAI_CHECK(w_scale->is_contiguous() && w_scale->numel() == w.size(0), "w_scale must be fp32 [N]");
+    SHAI_CHECK(a.dim() == 2 && a.size(0) <= 64 && a.size(1) % 16 == 0,
+               "fp8 gemm: decode-shaped activations only (M <= 64, K % 16 == 0); dequantize for larger M");
+  } else {
+    check_rows(w, "w");
+  }
   check_bf16(c, "c");
   SHAI_CHECK(a.dim() == w.dim() || w.dim() == 2, "gemm rank mismatch");
   const bool batched = a.dim() == 3;
@@ -487,6 +497,17 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
   g.res_alpha = res_alpha;
   g.act = act;
   g.glu = glu;
+  if (w_scale.has_value()) {
+    g.w_scale = w_scale->data_ptr<float>();
+    SHAI_CHECK(shai::skinny_supported(g), "fp8 gemm: problem not supported by the skinny kernel");
+    if (rms_eps >= 0) {
+      g.rms = 1;
+      g.rms_eps = (float)rms_eps;
+    }
+    if (force_cfg > kSkinnyCfg) launch_choice(g, a, Choice{kSkinnyCfg, (int)(force_cfg - kSkinnyCfg)});
+    else run_skinny(g, a);
+    return;
+  }
   const long a_bytes = (batched ? (long)a.size(0) * a.stride(0) : (long)g.M * g.lda) * 2;
   // tests / tools bypass the tuner: force_cfg = gemm2 config, 1000 = skinny kernel (heuristic K groups),
   // 1000 + kg = skinny kernel with kg K groups
@@ -869,12 +890,24 @@ void embedding(const Tensor& ids, const Tensor& table, const Tensor& out) {
 
 }  // namespace
 
+void dequant_fp8(const Tensor& w8, const Tensor& scale, const Tensor& out) {
+  SHAI_CHECK(w8.is_cuda() && w8.scalar_type() == at::kFloat8_e4m3fn && w8.dim() == 2 && w8.is_contiguous() &&
+                 w8.size(1) % 8 == 0,
+             "dequant_fp8: w8 must be a contiguous float8_e4m3fn [N, K], K % 8 == 0");
+  check_f32(scale, "scale");
+  check_bf16(out, "out");
+  SHAI_CHECK(scale.numel() == w8.size(0) && out.is_contiguous() && out.numel() == w8.numel(), "dequant_fp8 shapes");
+  shai::launch_dequant_fp8_rows(reinterpret_cast<const uint8_t*>(w8.data_ptr()), scale.data_ptr<float>(), mptr(out),
+                                w8.size(0), w8.size(1), stream());
+}
+
 TORCH_LIBRARY(shai, m) {
   m.def("rmsnorm(Tensor x, Tensor? w, Tensor(a!) out, Tensor? residual, Tensor(b!)? residual_out, float eps, float w_offset) -> ()");
   m.def("layernorm(Tensor x, Tensor? w, Tensor? b, Tensor(a!) out, Tensor? residual, Tensor(b!)? residual_out, float eps) -> ()");
   m.def("groupnorm_stats(Tensor x, Tensor? x2, Tensor? gamma, Tensor? beta, Tensor(a!) partials, Tensor(b!) scale, Tensor(c!) shift, Tensor(d!)? counters, int G, float eps) -> ()");
   m.def("groupnorm_apply(Tensor x, Tensor? x2, Tensor scale, Tensor shift, Tensor(a!) out, bool silu) -> ()");
-  m.def("gemm(Tensor a, Tensor w, Tensor(a!) c, Tensor? bias, Tensor? bias2d, int rows_per_bias2d, Tensor? residual, float alpha, float res_alpha, int act, bool glu, Tensor? gate=None, int rows_per_gate=1, int force_cfg=-1, float rms_eps=-1.0) -> ()");
+  m.def("gemm(Tensor a, Tensor w, Tensor(a!) c, Tensor? bias, Tensor? bias2d, int rows_per_bias2d, Tensor? residual, float alpha, float res_alpha, int act, bool glu, Tensor? gate=None, int rows_per_gate=1, int force_cfg=-1, float rms_eps=-1.0, Tensor? w_scale=None) -> ()");
+  m.def("dequant_fp8(Tensor w8, Tensor scale, Tensor(a!) out) -> ()");
   m.def("layernorm_mod(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, int rows_per_mod, float eps) -> ()");
   m.def("qk_norm_rope(Tensor(a!) x, Tensor? q_w, Tensor? k_w, Tensor? cos, Tensor? sin, int H, int D, int S, float eps) -> ()");
   m.def("conv2d(Tensor x, Tensor? x2, Tensor w, Tensor(a!) out, Tensor? bias, Tensor? bias2d, Tensor? residual, Tensor? in_scale, Tensor? in_shift, int in_act, int kh, int kw, int stride, int pad, bool upsample, int act, float res_alpha) -> ()");
@@ -901,6 +934,7 @@ TORCH_LIBRARY_IMPL(shai, CUDA, m) {
   m.impl("groupnorm_stats", &groupnorm_stats);
   m.impl("groupnorm_apply", &groupnorm_apply);
   m.impl("gemm", &gemm);
+  m.impl("dequant_fp8", &dequant_fp8);
   m.impl("layernorm_mod", &layernorm_mod);
   m.impl("qk_norm_rope", &qk_norm_rope);
   m.impl("conv2d", &conv2d);

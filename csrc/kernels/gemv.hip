@@ -24,6 +24,11 @@
 //   residual / folded RMSNorm).  When N/64 tiles cannot fill the chip, K is
 //   additionally split over KG workgroups writing fp32 partials that the shared
 //   split-K fold (gemm_lds.hip) reduces + epilogues.
+// * fp8 weights (F8, GemmArgs::w_scale set): W is OCP e4m3 [N, K] with one fp32 scale per
+//   output row.  The W tile is 64 rows x 64 B (one DMA instruction per wave, 16-B chunk
+//   swizzle chunk ^ (row >> 2) & 3); each lane's 8-byte fragment is widened in registers
+//   (v_cvt_pk_f32_fp8 -> bf16, exact) and fed to the same bf16 MFMA; the row scale is applied
+//   in the reduction.  Half the weight bytes per token: decode is weight-bandwidth bound.
 #include "common.h"
 #include "launchers.h"
 
@@ -37,12 +42,13 @@ constexpr int SK_BK = 64;       // K per step
 constexpr int SK_WAVES = 4;
 constexpr uint32_t SK_OOB = 0x80000000u;
 
-template <int MB>
+template <int MB, bool F8 = false>
 struct SkGeom {
   static constexpr int XG = MB / 32;                    // 32-row X groups
   static constexpr int STAGES = MB == 32 ? 6 : 4;
-  static constexpr int STAGE_ELEMS = (SK_BN + MB) * SK_BK;  // W tile then X tile
-  static constexpr int PER = 2 + XG;                    // DMA instructions per wave per step
+  static constexpr int W_ELEMS = F8 ? SK_BN * SK_BK / 2 : SK_BN * SK_BK;  // W tile in bf16 units
+  static constexpr int STAGE_ELEMS = W_ELEMS + MB * SK_BK;  // W tile then X tile
+  static constexpr int PER = (F8 ? 1 : 2) + XG;         // DMA instructions per wave per step
   static constexpr int RP = MB + 1;                     // padded row of the reduction image
   static constexpr size_t LDS = (size_t)STAGES * STAGE_ELEMS * 2 > (size_t)SK_WAVES * SK_BN * RP * 4
                                     ? (size_t)STAGES * STAGE_ELEMS * 2
@@ -105,10 +111,31 @@ __device__ __forceinline__ void sk_epilogue(const GemmArgs& p, int n0, Get get) 
   }
 }
 
-template <int MB, bool GLU, int ACT, bool RMS>
+// 8 fp8 (e4m3) weights at `src` (8-byte aligned LDS) -> bf16x8 (exact widening)
+__device__ __forceinline__ bf16x8s sk_fp8x8(const bf16_t* src) {
+  const uint2_ v = *reinterpret_cast<const uint2_*>(src);
+  bf16x8s r;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)v[h], false);
+    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)v[h], true);
+    r[4 * h + 0] = (__bf16)lo[0];
+    r[4 * h + 1] = (__bf16)lo[1];
+    r[4 * h + 2] = (__bf16)hi[0];
+    r[4 * h + 3] = (__bf16)hi[1];
+  }
+  return r;
+}
+
+// byte offset of the 8-byte chunk c8 (0..7) of fp8 W row `row` in the 64 x 64 B tile image
+__device__ __forceinline__ int sk_f8_off(int row, int c8) {
+  return row * 64 + (((c8 >> 1) ^ ((row >> 2) & 3)) << 4) + ((c8 & 1) << 3);
+}
+
+template <int MB, bool GLU, int ACT, bool RMS, bool F8>
 __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmArgs p, float* __restrict__ ws,
                                                                     int kg_steps) {
-  using G = SkGeom<MB>;
+  using G = SkGeom<MB, F8>;
   constexpr int XG = G::XG;
   extern __shared__ __attribute__((aligned(16))) bf16_t sk_smem[];
   __shared__ float ss_red[SK_WAVES][64 * XG];
@@ -122,7 +149,7 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
   const int t0 = kg * kg_steps;
   const int nk = max(0, min(ksteps, t0 + kg_steps) - t0);
 
-  const __amdgpu_buffer_rsrc_t rW = sk_rsrc(p.W, (uint32_t)min((long)p.N * p.ldw * 2, 0x7fffffffL));
+  const __amdgpu_buffer_rsrc_t rW = sk_rsrc(p.W, (uint32_t)min((long)p.N * p.ldw * (F8 ? 1 : 2), 0x7fffffffL));
   const __amdgpu_buffer_rsrc_t rX = sk_rsrc(p.A, (uint32_t)min((long)p.M * p.lda * 2, 0x7fffffffL));
 
   // DMA geometry: a wave instruction fills 8 LDS rows x 128 B, lane-linear; the lane at
@@ -137,15 +164,25 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
   const int xr = w * 8 + lrow;                 // X rows xr (+ 32 for the second group)
   const int xc = lpos ^ ((xr >> 1) & 7);       // (xr + 32) has the same swizzle
 
+  // fp8 W: one wave instruction = 16 rows x 64 B; lane at chunk position lpos4 fetches chunk lpos4 ^ swz
+  const int f8row = w * 16 + (lane >> 2), f8pos = lane & 3;
+  const int f8c = f8pos ^ ((f8row >> 2) & 3);
   auto stage = [&](int buf, int step) {
     bf16_t* sw = sk_smem + buf * G::STAGE_ELEMS;
-    bf16_t* sx = sw + SK_BN * SK_BK;
+    bf16_t* sx = sw + G::W_ELEMS;
     const int k0 = (t0 + step) * SK_BK;
+    if constexpr (F8) {
+      const int n = n0 + f8row, k = k0 + f8c * 16;
+      const uint32_t off = (n < p.N && k < p.K) ? (uint32_t)((long)n * p.ldw + k) : SK_OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (sk_lds_void*)(sw + w * 16 * 32), 16, off, 0, 0, 0);
+    } else {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wr[j], k = k0 + wc[j] * 8;
-      const uint32_t off = (n < p.N && k < p.K) ? (uint32_t)(((long)n * p.ldw + k) * 2) : SK_OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (sk_lds_void*)(sw + (w * 2 + j) * 8 * SK_BK), 16, off, 0, 0, 0);
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wr[j], k = k0 + wc[j] * 8;
+        const uint32_t off = (n < p.N && k < p.K) ? (uint32_t)(((long)n * p.ldw + k) * 2) : SK_OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (sk_lds_void*)(sw + (w * 2 + j) * 8 * SK_BK), 16, off, 0, 0,
+                                                 0);
+      }
     }
 #pragma unroll
     for (int j = 0; j < XG; ++j) {
@@ -181,9 +218,16 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
       stage(nb, kt + G::STAGES - 1);
     }
     const bf16_t* sw = sk_smem + buf * G::STAGE_ELEMS;
-    const bf16_t* sx = sw + SK_BN * SK_BK;
-    const bf16x8s w0 = *reinterpret_cast<const bf16x8s*>(sw + sk_swz(fr, ch));
-    const bf16x8s w1 = *reinterpret_cast<const bf16x8s*>(sw + sk_swz(32 + fr, ch));
+    const bf16_t* sx = sw + G::W_ELEMS;
+    bf16x8s w0, w1;
+    if constexpr (F8) {
+      const char* swb = reinterpret_cast<const char*>(sw);
+      w0 = sk_fp8x8(reinterpret_cast<const bf16_t*>(swb + sk_f8_off(fr, ch)));
+      w1 = sk_fp8x8(reinterpret_cast<const bf16_t*>(swb + sk_f8_off(32 + fr, ch)));
+    } else {
+      w0 = *reinterpret_cast<const bf16x8s*>(sw + sk_swz(fr, ch));
+      w1 = *reinterpret_cast<const bf16x8s*>(sw + sk_swz(32 + fr, ch));
+    }
 #pragma unroll
     for (int j = 0; j < XG; ++j) {
       const bf16x8s xf = *reinterpret_cast<const bf16x8s*>(sx + sk_swz(32 * j + fr, ch));
@@ -234,6 +278,7 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
     float v = 0.f;
 #pragma unroll
     for (int q = 0; q < SK_WAVES; ++q) v += red[(q * SK_BN + nl) * RP + m];
+    if constexpr (F8) v *= (n0 + nl < p.N) ? p.w_scale[n0 + nl] : 0.f;
     if constexpr (RMS) {
       if (KG == 1) v *= rstd_s[m];
     }
@@ -258,11 +303,39 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
   }
 }
 
+// fp8 (e4m3) rows x per-row scale -> bf16 (prefill-shaped problems run the bf16 GEMMs on it)
+__global__ void __launch_bounds__(256) dequant_fp8_rows_kernel(const uint8_t* __restrict__ w8,
+                                                               const float* __restrict__ scale,
+                                                               bf16_t* __restrict__ out, long total8, int K8) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total8; i += (long)gridDim.x * blockDim.x) {
+    const float sc = scale[i / K8];
+    const uint2_ v = reinterpret_cast<const uint2_*>(w8)[i];
+    float f[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)v[h], false);
+      const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)v[h], true);
+      f[4 * h + 0] = lo[0] * sc;
+      f[4 * h + 1] = lo[1] * sc;
+      f[4 * h + 2] = hi[0] * sc;
+      f[4 * h + 3] = hi[1] * sc;
+    }
+    reinterpret_cast<uint4_*>(out)[i] = pack8(f);
+  }
+}
+
+void launch_dequant_fp8_rows(const uint8_t* w8, const float* scale, bf16_t* out, long N, int K, hipStream_t s) {
+  const long total8 = N * (long)K / 8;
+  long blocks = (total8 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  dequant_fp8_rows_kernel<<<(int)blocks, 256, 0, s>>>(w8, scale, out, total8, K / 8);
+}
+
 // ---------------------------------------------------------------------------- host side
 bool skinny_supported(const GemmArgs& a) {
   return !a.conv && (a.batch <= 1) && a.M >= 1 && a.M <= 64 && a.K % 8 == 0 && a.N % 2 == 0 &&
          a.bias2d == nullptr && a.gate == nullptr && a.in_scale == nullptr && (a.lda % 8) == 0 &&
-         (a.ldw % 8) == 0 && (long)a.N * a.ldw * 2 < 0x7fffffffL;
+         (a.ldw % (a.w_scale ? 16 : 8)) == 0 && (long)a.N * a.ldw * 2 < 0x7fffffffL;
 }
 
 // K groups: enough workgroups for ~2 per CU, each group >= 2 pipeline depths of K steps.
@@ -287,16 +360,16 @@ int skinny_max_kgroups(const GemmArgs& a) {
   return kg;
 }
 
-template <int MB>
+template <int MB, bool F8>
 static void launch_skinny_mb(const GemmArgs& a, float* ws, int kg, hipStream_t s) {
   const int ksteps = (a.K + SK_BK - 1) / SK_BK;
   const int kg_steps = (ksteps + kg - 1) / kg;
   dim3 grid((a.N + SK_BN - 1) / SK_BN, kg), block(SK_WAVES * 64);
-  const size_t lds = SkGeom<MB>::LDS;
-#define SK(G, A)                                                                         \
-  do {                                                                                   \
-    if (a.rms) skinny_gemm_kernel<MB, G, A, true><<<grid, block, lds, s>>>(a, ws, kg_steps);  \
-    else skinny_gemm_kernel<MB, G, A, false><<<grid, block, lds, s>>>(a, ws, kg_steps);       \
+  const size_t lds = SkGeom<MB, F8>::LDS;
+#define SK(G, A)                                                                                  \
+  do {                                                                                            \
+    if (a.rms) skinny_gemm_kernel<MB, G, A, true, F8><<<grid, block, lds, s>>>(a, ws, kg_steps);  \
+    else skinny_gemm_kernel<MB, G, A, false, F8><<<grid, block, lds, s>>>(a, ws, kg_steps);       \
   } while (0)
 #define SK_ACT(G)                                      \
   switch (a.act) {                                     \
@@ -321,8 +394,13 @@ void launch_skinny_kg(const GemmArgs& a, float* ws, int kg, hipStream_t s) {
   const int ksteps = (a.K + SK_BK - 1) / SK_BK;
   if (ws == nullptr || kg < 1) kg = 1;
   if (kg > ksteps) kg = ksteps;
-  if (a.M <= 32) launch_skinny_mb<32>(a, ws, kg, s);
-  else launch_skinny_mb<64>(a, ws, kg, s);
+  if (a.w_scale) {
+    if (a.M <= 32) launch_skinny_mb<32, true>(a, ws, kg, s);
+    else launch_skinny_mb<64, true>(a, ws, kg, s);
+  } else {
+    if (a.M <= 32) launch_skinny_mb<32, false>(a, ws, kg, s);
+    else launch_skinny_mb<64, false>(a, ws, kg, s);
+  }
   if (kg > 1) launch_splitk_epilogue(a, ws, kg, s);
 }
 

@@ -112,7 +112,10 @@ struct GemmArgs {
   // rstd[m] = rsqrt(mean_k A[m, k]^2 + rms_eps); the norm gain is pre-multiplied into W's columns.
   int rms;
   float rms_eps;
+  // fp8 weights (skinny kernel only): W is e4m3 [N, K] bytes, w_scale[n] fp32 per output row
+  const float* w_scale;
 };
+void launch_dequant_fp8_rows(const uint8_t* w8, const float* scale, bf16_t* out, long N, int K, hipStream_t s);
 void launch_gemm(const GemmArgs& a, hipStream_t s);       // v1: register-staged (supports fused GN gather)
 // v2: LDS-DMA staged, tile configs + split-K (ws: fp32 workspace of gemm2_workspace_bytes, may be null)
 void launch_gemm2(const GemmArgs& a, float* ws, hipStream_t s);

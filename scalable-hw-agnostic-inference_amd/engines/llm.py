@@ -187,7 +187,8 @@ class LLMEngine:
     def __init__(self, cfg: LlamaConfig, device="cuda", model_path: Optional[str] = None, seed: int = 0,
                  max_num_seqs: int = 64, max_model_len: int = 4096, num_kv_blocks: Optional[int] = None,
                  gpu_memory_utilization: float = 0.85, prefill_token_budget: int = 8192, use_graphs: bool = True,
-                 enable_prefix_caching: bool = True, prefill_chunk: Optional[int] = None):
+                 enable_prefix_caching: bool = True, prefill_chunk: Optional[int] = None,
+                 quantization: Optional[str] = None):
         from ..models.mllama import MllamaConfig, MllamaForConditionalGeneration
         from ..runtime import BlockManager
         self.mcfg = cfg if isinstance(cfg, MllamaConfig) else None
@@ -201,6 +202,14 @@ class LLMEngine:
         materialize(self.model, self.device, model_path, None, seed)
         self.model.fold_norms()  # before any graph capture (re-folded lazily after a later load)
         self.weights = self.model._shai_weights
+        # vLLM-style ``quantization: fp8``: fp8 e4m3 weights + per-row scales for every TP linear
+        # (after the norm fold, which rescales weight columns); decode GEMMs stream half the bytes
+        self.quantization = (quantization or "").lower() or None
+        if self.quantization == "fp8":
+            from ..parallel.layers import quantize_fp8_
+            quantize_fp8_(self.model)
+        elif self.quantization not in (None, "none", "bf16"):
+            raise ValueError(f"quantization={quantization!r}: supported: fp8 (weight-only e4m3) or none")
         self.max_num_seqs = max_num_seqs
         self.max_model_len = min(max_model_len, cfg.max_position_embeddings)
         self.max_blocks = (self.max_model_len + KV_BLOCK - 1) // KV_BLOCK
@@ -496,8 +505,9 @@ def bench_decode_throughput(args, rank, world):
     init_distributed(tp_size=world)
     cfg = LlamaConfig.mistral_7b()
     B, P, G = args.batch, args.prompt_len, args.gen_len
+    quant = getattr(args, "quantization", None)
     eng = LLMEngine(cfg, device=f"cuda:{torch.cuda.current_device()}", max_num_seqs=max(B, 1),
-                    max_model_len=P + G + 64, enable_prefix_caching=False)
+                    max_model_len=P + G + 64, enable_prefix_caching=False, quantization=quant)
     params = SamplingParams(temperature=0.7, top_k=50, top_p=0.9, max_tokens=G, ignore_eos=True)
     rng = np.random.default_rng(0)
     prompts = lambda: [rng.integers(10, cfg.vocab_size - 10, P).tolist() for _ in range(B)]
@@ -524,10 +534,12 @@ def bench_decode_throughput(args, rank, world):
         el = float(t.item())
     toks = B * G * args.steps
     return {
-        "metric": "Mistral-7B output tokens/sec (bf16, continuous batching)",
+        "metric": ("Mistral-7B output tokens/sec (fp8 e4m3 weights, bf16 activations, continuous batching)"
+                   if quant == "fp8" else "Mistral-7B output tokens/sec (bf16, continuous batching)"),
         "value": round(toks / el, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 2), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "bf16", "data": "synthetic prompts, random-init weights",
+        "scaling": "strong", "vs_baseline": None, "dtype": "fp8w-bf16a" if quant == "fp8" else "bf16",
+        "data": "synthetic prompts, random-init weights",
         "config": {"model": "mistralai/Mistral-7B-Instruct-v0.3 (architecture)", "global_batch": B,
                    "seq_len": P + G, "prompt_len": P, "gen_len": G, "parallelism": f"tp{world}"},
         "p50_ttft_ms": round(1000 * float(np.median(ttft)), 2), "p50_tpot_ms": round(1000 * float(np.median(tpot)), 3),

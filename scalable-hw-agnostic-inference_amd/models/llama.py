@@ -210,6 +210,8 @@ class LlamaForCausalLM(nn.Module):
         with ``rms_eps`` set: on the GPU the per-row 1/rms is computed from the activation tiles
         already streaming through the decode GEMM, so the two norm kernels per layer disappear."""
         def fold(lin_w, norm):
+            if lin_w.dtype == torch.float8_e4m3fn:
+                raise RuntimeError("fold_norms after fp8 quantisation: fold first, then quantize_fp8_")
             lin_w.copy_((lin_w.float() * norm.weight.float()[None, :]).to(lin_w.dtype))
             norm.weight.fill_(1.0)
         for layer in self.layers:

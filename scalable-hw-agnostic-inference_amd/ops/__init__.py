@@ -24,7 +24,7 @@ from .reference import (ACT_GELU, ACT_GELU_TANH, ACT_NONE, ACT_QUICK_GELU, ACT_R
 __all__ = [
     "rmsnorm", "layernorm", "groupnorm_stats", "groupnorm_apply", "groupnorm", "linear", "conv2d", "attention",
     "paged_attention", "decode_attention", "kv_write", "rope", "rope_pairs", "gated_act", "bias_act", "sched_step",
-    "softmax_", "embedding", "pack_conv_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
+    "softmax_", "embedding", "quantize_fp8_rows", "dequant_fp8", "pack_conv_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
     "ACT_GELU_TANH", "ACT_QUICK_GELU", "ACT_RELU", "decode_splits",
 ]
 
@@ -126,16 +126,46 @@ def groupnorm(x, gamma, beta, groups, eps, silu=False, x2=None):
 
 
 # ----------------------------------------------------------------------------- GEMM / conv
+FP8_E4M3_MAX = 448.0
+
+
+def quantize_fp8_rows(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-output-row symmetric fp8 (OCP e4m3) quantisation: w ~= w8 * scale[:, None].
+    One-time load transform (not a hot op): returns (w8 float8_e4m3fn [N, K], scale fp32 [N])."""
+    wf = w.float()
+    scale = (wf.abs().amax(dim=1) / FP8_E4M3_MAX).clamp(min=1e-12)
+    w8 = (wf / scale[:, None]).clamp(-FP8_E4M3_MAX, FP8_E4M3_MAX).to(torch.float8_e4m3fn)
+    return w8.contiguous(), scale.contiguous()
+
+
+def dequant_fp8(w8: torch.Tensor, scale: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+    """w8 * scale[:, None] -> bf16 (native kernel on the GPU)."""
+    if not w8.is_cuda:
+        return (w8.float() * scale.float()[:, None]).to(dtype)
+    out = torch.empty(w8.shape, dtype=torch.bfloat16, device=w8.device)
+    _K().dequant_fp8(w8, scale, out)
+    return out
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act=None,
            residual: Optional[torch.Tensor] = None, glu: bool = False, alpha: float = 1.0,
-           res_alpha: float = 1.0, rms_eps: Optional[float] = None) -> torch.Tensor:
+           res_alpha: float = 1.0, rms_eps: Optional[float] = None,
+           w_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = act(alpha * x @ w^T + bias) (+ res_alpha * residual).
 
     glu=True: ``w`` rows are interleaved (value_i, gate_i) pairs and the output
     has N/2 columns: value * act(gate) (SwiGLU / GEGLU fused in the epilogue).
     rms_eps: x is RMS-normalised first (unweighted: the norm gain must already be
     folded into w's columns); on the GPU this is fused into the decode GEMM.
+    w_scale: ``w`` is fp8 e4m3 with one fp32 scale per row (``quantize_fp8_rows``).  Decode-shaped
+    problems (<= 64 rows) stream the fp8 bytes through the skinny kernel (half the weight
+    traffic); larger ones dequantize to bf16 first and run the bf16 GEMMs.
     """
+    if w_scale is not None:
+        M = x.numel() // x.shape[-1]
+        if not _gpu(x) or M > 64 or x.shape[-1] % 16 != 0:
+            w = dequant_fp8(w, w_scale)
+            w_scale = None
     if not _gpu(x):
         if rms_eps is not None:
             x = ref.rmsnorm(x, None, rms_eps)[0]
@@ -151,7 +181,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     y = torch.empty(x2.shape[0], Nout, dtype=x.dtype, device=x.device)
     r2 = residual.reshape(-1, Nout) if residual is not None else None
     _K().gemm(x2, w, y, bias, None, 1, r2, float(alpha), float(res_alpha), act_id(act), bool(glu), None, 1, -1,
-              float(rms_eps) if rms_eps is not None else -1.0)
+              float(rms_eps) if rms_eps is not None else -1.0, w_scale)
     return y.view(*lead, Nout)
 
 

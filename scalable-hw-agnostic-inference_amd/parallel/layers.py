@@ -38,6 +38,19 @@ class _ShardLoadMixin:
     def _shard(self, name: str, full: torch.Tensor) -> torch.Tensor:
         raise NotImplementedError
 
+    # ---- fp8 weight-only quantisation (vLLM-style ``quantization: fp8``): the weight becomes
+    # OCP e4m3 [N, K] + an fp32 per-row ``weight_scale``; decode GEMMs stream half the bytes.
+    def quantize_fp8_(self) -> None:
+        if getattr(self, "weight_scale", None) is not None:
+            return
+        w8, scale = ops.quantize_fp8_rows(self.weight.data)
+        self.weight = nn.Parameter(w8, requires_grad=False)
+        self.register_buffer("weight_scale", scale)
+
+    @property
+    def w_scale(self):
+        return getattr(self, "weight_scale", None)
+
     def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
         for name, p in list(self._parameters.items()):
             k = prefix + name
@@ -62,7 +75,7 @@ class ColumnParallelLinear(_ShardLoadMixin, nn.Module):
         return full.narrow(0, self.tp_rank * self.out_local, self.out_local).contiguous()
 
     def forward(self, x, act=None, rms_eps=None):
-        y = ops.linear(x, self.weight, self.bias, act=act, rms_eps=rms_eps)
+        y = ops.linear(x, self.weight, self.bias, act=act, rms_eps=rms_eps, w_scale=self.w_scale)
         return comm.all_gather_last(y) if self.gather_output else y
 
 
@@ -87,8 +100,8 @@ class RowParallelLinear(_ShardLoadMixin, nn.Module):
         if not self.input_is_parallel and self.tp_size > 1:
             x = x.narrow(-1, self.tp_rank * self.in_local, self.in_local).contiguous()
         if self.tp_size == 1:
-            return ops.linear(x, self.weight, self.bias, residual=residual)
-        y = ops.linear(x, self.weight, None)
+            return ops.linear(x, self.weight, self.bias, residual=residual, w_scale=self.w_scale)
+        y = ops.linear(x, self.weight, None, w_scale=self.w_scale)
         comm.all_reduce(y)
         if self.bias is not None or residual is not None:
             y = ops.bias_act(y, self.bias, residual)
@@ -123,7 +136,7 @@ class QKVParallelLinear(_ShardLoadMixin, nn.Module):
         return torch.cat([qs, ks, vs], 0).contiguous()
 
     def forward(self, x, rms_eps=None):
-        return ops.linear(x, self.weight, self.bias, rms_eps=rms_eps)
+        return ops.linear(x, self.weight, self.bias, rms_eps=rms_eps, w_scale=self.w_scale)
 
 
 class GLUParallelLinear(_ShardLoadMixin, nn.Module):
@@ -143,7 +156,7 @@ class GLUParallelLinear(_ShardLoadMixin, nn.Module):
         return full.narrow(0, self.tp_rank * 2 * self.i_local, 2 * self.i_local).contiguous()
 
     def forward(self, x, rms_eps=None):
-        return ops.linear(x, self.weight, self.bias, act=self.act, glu=True, rms_eps=rms_eps)
+        return ops.linear(x, self.weight, self.bias, act=self.act, glu=True, rms_eps=rms_eps, w_scale=self.w_scale)
 
 
 class VocabParallelEmbedding(_ShardLoadMixin, nn.Module):
@@ -178,3 +191,18 @@ class ParallelLMHead(VocabParallelEmbedding):
         if self.tp_size > 1:
             y = comm.all_gather_last(y)
         return y[..., : self.vocab]
+
+
+FP8_LAYER_TYPES = (ColumnParallelLinear, RowParallelLinear, QKVParallelLinear, GLUParallelLinear)
+
+
+@torch.no_grad()
+def quantize_fp8_(model: nn.Module) -> int:
+    """Quantise every TP linear layer of ``model`` to fp8 weights in place (embeddings / LM head
+    stay bf16).  Call after any weight transform (e.g. RMSNorm gain folding).  Returns the count."""
+    n = 0
+    for m in model.modules():
+        if isinstance(m, FP8_LAYER_TYPES):
+            m.quantize_fp8_()
+            n += 1
+    return n

@@ -11,7 +11,8 @@ Sampling defaults follow the reference (temperature 0.7, top-k 50, top-p 0.9,
 app/vllm_model_api.py:24).  Unlike vllm_model_api.py:38-43, ``max_new_tokens``
 is honoured (the _m variant's behaviour).  Engine kwargs can come from a
 /vllm_config.yaml-style file (``VLLM_CONFIG``): tensor_parallel_size,
-max_num_seqs, max_model_len, block_size (rounded to 64-token KV blocks).
+max_num_seqs, max_model_len, block_size (rounded to 64-token KV blocks),
+quantization (``fp8``: e4m3 weights + per-row scales, bf16 activations).
 
 ``image``: with a Llama-3.2-Vision model (``MODEL_ID`` containing "vision", or a
 local checkpoint with a ``vision_config``) the image goes through the native
@@ -46,7 +47,7 @@ def build_service(env: ServerEnv):
     eng = LLMEngine(cfg, device=env.torch_device, model_path=env.model_path,
                     max_num_seqs=int(vc.get("max_num_seqs", 64)),
                     max_model_len=int(vc.get("max_model_len", min(8192, text.max_position_embeddings))),
-                    enable_prefix_caching=True)
+                    enable_prefix_caching=True, quantization=vc.get("quantization"))
     specials = {"<|begin_of_text|>": text.bos_token_id}
     if text is not cfg:
         specials["<|image|>"] = cfg.image_token_index

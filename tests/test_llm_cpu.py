@@ -112,3 +112,27 @@ def test_chunked_prefill_matches_and_interleaves():
     # decode of the short sequence advanced while the long prompt was still being prefilled
     assert lens[4] > lens[0]
     assert eng.stats["prefill_tokens"] >= 300
+
+
+def test_fp8_quantize_roundtrip_and_cpu_linear():
+    """quantize_fp8_rows / dequant_fp8 on the host; ops.linear with w_scale equals the bf16 GEMM on
+    the dequantised weight (the CPU path dequantises)."""
+    from shai_amd import ops
+    torch.manual_seed(0)
+    w = torch.randn(64, 128) * 0.1
+    w8, sc = ops.quantize_fp8_rows(w)
+    wd = ops.dequant_fp8(w8, sc)
+    assert w8.dtype == torch.float8_e4m3fn and wd.dtype == torch.bfloat16
+    assert ((wd.float() - w).norm() / w.norm()).item() < 0.05
+    x = torch.randn(3, 128).bfloat16()
+    torch.testing.assert_close(ops.linear(x, w8, w_scale=sc), ops.linear(x, wd))
+
+
+def test_fp8_engine_cpu_generates():
+    c = LlamaConfig.tiny()
+    eng = LLMEngine(c, device="cpu", max_num_seqs=2, max_model_len=128, enable_prefix_caching=False,
+                    quantization="fp8")
+    out = eng.generate([[1, 2, 3, 4]], SamplingParams(max_tokens=4, temperature=0.0, ignore_eos=True))[0].output
+    assert len(out) == 4
+    with pytest.raises(ValueError):
+        LLMEngine(c, device="cpu", max_num_seqs=2, max_model_len=128, quantization="int3")
