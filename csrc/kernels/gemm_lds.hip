@@ -452,8 +452,9 @@ static void launch_all(const GemmArgs& a, float* ws, int cfg, int splits, hipStr
 }
 
 void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStream_t s) {
-  if (cfg >= kNumCfgs) {  // pipelined 256x256 kernel (gemm_pipe.hip): 4-stage / 2-stage ring
-    launch_gemm3(a, ws, splits, cfg == kNumCfgs ? 4 : 2, s);
+  if (cfg >= kNumCfgs) {  // pipelined kernel (gemm_pipe.hip): 256x256 / 256x320 tile, 4- / 2-stage ring
+    const int v = cfg - kNumCfgs;
+    launch_gemm3(a, ws, splits, (v & 1) ? 2 : 4, s, v >= 2 ? 320 : 256);
     return;
   }
   if (!a.conv) {
@@ -483,10 +484,10 @@ void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipS
   }
 }
 
-int gemm2_num_cfgs() { return kNumCfgs + 2; }
+int gemm2_num_cfgs() { return kNumCfgs + 4; }
 
 bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
-  if (cfg >= kNumCfgs) return cfg < kNumCfgs + 2 && gemm3_supported(a);
+  if (cfg >= kNumCfgs) return cfg < kNumCfgs + 4 && gemm3_supported(a);
   if (a.in_scale != nullptr) return false;
   if (a.conv && a.A2 != nullptr && (a.Cin % 64 != 0 || a.Cin1 % 64 != 0)) return false;  // 64-wide K tiles
   return cfg >= 0 && cfg < kNumCfgs;
@@ -494,8 +495,9 @@ bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
 
 void gemm2_cfg_info(int cfg, int* bm, int* bn) {
   if (cfg >= kNumCfgs) {
-    *bm = cfg == kNumCfgs ? 4 : 2;  // pipelined v3 kernel: stages
-    *bn = -256;
+    const int v = cfg - kNumCfgs;
+    *bm = (v & 1) ? 2 : 4;  // pipelined v3 kernel: stages
+    *bn = v >= 2 ? -320 : -256;
     return;
   }
   *bm = kCfgs[cfg].bm;

@@ -126,7 +126,7 @@ int gemm2_num_cfgs();
 bool gemm2_cfg_supported(const GemmArgs& a, int cfg);
 // v3: pipelined 256x256 LDS-DMA GEMM / conv (gemm_pipe.hip); config index gemm2_num_cfgs() - 1
 bool gemm3_supported(const GemmArgs& a);
-void launch_gemm3(const GemmArgs& a, float* ws, int splits, int stages, hipStream_t s);
+void launch_gemm3(const GemmArgs& a, float* ws, int splits, int stages, hipStream_t s, int bn = 256);
 void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipStream_t s);
 // skinny (decode-shaped, M <= 64) streaming GEMM; ws: skinny_workspace_bytes (fp32 split-K partials)
 bool skinny_supported(const GemmArgs& a);

@@ -1,4 +1,5 @@
-"""Pipelined 256x256 GEMM / conv kernel (config 5, gemm_pipe.hip) vs fp32 PyTorch."""
+"""Pipelined GEMM / conv kernel (gemm_pipe.hip) vs fp32 PyTorch: configs 5 / 6 (256x256 tile, 4- / 2-stage
+ring) and 7 / 8 (256x320 tile: 128x80 per wave, the extra W rows staged by waves 0-3)."""
 import os
 import subprocess
 import sys
@@ -9,7 +10,7 @@ import torch
 from shai_amd import ops
 
 pytestmark = pytest.mark.gpu
-CFG = 5
+CFGS = [5, 7, 8]
 
 
 def _rel(a, b):
@@ -19,35 +20,38 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("M,N,K", [(4096, 4096, 4096), (300, 520, 200), (1000, 256, 96), (257, 1024, 2048),
                                    (65536, 320, 320)])
-def test_gemm3_plain_bias_residual(cuda, M, N, K):
+@pytest.mark.parametrize("cfg", CFGS)
+def test_gemm3_plain_bias_residual(cuda, M, N, K, cfg):
     torch.manual_seed(M)
     a = torch.randn(M, K, device=cuda).bfloat16()
     w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
     bias = torch.randn(N, device=cuda).bfloat16()
     r = torch.randn(M, N, device=cuda).bfloat16()
     out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
-    ops.gemm_into(a, w, out, bias, residual=r, force_cfg=CFG)
+    ops.gemm_into(a, w, out, bias, residual=r, force_cfg=cfg)
     assert _rel(out, a.float() @ w.float().t() + bias.float() + r.float()) < 1e-2
 
 
 @pytest.mark.parametrize("act", ["gelu", "silu"])
-def test_gemm3_glu(cuda, act):
+@pytest.mark.parametrize("cfg", CFGS)
+def test_gemm3_glu(cuda, act, cfg):
     M, N, K = 2048, 2560, 320
     a = torch.randn(M, K, device=cuda).bfloat16()
     w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
     out = torch.empty(M, N // 2, device=cuda, dtype=torch.bfloat16)
-    ops.gemm_into(a, w, out, act=act, glu=True, force_cfg=CFG)
+    ops.gemm_into(a, w, out, act=act, glu=True, force_cfg=cfg)
     y = a.float() @ w.float().t()
     f = torch.nn.functional.gelu if act == "gelu" else torch.nn.functional.silu
     assert _rel(out, y[:, 0::2] * f(y[:, 1::2])) < 1e-2
 
 
-def test_gemm3_batched_strided(cuda):
+@pytest.mark.parametrize("cfg", CFGS)
+def test_gemm3_batched_strided(cuda, cfg):
     B, M, N, K = 3, 300, 384, 256
     a = torch.randn(B, M, K, device=cuda).bfloat16()
     w = torch.randn(N, K, device=cuda).bfloat16()
     j = torch.zeros(B, M + 40, N, device=cuda).bfloat16()
-    ops.gemm_into(a, w, j[:, 40:], force_cfg=CFG)
+    ops.gemm_into(a, w, j[:, 40:], force_cfg=cfg)
     assert _rel(j[:, 40:], a.float() @ w.float().t()) < 1e-2 and j[:, :40].abs().sum().item() == 0
 
 
@@ -59,7 +63,8 @@ from shai_amd.ops import reference as ref
 torch.manual_seed(0)
 cases = [(2, 32, 32, 64, 128, 3, 1, 1, False, 0), (2, 16, 16, 320, 320, 3, 1, 1, False, 0),
          (1, 16, 16, 64, 96, 3, 2, 1, False, 0), (2, 8, 8, 128, 64, 3, 1, 1, True, 0),
-         (2, 16, 16, 96, 64, 3, 1, 1, False, 64), (2, 16, 16, 64, 64, 1, 1, 0, False, 0)]
+         (2, 16, 16, 96, 64, 3, 1, 1, False, 64), (2, 16, 16, 64, 64, 1, 1, 0, False, 0),
+         (2, 32, 32, 320, 640, 3, 1, 1, False, 320)]
 worst = 0.0
 for N, H, C, Co, k, stride, pad, up, c2 in [(c[0], c[1], c[3], c[4], c[5], c[6], c[7], c[8], c[9]) for c in cases]:
     x = torch.randn(N, H, H, C, device="cuda").bfloat16()
@@ -77,9 +82,10 @@ assert worst < 2e-2, worst
 """
 
 
-def test_gemm3_conv_forced(cuda):
+@pytest.mark.parametrize("cfg", CFGS)
+def test_gemm3_conv_forced(cuda, cfg):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, SHAI_GEMM_FORCE=str(CFG))
+    env = dict(os.environ, SHAI_GEMM_FORCE=str(cfg))
     r = subprocess.run([sys.executable, "-c", CONV_SCRIPT.format(root=root)], env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]

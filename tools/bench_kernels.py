@@ -80,6 +80,44 @@ def bench_decode(rows):
                              skinny_TBps=gb / res[1000] / 1e3, torch_TBps=gb / t_t / 1e3))
 
 
+def bench_decode_fp8(rows):
+    """Decode GEMMs at M = 1 / 32 / 64: skinny kernel with bf16 vs fp8-e4m3 weights, per K-group
+    count, as time and achieved weight bandwidth (bf16-equivalent bytes / time for fp8)."""
+    for M in (1, 32, 64):
+        for N, K in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]:
+            ncopy = max(2, min(16, (768 << 20) // (N * K * 2) + 1))
+            a = rnd(M, K)
+            wb = [rnd(N, K) * 0.02 for _ in range(ncopy)]
+            w8 = [ops.quantize_fp8_rows(w) for w in wb]
+            out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            it = [0]
+
+            def nxt(lst):
+                it[0] = (it[0] + 1) % ncopy
+                return lst[it[0]]
+            best = {}
+            for name in ("bf16", "fp8"):
+                for kg in (1, 2, 4, 8, 16):
+                    if name == "bf16":
+                        f = lambda: ops.gemm_into(a, nxt(wb), out, force_cfg=1000 + kg)
+                    else:
+                        def f():
+                            w, sc = nxt(w8)
+                            torch.ops.shai.gemm(a, w, out, None, None, 1, None, 1.0, 1.0, 0, False, None, 1,
+                                                1000 + kg, -1.0, sc)
+                    try:
+                        t = timeit(f, iters=48)
+                    except Exception:  # noqa
+                        continue
+                    if name not in best or t < best[name][0]:
+                        best[name] = (t, kg)
+            del wb, w8
+            gb = N * K * 2 / 1e9
+            rows.append(dict(op="decode_fp8", shape=f"{M}x{N}x{K}", bf16_us=best["bf16"][0] * 1e6,
+                             bf16_kg=best["bf16"][1], fp8_us=best["fp8"][0] * 1e6, fp8_kg=best["fp8"][1],
+                             bf16_TBps=gb / best["bf16"][0] / 1e3, fp8_eqTBps=gb / best["fp8"][0] / 1e3))
+
+
 def bench_sdgemm(rows):
     """SD2.1 batch-8 (CFG 16) transformer GEMMs: every tile config (forced) vs the tuned choice vs hipBLASLt."""
     shapes = [("sq4096", 4096, 4096, 4096, False), ("sq8192", 8192, 8192, 8192, False),
@@ -158,7 +196,7 @@ def main():
     with torch.inference_mode():
         for name in a.only.split(","):
             {"gemm": bench_gemm, "conv": bench_conv, "attn": bench_attn, "norm": bench_norm,
-             "decode": bench_decode, "sdgemm": bench_sdgemm}[name](rows)
+             "decode": bench_decode, "decode_fp8": bench_decode_fp8, "sdgemm": bench_sdgemm}[name](rows)
     for r in rows:
         print("  ".join(f"{k}={v:.1f}" if isinstance(v, float) else f"{k}={v}" for k, v in r.items()), flush=True)
     if a.json:
