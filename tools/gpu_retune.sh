@@ -1,10 +1,11 @@
-# Fresh autotune over the bench workloads, starting from gpurun_out/tune_sd_b32.json (a fresh SD2.1 b32 tune);
+# Autotune the bench workloads' shapes missing from config/gemm_tuning_mi355x.json;
 # result gpurun_out/gemm_tuning_mi355x.json (merge over config/ afterwards with tools/merge_tuning.py).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-cp gpurun_out/tune_sd_b32.json gpurun_out/gemm_tuning_mi355x.json
+# NOTE: gpurun_out/ is not shipped to the box: start from the committed config instead
+cp config/gemm_tuning_mi355x.json gpurun_out/gemm_tuning_mi355x.json
 export SHAI_GEMM_TUNE_FILE=gpurun_out/gemm_tuning_mi355x.json SHAI_GEMM_TUNE_SAVE=gpurun_out/gemm_tuning_mi355x.json
 for spec in "sd21:--workload sd21 --batch 16 --steps 1 --warmup 1 --latency-runs 1" \
             "flux:--workload flux --steps 1 --warmup 1 --latency-runs 1" \
