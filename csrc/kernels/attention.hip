@@ -272,17 +272,26 @@ void launch_flash_attn(const AttnArgs& a, hipStream_t s) {
 // Paged decode attention (one query token per sequence).
 // grid (B, Hkv, splits); block = G waves (G = Hq/Hkv <= 8), wave w = head hk*G+w.
 // ----------------------------------------------------------------------------
-template <int D>
+typedef __attribute__((address_space(3))) void da_lds_void;
+
+// Decode attention, one workgroup per (sequence, KV head, split): G = Hq/Hkv waves, one query head
+// each.  The 64-token K/V blocks stream global -> LDS by LDS-DMA (buffer_load ... lds) into a
+// two-slot ring: block i+1's DMA is in flight while block i is consumed (counted vmcnt of NI
+// instructions per wave per block + one barrier), so HBM latency hides behind the dot products.
+// Per-block buffer descriptors (the cache can exceed 4 GiB) range-check the tail rows past the
+// context: zero-filled, since P = 0 times a never-written NaN pattern would poison P.V.
+template <int D, int NI>
 __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
   constexpr int CPR = D / 8;
+  constexpr int RPI = 1024 / (D * 2);           // K/V rows per 1-KB wave DMA instruction
+  constexpr int SLOT = 2 * 64 * D;              // bf16 elements per ring slot (K then V)
   extern __shared__ __attribute__((aligned(16))) char dsm[];
-  bf16_t* sK = reinterpret_cast<bf16_t*>(dsm);           // [64][D] swizzled
-  bf16_t* sV = sK + 64 * D;                              // [64][D] linear
-  float* sQ = reinterpret_cast<float*>(sV + 64 * D);     // [G][D]
-  float* sP = sQ + 8 * D;                                // [G][64]
+  bf16_t* ring = reinterpret_cast<bf16_t*>(dsm);              // [2][K 64xD swizzled | V 64xD linear]
+  float* sQ = reinterpret_cast<float*>(ring + 2 * SLOT);      // [G][D]
+  float* sP = sQ + 8 * D;                                     // [G][64]
   const int G = p.Hq / p.Hkv;
-  const int nthr = G * 64;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x, hk = blockIdx.y, split = blockIdx.z;
   const int hq = hk * G + w;
   const int ctx = p.ctx_lens[b];
@@ -290,26 +299,57 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
   const int per = (nblk + p.num_splits - 1) / p.num_splits;
   const int blk0 = split * per, blk1 = min(nblk, blk0 + per);
 
+  // wave w issues instructions j = w + G*t (t < NI) of the block's 2 * 64 * D * 2 / 1024 = NI * G
+  // physical block ids of this split, 64 per lane-distributed chunk (read ahead, so the ring's
+  // DMA issue never waits on a block-table load queued behind the previous block's DMA)
+  const int* bt = p.block_table + (long)b * p.max_blocks;
+  int chunk0 = blk0;
+  int my_phys = (blk0 + lane < blk1) ? bt[blk0 + lane] : 0;
+  auto phys_of = [&](int bi) {
+    if (bi - chunk0 >= 64) {
+      chunk0 += 64;
+      my_phys = (chunk0 + lane < blk1) ? bt[chunk0 + lane] : 0;
+    }
+    return __builtin_amdgcn_readfirstlane(__shfl(my_phys, bi - chunk0, 64));
+  };
+  auto stage = [&](int slot, int bi) {
+    const int phys = phys_of(bi);
+    const long base = ((long)phys * p.Hkv + hk) * 64 * D;
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.k_cache + base),
+                                                                        (short)0, 64 * D * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p.v_cache + base),
+                                                                        (short)0, 64 * D * 2, 0x00020000);
+    bf16_t* dst = ring + slot * SLOT;
+#pragma unroll
+    for (int t = 0; t < NI; ++t) {
+      const int j = w + G * t;                  // 0 .. 64*D*2*2/1024 - 1
+      const bool isv = j >= NI * G / 2;
+      const int jj = isv ? j - NI * G / 2 : j;
+      const int row = jj * RPI + lane / CPR;    // this lane's row and LDS chunk position
+      const int pos = lane % CPR;
+      const int ch = isv ? pos : (pos ^ (row & (CPR - 1)));  // K: source-side XOR swizzle
+      const uint32_t off = (bi * 64 + row < ctx) ? (uint32_t)((row * D + ch * 8) * 2) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(isv ? rv : rk, (da_lds_void*)(dst + (isv ? 64 * D : 0) + jj * 512),
+                                               16, off, 0, 0, 0);
+    }
+  };
+
   for (int i = lane; i < D; i += 64) sQ[w * D + i] = bf2f(p.q[(long)b * p.q_bs + (long)hq * D + i]) * p.scale * kLog2e;
   float m_run = -INFINITY, l_run = 0.f;
-  float o0 = 0.f, o1 = 0.f;  // this lane's d = lane, lane + 64 (D=128) or d = lane (D=64)
-  __syncthreads();
-  for (int bi = blk0; bi < blk1; ++bi) {
-    const int phys = p.block_table[(long)b * p.max_blocks + bi];
-    const bf16_t* kc = p.k_cache + ((long)phys * p.Hkv + hk) * 64 * D;
-    const bf16_t* vc = p.v_cache + ((long)phys * p.Hkv + hk) * 64 * D;
-    for (int id = tid; id < 64 * CPR; id += nthr) {
-      const int row = id / CPR, ch = id % CPR;
-      // rows past the context are never-written cache memory: zero them, since P = 0 times a
-      // NaN bit pattern would still poison the P.V sum
-      const bool ok = bi * 64 + row < ctx;
-      const uint4_ zero = {0u, 0u, 0u, 0u};
-      const uint4_ kv = ok ? *reinterpret_cast<const uint4_*>(kc + row * D + ch * 8) : zero;
-      const uint4_ vv = ok ? *reinterpret_cast<const uint4_*>(vc + row * D + ch * 8) : zero;
-      *reinterpret_cast<uint4_*>(sK + row * D + ((ch ^ (row & (CPR - 1))) << 3)) = kv;
-      *reinterpret_cast<uint4_*>(sV + row * D + ch * 8) = vv;
+  float o0 = 0.f, o1 = 0.f;  // D=128: this lane's d = 2 lane, 2 lane + 1; D=64: d = lane
+  if (blk0 < blk1) stage(0, blk0);
+  // (no barrier here: each wave reads only its own sQ row; the loop's barrier publishes the ring)
+  for (int bi = blk0, slot = 0; bi < blk1; ++bi, slot ^= 1) {
+    if (bi + 1 < blk1) {
+      stage(slot ^ 1, bi + 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");  // block bi landed, bi+1 in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
+    // raw barrier: __syncthreads' fence would drain the ring (vmcnt(0)) and serialise the prefetch
+    __builtin_amdgcn_s_barrier();
+    const bf16_t* sK = ring + slot * SLOT;
+    const bf16_t* sV = sK + 64 * D;
     // lane = key
     const int key = bi * 64 + lane;
     float sc = 0.f;
@@ -332,13 +372,32 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
     sP[w * 64 + lane] = e;
     o0 *= alpha;
     o1 *= alpha;
-    __syncthreads();  // sP visible (same wave, but keeps K/V reuse simple)
-    for (int k = 0; k < 64; ++k) {
-      const float pk = sP[w * 64 + k];
-      o0 += pk * bf2f(sV[k * D + lane]);
-      if (D == 128) o1 += pk * bf2f(sV[k * D + 64 + lane]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's sP row is written before it is read
+#pragma unroll 4
+    for (int k = 0; k < 64; k += 4) {
+      const float4_ pk = *reinterpret_cast<const float4_*>(sP + w * 64 + k);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if constexpr (D == 128) {
+          const uint32_t vv = *reinterpret_cast<const uint32_t*>(sV + (k + u) * D + 2 * lane);
+          o0 += pk[u] * bf2f(vv & 0xffff);
+          o1 += pk[u] * bf2f(vv >> 16);
+        } else {
+          o0 += pk[u] * bf2f(sV[(k + u) * D + lane]);
+        }
+      }
     }
-    __syncthreads();
+    __builtin_amdgcn_s_barrier();  // every wave is done with this slot before it is refilled (block bi+2)
+  }
+  if (p.num_splits == 1) {  // no split-K: normalise and write the output here (no combine launch)
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    bf16_t* op = p.o + (long)b * p.o_bs + (long)hq * D;
+    if constexpr (D == 128) {
+      *reinterpret_cast<uint32_t*>(op + 2 * lane) = pack2(o0 * inv, o1 * inv);
+    } else {
+      op[lane] = f2bf(o0 * inv);
+    }
+    return;
   }
   // partial results: ws[b][hq][split] = {m, l, o[D]}
   float* dst = p.ws + (((long)b * p.Hq + hq) * p.num_splits + split) * (D + 2);
@@ -346,8 +405,12 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
     dst[0] = m_run;
     dst[1] = l_run;
   }
-  dst[2 + lane] = o0;
-  if (D == 128) dst[2 + 64 + lane] = o1;
+  if constexpr (D == 128) {
+    dst[2 + 2 * lane] = o0;
+    dst[3 + 2 * lane] = o1;
+  } else {
+    dst[2 + lane] = o0;
+  }
 }
 
 __global__ void decode_combine_kernel(const DecodeAttnArgs p) {
@@ -379,10 +442,26 @@ size_t decode_attn_workspace(int B, int Hq, int D, int num_splits) {
 void launch_decode_attn(const DecodeAttnArgs& a, hipStream_t s) {
   const int G = a.Hq / a.Hkv;
   dim3 grid(a.B, a.Hkv, a.num_splits);
-  const size_t lds = (size_t)2 * 64 * a.D * sizeof(bf16_t) + (size_t)8 * a.D * 4 + 8 * 64 * 4;
-  if (a.D == 128) decode_attn_kernel<128><<<grid, G * 64, lds, s>>>(a);
-  else decode_attn_kernel<64><<<grid, G * 64, lds, s>>>(a);
-  decode_combine_kernel<<<dim3(a.B, a.Hq), 128, 0, s>>>(a);
+  const size_t lds = (size_t)4 * 64 * a.D * sizeof(bf16_t) + (size_t)8 * a.D * 4 + 8 * 64 * 4;
+  // NI = wave DMA instructions per block per wave = (2 * 64 * D * 2 / 1024) / G
+#define DA(D_, NI_) decode_attn_kernel<D_, NI_><<<grid, G * 64, lds, s>>>(a)
+  if (a.D == 128) {
+    switch (G) {
+      case 1: DA(128, 32); break;
+      case 2: DA(128, 16); break;
+      case 4: DA(128, 8); break;
+      default: DA(128, 4); break;  // G = 8
+    }
+  } else {
+    switch (G) {
+      case 1: DA(64, 16); break;
+      case 2: DA(64, 8); break;
+      case 4: DA(64, 4); break;
+      default: DA(64, 2); break;
+    }
+  }
+#undef DA
+  if (a.num_splits > 1) decode_combine_kernel<<<dim3(a.B, a.Hq), 128, 0, s>>>(a);
 }
 
 // ----------------------------------------------------------------------------

@@ -205,12 +205,15 @@ def _paged_setup(B, Hkv, D, ctx, nblocks=64):
     return kc, vc, bt
 
 
-@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (64, 8, 8), (128, 64, 8)])
-def test_decode_attn(cuda, D, Hq, Hkv):
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (64, 8, 8), (128, 64, 8), (128, 16, 8), (64, 16, 4)])
+@pytest.mark.parametrize("long_ctx", [False, True])
+def test_decode_attn(cuda, D, Hq, Hkv, long_ctx):
+    """Paged decode attention (LDS-DMA two-slot ring per 64-token block); long_ctx puts > 64 blocks
+    in one split (block-id read-ahead reloads its 64-entry chunk)."""
     torch.manual_seed(12)
-    ctx = [1, 64, 300, 1000]
+    ctx = [1, 64, 300, 1000] + ([4100, 5000] if long_ctx else [])
     B = len(ctx)
-    kc, vc, bt = _paged_setup(B, Hkv, D, ctx)
+    kc, vc, bt = _paged_setup(B, Hkv, D, ctx, nblocks=sum((c + 63) // 64 for c in ctx) + 8)
     q = rnd(B, Hq, D)
     lens = torch.tensor(ctx, dtype=torch.int32, device="cuda")
     for splits in (1, 3):
