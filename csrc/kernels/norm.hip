@@ -100,8 +100,117 @@ __global__ void __launch_bounds__(256) row_norm_kernel(
   }
 }
 
+// Narrow rows (D <= 512, D % 64 == 0; e.g. the SD2.1 UNet's C = 320 LayerNorms over 262k rows):
+// one wave row-per-wave left 24 of 64 lanes idle at D = 320 and paid a 6-step wave reduction per
+// 640-B row.  Here 8 lanes own a row (8 rows per wave): each lane holds NV = D / 64 16-byte
+// vectors (8-lane groups read 128 contiguous bytes per vector), reductions are 3 xor-shuffles.
+template <int NV, bool LAYERNORM>
+__global__ void __launch_bounds__(256) row_norm8_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ residual, const bf16_t* __restrict__ w,
+    const bf16_t* __restrict__ b, bf16_t* __restrict__ out, bf16_t* __restrict__ residual_out, int rows,
+    int D, long x_stride, long out_stride, float eps, float w_offset, int rows_per_w, long w_stride) {
+  const int lane = threadIdx.x & 63, sub = lane & 7;
+  const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (lane >> 3);
+  const bool live = row < rows;
+  const int r = live ? row : rows - 1;  // dead lanes mirror a real row (shuffles stay uniform)
+  if (rows_per_w > 0) {
+    const long wo = (long)(r / rows_per_w) * w_stride;
+    if (w) w += wo;
+    if (b) b += wo;
+  }
+  const bf16_t* xr = x + (long)r * x_stride;
+  uint4_ v[NV];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) v[c] = *reinterpret_cast<const uint4_*>(xr + (c * 8 + sub) * 8);
+  if (residual) {
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int col = (c * 8 + sub) * 8;
+      const uint4_ rr = *reinterpret_cast<const uint4_*>(residual + (long)r * D + col);
+      float f[8], g[8];
+      unpack8(v[c], f);
+      unpack8(rr, g);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] += g[i];
+      v[c] = pack8(f);
+      if (residual_out && live) *reinterpret_cast<uint4_*>(residual_out + (long)r * D + col) = v[c];
+    }
+  }
+  float sum = 0.f, sumsq = 0.f;
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    float f[8];
+    unpack8(v[c], f);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sum += f[i];
+      sumsq += f[i] * f[i];
+    }
+  }
+#pragma unroll
+  for (int m = 1; m < 8; m <<= 1) {
+    sum += __shfl_xor(sum, m, 64);
+    sumsq += __shfl_xor(sumsq, m, 64);
+  }
+  float mean = 0.f, rstd;
+  if (LAYERNORM) {
+    mean = sum / D;
+    float var = 0.f;  // second pass over the registers (two-pass variance, as the wave-per-row kernel)
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      float f[8];
+      unpack8(v[c], f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) var += (f[i] - mean) * (f[i] - mean);
+    }
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) var += __shfl_xor(var, m, 64);
+    rstd = rsqrtf(var / D + eps);
+  } else {
+    rstd = rsqrtf(sumsq / D + eps);
+  }
+  if (!live) return;
+  bf16_t* orow = out + (long)r * out_stride;
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int col = (c * 8 + sub) * 8;
+    float f[8], wf[8], bf[8];
+    unpack8(v[c], f);
+    if (w) unpack8(*reinterpret_cast<const uint4_*>(w + col), wf);
+    else
+#pragma unroll
+      for (int i = 0; i < 8; ++i) wf[i] = 1.f;
+    if (LAYERNORM && b) unpack8(*reinterpret_cast<const uint4_*>(b + col), bf);
+    else
+#pragma unroll
+      for (int i = 0; i < 8; ++i) bf[i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = (f[i] - mean) * rstd * (wf[i] + w_offset) + bf[i];
+    *reinterpret_cast<uint4_*>(orow + col) = pack8(f);
+  }
+}
+
 template <bool LN>
 static void launch_row_norm(const RowNormArgs& a, hipStream_t s) {
+  if (a.D % 64 == 0 && a.D <= 512 && a.x_stride % 8 == 0 && a.out_stride % 8 == 0 && a.rows > 0) {
+    dim3 grid((a.rows + 31) / 32), block(256);  // 4 waves x 8 rows
+#define SHAI_RN8(NV)                                                                                      \
+  row_norm8_kernel<NV, LN><<<grid, block, 0, s>>>(a.x, a.residual, a.w, a.b, a.out, a.residual_out, a.rows, \
+                                                  a.D, a.x_stride, a.out_stride, a.eps, a.w_offset,     \
+                                                  a.rows_per_w, a.w_stride)
+    switch (a.D / 64) {
+      case 1: SHAI_RN8(1); break;
+      case 2: SHAI_RN8(2); break;
+      case 3: SHAI_RN8(3); break;
+      case 4: SHAI_RN8(4); break;
+      case 5: SHAI_RN8(5); break;
+      case 6: SHAI_RN8(6); break;
+      case 7: SHAI_RN8(7); break;
+      default: SHAI_RN8(8); break;
+    }
+#undef SHAI_RN8
+    return;
+  }
   dim3 grid((a.rows + 3) / 4), block(256);
   const int chunks = (a.D + 511) / 512;
 #define SHAI_RN(C)                                                                                       \

@@ -40,12 +40,18 @@ def test_rmsnorm(cuda, D):
     close(y2, ref.rmsnorm(x, w, 1e-5)[0], 2e-2)
 
 
-@pytest.mark.parametrize("D", [64, 768, 1024, 3072])
+@pytest.mark.parametrize("D", [64, 192, 320, 512, 640, 768, 1024, 3072])
 def test_layernorm(cuda, D):
+    """D <= 512 (multiple of 64) runs the 8-rows-per-wave kernel; 129 rows leave a partial wave."""
     torch.manual_seed(1)
     x, w, b = rnd(129, D, scale=3.0) + 1.0, rnd(D), rnd(D)
     close(ops.layernorm(x, w, b, 1e-5)[0], ref.layernorm(x, w, b, 1e-5)[0], 2e-2)
     close(ops.layernorm(x, None, None, 1e-6)[0], ref.layernorm(x, None, None, 1e-6)[0], 2e-2)
+    r = rnd(129, D)
+    y, nr = ops.layernorm(x, w, b, 1e-5, residual=r)
+    yr, nrr = ref.layernorm(x, w, b, 1e-5, residual=r)
+    close(y, yr, 2e-2)
+    close(nr, nrr, 1e-2)
 
 
 @pytest.mark.parametrize("N,HW,C,G", [(2, 4096, 320, 32), (1, 256, 1280, 32), (2, 64, 2560, 32), (1, 16384, 128, 32),
