@@ -23,6 +23,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from . import new_graph
 from ..models.clip import CLIPTextConfig, CLIPTextModel
 from ..models.unet2d import UNet2DConditionModel, UNetConfig
 from ..models.vae import AutoencoderKLDecoder, VAEConfig
@@ -60,7 +61,7 @@ class _UNetGraph:
         self.lat = torch.zeros(B, h, w, unet.cfg.in_channels, dtype=torch.bfloat16, device=device)
         self.t = torch.zeros(1, dtype=torch.float32, device=device)
         self.kv = [torch.zeros(s, dtype=torch.bfloat16, device=device) for s in ctx_shapes]
-        self.graph = torch.cuda.CUDAGraph()
+        self.graph = new_graph(device)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):

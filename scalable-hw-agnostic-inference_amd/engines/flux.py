@@ -27,6 +27,7 @@ import torch
 
 from ..utils import profiling as prof
 from .. import ops
+from . import new_graph
 from ..models.clip import CLIPTextConfig, CLIPTextModel
 from ..models.flux import FluxConfig, FluxTransformer2DModel, pack_latents, unpack_latents_nhwc
 from ..models.t5 import T5Config, T5EncoderModel
@@ -77,7 +78,7 @@ class _StepGraph:
         self.ctx = torch.zeros(B, Nt, c.hidden, dtype=torch.bfloat16, device=device)
         self.mod = torch.zeros(B, model.mod_layout()[3], dtype=torch.bfloat16, device=device)
         self.cos, self.sin = model.rope(Nt, h2, w2, device)
-        self.graph = torch.cuda.CUDAGraph()
+        self.graph = new_graph(device)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):

@@ -33,6 +33,7 @@ import torch
 
 from ..utils import profiling as prof
 from .. import ops
+from . import new_graph
 from ..models.llama import (KV_BLOCK, Batch, LlamaConfig, LlamaForCausalLM, allocate_kv_cache, kv_bytes_per_block)
 from ..parallel.state import tp
 from ..weights import materialize
@@ -149,7 +150,7 @@ class _DecodeGraph:
                 for _ in range(2):
                     engine.model(self.batch, engine.kv)
             torch.cuda.current_stream().wait_stream(s)
-            self.graph = torch.cuda.CUDAGraph()
+            self.graph = new_graph(dev)
             with torch.cuda.graph(self.graph):
                 self.logits = engine.model(self.batch, engine.kv)
 

@@ -160,6 +160,10 @@ def test_conv2d_fused(cuda):
     (1, 128, 128, 32, 8, 128, True),
     (3, 197, 197, 12, 12, 64, False),
     (1, 1056, 1056, 3, 3, 128, False),
+    # d64 with Sq >= 512 runs the 64-queries-per-wave kernel (partial last workgroup, causal, GQA)
+    (2, 1030, 1030, 4, 2, 64, True),
+    (1, 600, 77, 5, 5, 64, False),
+    (2, 4096, 4096, 1, 1, 64, False),
 ])
 def test_flash_attn(cuda, B, Sq, Skv, Hq, Hkv, D, causal):
     torch.manual_seed(8)
@@ -188,13 +192,23 @@ def test_flash_attn_bias(cuda):
     close(ops.attention(q, k, v, scale=1.0, bias=bias), ref.attention(q, k, v, 1.0, bias=bias), 3e-2)
 
 
-def test_flash_attn_spike_forces_rescale(cuda):
+@pytest.mark.parametrize("S,D", [(256, 128), (700, 64)])
+def test_flash_attn_spike_forces_rescale(cuda, S, D):
     """A late key with a huge score forces the online-softmax rescale branch."""
     torch.manual_seed(11)
-    B, S, H, D = 1, 256, 2, 128
+    B, H = 1, 2
     q, k, v = rnd(B, S, H, D), rnd(B, S, H, D), rnd(B, S, H, D)
     k[:, 200] = q[:, 10] * 4
+    k[:, S - 3] = q[:, S - 40] * 4
     close(ops.attention(q, k, v), ref.attention(q, k, v, 1 / math.sqrt(D)), 2e-2)
+
+
+def test_flash_attn_bias_d64_long(cuda):
+    torch.manual_seed(12)
+    B, S, H, D = 1, 520, 2, 64
+    q, k, v = rnd(B, S, H, D), rnd(B, S, H, D), rnd(B, S, H, D)
+    bias = rnd(H, S, S, scale=2.0)
+    close(ops.attention(q, k, v, scale=1.0, bias=bias), ref.attention(q, k, v, 1.0, bias=bias), 3e-2)
 
 
 def _paged_setup(B, Hkv, D, ctx, nblocks=64):
