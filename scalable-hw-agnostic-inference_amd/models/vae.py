@@ -122,8 +122,36 @@ class AutoencoderKLDecoder(nn.Module):
         self.post_quant_conv = Conv2d(cfg.latent_channels, cfg.latent_channels, 1) if cfg.use_post_quant_conv else None
         self.decoder = Decoder(cfg)
 
+    # Largest operand the tuned (v2/v3) GEMM/conv kernels address with 32-bit offsets; bigger operands fall
+    # back to the register-staged v1 kernel (csrc/bindings.cpp use_v2), 2-4x slower on the full-res VAE convs.
+    OPERAND_LIMIT = (1 << 31) - (1 << 24)
+
+    def peak_bytes_per_image(self, h: int, w: int) -> int:
+        """Largest bf16 activation (bytes) one image produces in the decoder, latent h x w."""
+        rev = list(reversed(self.cfg.block_out_channels))
+        f, peak, prev = 1, rev[0], rev[0]
+        for i, c in enumerate(rev):
+            peak = max(peak, f * f * max(prev, c))
+            if i < len(rev) - 1:
+                f *= 2
+                peak = max(peak, f * f * c)
+            prev = c
+        return h * w * peak * 2
+
     def forward(self, latents: torch.Tensor) -> torch.Tensor:
-        """latents NHWC [B, h, w, C] (scaled) -> image NHWC [B, 8h, 8w, 3] in [-1, 1]."""
+        """latents NHWC [B, h, w, C] (scaled) -> image NHWC [B, 8h, 8w, 3] in [-1, 1].
+
+        Large batches decode in balanced chunks whose activations stay under OPERAND_LIMIT, so every
+        full-resolution conv runs on the tuned kernels (SD2.1 512^2: 11 images per chunk)."""
+        B = latents.shape[0]
+        per = max(1, self.OPERAND_LIMIT // self.peak_bytes_per_image(latents.shape[1], latents.shape[2]))
+        if latents.is_cuda and B > per:
+            n = -(-B // per)
+            step = -(-B // n)
+            return torch.cat([self._decode(latents[i:i + step]) for i in range(0, B, step)], 0)
+        return self._decode(latents)
+
+    def _decode(self, latents: torch.Tensor) -> torch.Tensor:
         lat = latents.contiguous()
         z = ops.bias_act(lat.view(-1, 8), None, None, None, alpha=1.0 / self.cfg.scaling_factor).view(lat.shape)
         if self.cfg.shift_factor:

@@ -48,3 +48,17 @@ def test_sd_engine_graph_matches_eager(cuda):
     e.use_graphs = False
     b = e.generate(["a cat", "a dog"], 4, seed=7, output="tensor")
     assert _rel(a, b) < 1e-3
+
+
+def test_vae_chunked_decode_matches_whole_batch(cuda):
+    """Batches whose activations exceed the 32-bit-offset kernels' operand limit decode in chunks."""
+    from shai_amd.models.layers import init_random_
+    from shai_amd.models.vae import AutoencoderKLDecoder, VAEConfig
+    vae = init_random_(AutoencoderKLDecoder(VAEConfig.tiny()), seed=6).cuda()
+    z = torch.randn(5, 8, 8, 4, device="cuda").to(torch.bfloat16)
+    with torch.no_grad():
+        whole = vae(z)
+        vae.OPERAND_LIMIT = 2 * vae.peak_bytes_per_image(8, 8)  # 2 images per chunk -> chunks of 2, 2, 1
+        chunked = vae(z)
+    assert chunked.shape == whole.shape
+    assert _rel(chunked, whole) < 1e-2
