@@ -33,11 +33,18 @@ MI355X design (not a translation of the reference's NxD wrappers):
   so the rank's concatenated [attn | mlp] activations feed a single GEMM (the
   reference splits it into two RowParallel layers and two all-reduces,
   app/src/transformer/model.py:303-322).
+* **Sequence parallelism (optional, ``FluxConfig.sequence_parallel`` / ``SHAI_FLUX_SP=1``)** -- the
+  reference disables SP (cova/mllama-32-11b-vllm-trn1-config.yaml:17) and runs Flux at TP8 only.  Here the
+  38 single-stream blocks can keep the joint residual stream split into S/n-row shards over the TP group:
+  LayerNorm-modulate and the gated residual run on S/n rows, an all-gather feeds the column-parallel
+  QKV / MLP GEMMs and proj_out's partial sums are reduce-scattered instead of all-reduced (same bytes on
+  xGMI as the all-reduce, 1/n of the norm / residual traffic and residual memory).
 """
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass
+import os
+from dataclasses import dataclass, field
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -65,6 +72,8 @@ class FluxConfig:
     guidance_embeds: bool = True
     axes_dims_rope: Tuple[int, int, int] = (16, 56, 56)
     rope_theta: float = 10000.0
+    # Megatron-style sequence parallelism over the TP group for the single-stream blocks (SHAI_FLUX_SP=1)
+    sequence_parallel: bool = field(default_factory=lambda: os.environ.get("SHAI_FLUX_SP", "0") == "1")
 
     @property
     def mlp_hidden(self) -> int:
@@ -155,6 +164,16 @@ def _gated_out(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], resi
         return
     y = ops.linear(x, w, None)
     comm.all_reduce(y)
+    yb = y.float() + (b.float() if b is not None else 0.0)
+    residual.add_((yb * gate.float().view(residual.shape[0], 1, -1)).to(residual.dtype))
+
+
+def _gated_out_sp(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], residual: torch.Tensor,
+                  gate: torch.Tensor) -> None:
+    """Sequence-parallel variant of :func:`_gated_out`: x is the full-sequence activation shard
+    [B, S, in_local], residual this rank's sequence rows [B, S/n, d]; the partial GEMM output is
+    reduce-scattered over the sequence, so the bias / gate / residual update touches S/n rows only."""
+    y = comm.reduce_scatter_seq(ops.linear(x, w, None))
     yb = y.float() + (b.float() if b is not None else 0.0)
     residual.add_((yb * gate.float().view(residual.shape[0], 1, -1)).to(residual.dtype))
 
@@ -261,21 +280,29 @@ class FluxSingleTransformerBlock(nn.Module):
         self.proj_mlp = ColumnParallelLinear(d, c.mlp_hidden)
         self.proj_out = _SingleProjOut(d, c.mlp_hidden)
 
-    def forward(self, x, mod, cos, sin):
-        """x [B, S, d] joint sequence, updated in place; mod [B, 3d]."""
+    def forward(self, x, mod, cos, sin, sp: bool = False):
+        """x [B, S, d] joint sequence, updated in place; mod [B, 3d].  sp: x holds only this rank's S/n
+        sequence rows (sequence parallel): the normalised rows are all-gathered before the column-parallel
+        QKV / MLP GEMMs and proj_out's partial sums are reduce-scattered back onto the local rows."""
         c = self.c
-        B, S, d = x.shape
+        B, s_loc, d = x.shape
         Hl = self.attn.qkv.h_local
         D = c.head_dim
         HD = Hl * D
-        xn = ops.layernorm_mod(x, mod[:, d:2 * d], mod[:, :d], S)
+        xn = ops.layernorm_mod(x, mod[:, d:2 * d], mod[:, :d], s_loc)
+        if sp:
+            xn = comm.all_gather_seq(xn)
+        S = xn.shape[1]
         qkv = ops.linear(xn, self.attn.qkv.weight, self.attn.qkv.bias)          # [B, S, 3HD]
         cat = torch.empty(B, S, HD + self.proj_mlp.out_local, dtype=x.dtype, device=x.device)
         ops.gemm_into(xn, self.proj_mlp.weight, cat[..., HD:], self.proj_mlp.bias, act="gelu_tanh")
         ops.qk_norm_rope(qkv.view(B * S, 3 * HD), self.attn.norm_q, self.attn.norm_k, cos, sin, Hl, D, S)
         ops.attention(qkv[..., :HD].view(B, S, Hl, D), qkv[..., HD:2 * HD].view(B, S, Hl, D),
                       qkv[..., 2 * HD:].view(B, S, Hl, D), out=cat[..., :HD].view(B, S, Hl, D))
-        _gated_out(cat, self.proj_out.weight, self.proj_out.bias, x, mod[:, 2 * d:], S)
+        if sp:
+            _gated_out_sp(cat, self.proj_out.weight, self.proj_out.bias, x, mod[:, 2 * d:])
+        else:
+            _gated_out(cat, self.proj_out.weight, self.proj_out.bias, x, mod[:, 2 * d:], S)
 
 
 class FluxTransformer2DModel(nn.Module):
@@ -343,8 +370,18 @@ class FluxTransformer2DModel(nn.Module):
         txt, img = joint[:, :Nt], joint[:, Nt:]
         for blk, (oi, ot) in zip(self.transformer_blocks, dual):
             blk(img, txt, mod[:, oi:oi + 6 * d], mod[:, ot:ot + 6 * d], cos, sin)
-        for blk, o in zip(self.single_transformer_blocks, single):
-            blk(joint, mod[:, o:o + 3 * d], cos, sin)
+        st = tp()
+        if self.cfg.sequence_parallel and st.size > 1 and (Nt + Ni) % st.size == 0:
+            # SP over the TP group: the joint residual stream is split into S/n-row shards for the single
+            # blocks (replicated after the dual blocks, so slicing needs no communication)
+            s = (Nt + Ni) // st.size
+            xs = joint[:, st.rank * s:(st.rank + 1) * s].contiguous()
+            for blk, o in zip(self.single_transformer_blocks, single):
+                blk(xs, mod[:, o:o + 3 * d], cos, sin, sp=True)
+            joint = comm.all_gather_seq(xs)
+        else:
+            for blk, o in zip(self.single_transformer_blocks, single):
+                blk(joint, mod[:, o:o + 3 * d], cos, sin)
         mo = mod[:, o_out:]
         x = ops.layernorm_mod(joint[:, Nt:], mo[:, :d], mo[:, d:], Ni)
         return self.proj_out(x)

@@ -3,7 +3,9 @@
 Issued on the current stream, so they are ordered with the surrounding kernels
 and capturable in HIP graphs.  Two transports:
 
-* RCCL (``torch.distributed`` backend "nccl" on ROCm) -- default for every size.
+* RCCL (``torch.distributed`` backend "nccl" on ROCm) -- default for every size;
+  also the sequence-parallel all-gather / reduce-scatter pair (:func:`all_gather_seq`,
+  :func:`reduce_scatter_seq`) used by the Flux single-stream blocks at SP > 1.
 * ``P2PAllReduce`` (``csrc/comm/p2p_allreduce.hip``) -- one-shot all-reduce for
   small, latency-bound messages (LLM decode: B x 4096 bf16 per layer), reading
   every peer's IPC-mapped buffer directly over xGMI in one kernel.  Enabled
@@ -57,6 +59,54 @@ def all_gather_last(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) 
     dist.all_gather_into_tensor(flat, x, group=g)   # rank-major concat along dim 0
     out = flat.view((n,) + tuple(x.shape))
     return out.movedim(0, -2).reshape(*x.shape[:-1], n * x.shape[-1])
+
+
+def _seq_major(x: torch.Tensor, n: int) -> torch.Tensor:
+    """[B, n*s, ...] -> rank-major contiguous [n, B, s, ...] (a view when B == 1)."""
+    B, S = x.shape[0], x.shape[1]
+    return x.reshape(B, n, S // n, *x.shape[2:]).transpose(0, 1).contiguous()   # no copy when B == 1
+
+
+def all_gather_seq(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """Sequence-parallel all-gather: local [B, s, ...] shards -> [B, n*s, ...] (rank r owns rows
+    [r*s, (r+1)*s)).  One all-gather of B*S*d elements; at B == 1 the rank-major result IS the output layout,
+    so no re-layout copy is made."""
+    st = tp()
+    g = group if group is not None else st.group
+    if st.size == 1 and group is None:
+        return x
+    n = st.size if group is None else dist.get_world_size(g)
+    x = x.contiguous()
+    B, s = x.shape[0], x.shape[1]
+    flat = torch.empty((n * B,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(flat, x, group=g)   # rank-major along dim 0
+    if B == 1:
+        return flat.view((1, n * s) + tuple(x.shape[2:]))
+    return flat.view((n,) + tuple(x.shape)).transpose(0, 1).reshape((B, n * s) + tuple(x.shape[2:]))
+
+
+def reduce_scatter_seq(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """Sequence-parallel reduce-scatter: partial sums [B, S, ...] -> this rank's reduced rows [B, S/n, ...].
+    Replaces the all-reduce after a RowParallel layer (same bytes on the wire as the all-gather that feeds
+    the next ColumnParallel layer; together they cost one all-reduce, but every norm / residual between
+    them touches only S/n rows).  gloo has no reduce-scatter: there it is all-reduce + slice."""
+    st = tp()
+    g = group if group is not None else st.group
+    if st.size == 1 and group is None:
+        return x
+    n = st.size if group is None else dist.get_world_size(g)
+    r = dist.get_rank(g)
+    B, S = x.shape[0], x.shape[1]
+    assert S % n == 0, f"sequence {S} not divisible by the SP degree {n}"
+    s = S // n
+    if dist.get_backend(g) == "gloo":
+        y = x.contiguous()
+        dist.all_reduce(y, group=g)
+        return y[:, r * s:(r + 1) * s].contiguous()
+    src = _seq_major(x, n)
+    out = torch.empty((B, s) + tuple(x.shape[2:]), dtype=x.dtype, device=x.device)
+    dist.reduce_scatter_tensor(out, src, group=g)
+    return out
 
 
 def broadcast_object(obj, src: int = 0):

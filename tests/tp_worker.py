@@ -65,17 +65,20 @@ def run(rank, world, port, which):
         m2 = T5EncoderModel(c)
         load_into(m2, dict(sd), strict=True)
         _close(m2(ids, mask), ref, 1e-2)
-    elif which == "flux":
+    elif which in ("flux", "flux_sp"):
+        # flux_sp: sequence-parallel single blocks (S/n-row residual shards, all-gather + reduce-scatter)
         from shai_amd.models.flux import FluxConfig, FluxTransformer2DModel
         c = FluxConfig.tiny()
+        c.sequence_parallel = which == "flux_sp"
+        B = 2 if c.sequence_parallel else 1
         _tp1()
         m1 = FluxTransformer2DModel(c)
         init_random_(m1, 5)
         sd = {k: v.clone() for k, v in m1.state_dict().items()}
-        lat = torch.randn(1, 24, c.in_channels).bfloat16()
-        t5 = torch.randn(1, 8, c.joint_attention_dim).bfloat16()
-        pooled = torch.randn(1, c.pooled_projection_dim).bfloat16()
-        t, g = torch.tensor([0.7]), torch.tensor([3.5])
+        lat = torch.randn(B, 24, c.in_channels).bfloat16()
+        t5 = torch.randn(B, 8, c.joint_attention_dim).bfloat16()
+        pooled = torch.randn(B, c.pooled_projection_dim).bfloat16()
+        t, g = torch.tensor([0.7] * B), torch.tensor([3.5] * B)
         with torch.no_grad():
             ref = m1(lat, t5, pooled, t, g, img_hw=(4, 6))
         init_distributed("gloo", tp_size=world)
@@ -83,6 +86,16 @@ def run(rank, world, port, which):
         load_into(m2, dict(sd), strict=True)
         with torch.no_grad():
             _close(m2(lat, t5, pooled, t, g, img_hw=(4, 6)), ref, 3e-2)
+    elif which == "seq_comm":
+        from shai_amd.parallel import comm
+        init_distributed("gloo", tp_size=world)
+        full = [torch.randn(3, 4 * world, 5, generator=torch.Generator().manual_seed(r)) for r in range(world)]
+        s = 4
+        got = comm.all_gather_seq(full[rank][:, rank * s:(rank + 1) * s])
+        want = torch.cat([full[r][:, r * s:(r + 1) * s] for r in range(world)], 1)
+        assert torch.equal(got, want)
+        rs = comm.reduce_scatter_seq(full[rank].clone())
+        assert torch.allclose(rs, sum(full)[:, rank * s:(rank + 1) * s], atol=1e-5)
     import torch.distributed as dist
     dist.barrier()
     dist.destroy_process_group()
