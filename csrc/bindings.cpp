@@ -62,6 +62,14 @@ bool autotune_enabled() {
   return on;
 }
 
+bool lib_enabled() {  // SHAI_GEMM_LIB=0 keeps every GEMM on the hand-written kernels
+  static const bool on = [] {
+    const char* e = getenv("SHAI_GEMM_LIB");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int max_splits_for(const shai::GemmArgs& g) {
   const int batch = g.batch > 0 ? g.batch : 1;
   if (batch != 1) return 1;
@@ -91,7 +99,44 @@ void launch_skinny_choice(const shai::GemmArgs& g, const Tensor& like, int kg) {
   shai::launch_skinny_kg(g, wsp, kg, stream());
 }
 
+// Choice.cfg of the library path: plain GEMMs (no fused epilogue beyond a bias or an unscaled residual) may
+// go to hipBLASLt through at::mm_out / at::addmm_out when the autotuner measures it faster than the tile
+// configs -- the hand-written kernels keep every fused-epilogue / conv / GLU / gated problem.
+constexpr int kLibCfg = 2000;
+
+bool lib_supported(const shai::GemmArgs& g) {
+  return g.conv == 0 && g.batch <= 1 && !g.glu && g.act == 0 && !g.bias2d && !g.gate && !g.rms && !g.w_scale &&
+         !g.A2 && !g.in_scale && g.alpha == 1.f && !(g.bias && g.residual) &&
+         (!g.residual || (g.res_alpha == 1.f && g.residual == g.C && g.ldr == g.ldc)) &&
+         g.lda >= g.K && g.ldw >= g.K && g.ldc >= g.N;
+}
+
+void launch_lib(const shai::GemmArgs& g, const Tensor& like) {
+  const auto opt = like.options().dtype(at::kBFloat16);
+  Tensor A = at::from_blob(const_cast<shai::bf16_t*>(g.A), {(long)g.M, (long)g.K}, {g.lda, 1L}, opt);
+  Tensor W = at::from_blob(const_cast<shai::bf16_t*>(g.W), {(long)g.N, (long)g.K}, {g.ldw, 1L}, opt);
+  Tensor C = at::from_blob(g.C, {(long)g.M, (long)g.N}, {g.ldc, 1L}, opt);
+  if (g.residual) {          // in place: C = C + A W^T (the residual IS the output buffer)
+    C.addmm_(A, W.t());
+  } else if (g.bias) {
+    Tensor b = at::from_blob(const_cast<shai::bf16_t*>(g.bias), {(long)g.N}, opt);
+    at::addmm_out(C, b, A, W.t());
+  } else {
+    at::mm_out(C, A, W.t());
+  }
+}
+
 void launch_choice(const shai::GemmArgs& g, const Tensor& like, Choice c) {
+  if (c.cfg == kLibCfg) {
+    if (lib_supported(g)) {
+      launch_lib(g, like);
+      return;
+    }
+    // the cache key does not encode the epilogue: a problem of the same shape with a fused epilogue
+    // falls back to the planner's tile config
+    shai::gemm2_plan(g, &c.cfg, &c.splits);
+    if (!shai::gemm2_cfg_supported(g, c.cfg)) c = Choice{shai::gemm2_num_cfgs() - 1, 1};
+  }
   if (c.cfg == kSkinnyCfg) {
     launch_skinny_choice(g, like, c.splits);
     return;
@@ -129,6 +174,9 @@ Choice tune(const shai::GemmArgs& g_real, const Tensor& like, bool skinny_only =
   }
   if (shai::skinny_supported(g))
     for (int kg = 1; kg <= shai::skinny_max_kgroups(g); kg *= 2) cands.push_back({kSkinnyCfg, kg});
+  // residual epilogues are in place (C aliases the residual): timing them into the scratch output is not
+  // equivalent, so only bias-or-nothing problems race the library
+  if (!skinny_only && lib_enabled() && lib_supported(g_real) && !g_real.residual) cands.push_back({kLibCfg, 1});
   hipStream_t st = stream();
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
@@ -220,6 +268,10 @@ std::vector<std::string> gemm_tuning_table() {
   for (auto& kv : g_tuned) {
     if (kv.second.cfg == kSkinnyCfg) {
       out.push_back(kv.first + " -> skinny kg=" + std::to_string(kv.second.splits));
+      continue;
+    }
+    if (kv.second.cfg == kLibCfg) {
+      out.push_back(kv.first + " -> hipblaslt");
       continue;
     }
     int bm, bn;
@@ -511,7 +563,7 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
   const long a_bytes = (batched ? (long)a.size(0) * a.stride(0) : (long)g.M * g.lda) * 2;
   // tests / tools bypass the tuner: force_cfg = gemm2 config, 1000 = skinny kernel (heuristic K groups),
   // 1000 + kg = skinny kernel with kg K groups
-  const bool force_skinny = force_cfg >= kSkinnyCfg;
+  const bool force_skinny = force_cfg >= kSkinnyCfg && force_cfg != kLibCfg;
   const int force_kg = force_cfg > kSkinnyCfg ? (int)(force_cfg - kSkinnyCfg) : shai::skinny_kgroups(g);
   if (rms_eps >= 0) {
     // RMSNorm(a) folded in (norm gain pre-multiplied into w): fused into the skinny kernel for
@@ -538,6 +590,11 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
     g.A = cptr(xn);
     g.lda = g.K;
     run_gemm(g, xn, (long)g.M * g.K * 2, (long)g.N * g.ldw * 2, 0);
+    return;
+  }
+  if (force_cfg == kLibCfg) {  // tests: pin the hipBLASLt path
+    SHAI_CHECK(lib_supported(g), "library GEMM path does not support this problem's epilogue");
+    launch_lib(g, a);
     return;
   }
   if (force_cfg >= 0) {
@@ -872,7 +929,8 @@ int64_t gemm_tuning_import(const std::vector<std::string>& entries) {
     if (eq == std::string::npos || cm == std::string::npos || cm < eq) continue;
     const int cfg = atoi(e.substr(eq + 1, cm - eq - 1).c_str());
     const int sp = atoi(e.substr(cm + 1).c_str());
-    if ((cfg < 0 || cfg >= shai::gemm2_num_cfgs()) && cfg != kSkinnyCfg) continue;
+    if ((cfg < 0 || cfg >= shai::gemm2_num_cfgs()) && cfg != kSkinnyCfg && cfg != kLibCfg) continue;
+    if (cfg == kLibCfg && !lib_enabled()) continue;
     if (sp < 1) continue;
     g_tuned[e.substr(0, eq)] = Choice{cfg, sp};
     ++n;

@@ -116,6 +116,31 @@ def test_gemm_glu(cuda, act):
     close(ops.linear(x, w, b, act=act, glu=True), ref.linear(x, w, b, act, glu=True), 2e-2)
 
 
+@pytest.mark.parametrize("case", ["plain", "bias", "residual_inplace", "strided_out"])
+def test_gemm_library_path(cuda, case):
+    """force_cfg=2000 pins the hipBLASLt candidate of the autotuner (plain / bias / in-place residual)."""
+    torch.manual_seed(6)
+    M, N, K = 1000, 640, 320
+    x, w, b = rnd(M, K), rnd(N, K, scale=1 / math.sqrt(K)), rnd(N)
+    if case == "plain":
+        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        close(ops.gemm_into(x, w, out, force_cfg=2000), ref.linear(x, w), 2e-2)
+    elif case == "bias":
+        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        close(ops.gemm_into(x, w, out, b, force_cfg=2000), ref.linear(x, w, b), 2e-2)
+    elif case == "residual_inplace":
+        r = rnd(M, N)
+        want = ref.linear(x, w, None, None, r)
+        close(ops.gemm_into(x, w, r, residual=r, force_cfg=2000), want, 2e-2)
+    else:
+        buf = torch.zeros(M, 2 * N, device="cuda", dtype=torch.bfloat16)
+        ops.gemm_into(x, w, buf[:, N:], b, force_cfg=2000)
+        close(buf[:, N:], ref.linear(x, w, b), 2e-2)
+        assert buf[:, :N].abs().sum().item() == 0
+    with pytest.raises(RuntimeError):
+        ops.gemm_into(x, w, torch.empty(M, N, device="cuda", dtype=torch.bfloat16), b, act="gelu", force_cfg=2000)
+
+
 def test_bmm(cuda):
     torch.manual_seed(5)
     a, w = rnd(3, 200, 64), rnd(3, 150, 64)
