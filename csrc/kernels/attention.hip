@@ -26,6 +26,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s4v __attribute__((ext_vector_type(4)));
 
 constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kRescaleThr = 8.f;   // flash_fwd deferred-max threshold (log2 units)
 
 template <int D>
 __device__ __forceinline__ int k_swz(int row, int ch) {
@@ -184,12 +185,16 @@ __global__ void __launch_bounds__(256, 2) flash_fwd_kernel(const AttnArgs p) {
       mloc = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
     }
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64)) * sl2;   // scale > 0: max commutes with scaling
-    const float m_new = fmaxf(m_run, mloc);
-    const float m_use = m_new == -INFINITY ? 0.f : m_new;
-    // Skip the O rescale when no row max grew in this tile (exact: alpha == 1).
-    const bool grew = __any(m_new > m_run);
+    // Deferred max: keep the running max (and skip the O rescale) unless some row's max grew by more
+    // than kRescaleThr (log2 units) -- P is then bounded by 2^kRescaleThr instead of 1, which the bf16 P /
+    // fp32 O, l accumulators absorb; the decision precedes this tile's exponentials, so everything still at
+    // the old max is rescaled exactly once.
+    const float m_cand = fmaxf(m_run, mloc);
+    const bool grew = __any(m_cand > m_run + kRescaleThr);
+    const float m_keep = grew ? m_cand : m_run;
+    const float m_use = m_keep == -INFINITY ? 0.f : m_keep;
     const float alpha = grew ? __builtin_amdgcn_exp2f(m_run - m_use) : 1.f;
-    m_run = m_new;
+    m_run = m_keep;
     float ls4[4] = {0.f, 0.f, 0.f, 0.f};  // independent partial row sums (ILP)
     bf16x8 pf[2][2];
 #pragma unroll
