@@ -47,11 +47,21 @@ struct Choice {
 std::mutex g_tune_mu;
 std::unordered_map<std::string, Choice> g_tuned;
 
+bool lib_supported(const shai::GemmArgs& g) {
+  return g.conv == 0 && g.batch <= 1 && !g.glu && g.act == 0 && !g.bias2d && !g.gate && !g.rms && !g.w_scale &&
+         !g.A2 && !g.in_scale && g.alpha == 1.f && !(g.bias && g.residual) &&
+         (!g.residual || (g.res_alpha == 1.f && g.residual == g.C && g.ldr == g.ldc)) &&
+         g.lda >= g.K && g.ldw >= g.K && g.ldc >= g.N;
+}
+
 std::string gemm_key(const shai::GemmArgs& g) {
   char buf[256];
   snprintf(buf, sizeof(buf), "%d:%d,%d,%d,b%d,g%d|%d,%d,%d,%d,%d,%d,%d,%d,%d", g.conv, g.M, g.N, g.K, g.batch, g.glu,
            g.Nimg, g.H, g.Wd, g.Cin, g.Cin1, g.KH, g.stride, g.upsample, g.A2 != nullptr);
-  return std::string(buf) + (g.rms ? "|rms" : "") + (g.w_scale ? "|fp8w" : "");
+  // library-eligible problems (plain GEMM, bias at most) race hipBLASLt in the tuner, so their winner must
+  // not be reused by a same-shape problem with a fused epilogue (and vice versa): separate key class
+  return std::string(buf) + (g.rms ? "|rms" : "") + (g.w_scale ? "|fp8w" : "") +
+         (lib_supported(g) && !g.residual ? "|lib" : "");
 }
 
 bool autotune_enabled() {
@@ -104,12 +114,6 @@ void launch_skinny_choice(const shai::GemmArgs& g, const Tensor& like, int kg) {
 // configs -- the hand-written kernels keep every fused-epilogue / conv / GLU / gated problem.
 constexpr int kLibCfg = 2000;
 
-bool lib_supported(const shai::GemmArgs& g) {
-  return g.conv == 0 && g.batch <= 1 && !g.glu && g.act == 0 && !g.bias2d && !g.gate && !g.rms && !g.w_scale &&
-         !g.A2 && !g.in_scale && g.alpha == 1.f && !(g.bias && g.residual) &&
-         (!g.residual || (g.res_alpha == 1.f && g.residual == g.C && g.ldr == g.ldc)) &&
-         g.lda >= g.K && g.ldw >= g.K && g.ldc >= g.N;
-}
 
 void launch_lib(const shai::GemmArgs& g, const Tensor& like) {
   const auto opt = like.options().dtype(at::kBFloat16);
@@ -556,6 +560,8 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
       g.rms = 1;
       g.rms_eps = (float)rms_eps;
     }
+    SHAI_CHECK(force_cfg < 0 || (force_cfg >= kSkinnyCfg && force_cfg <= kSkinnyCfg + 64),
+               "fp8 gemm: force_cfg must be 1000 (+ kg, 1 <= kg <= 64): only the skinny kernel takes fp8 weights");
     if (force_cfg > kSkinnyCfg) launch_choice(g, a, Choice{kSkinnyCfg, (int)(force_cfg - kSkinnyCfg)});
     else run_skinny(g, a);
     return;

@@ -100,7 +100,7 @@ def reduce_scatter_seq(x: torch.Tensor, group: Optional[dist.ProcessGroup] = Non
     assert S % n == 0, f"sequence {S} not divisible by the SP degree {n}"
     s = S // n
     if dist.get_backend(g) == "gloo":
-        y = x.contiguous()
+        y = x.clone(memory_format=torch.contiguous_format)   # never reduce into the caller's partial sums
         dist.all_reduce(y, group=g)
         return y[:, r * s:(r + 1) * s].contiguous()
     src = _seq_major(x, n)

@@ -185,7 +185,7 @@ def test_conv2d_fused(cuda):
     (1, 128, 128, 32, 8, 128, True),
     (3, 197, 197, 12, 12, 64, False),
     (1, 1056, 1056, 3, 3, 128, False),
-    # d64 with Sq >= 512 runs the 64-queries-per-wave kernel (partial last workgroup, causal, GQA)
+    # d64, Sq not a multiple of the query tile (partial last workgroup), causal, GQA
     (2, 1030, 1030, 4, 2, 64, True),
     (1, 600, 77, 5, 5, 64, False),
     (2, 4096, 4096, 1, 1, 64, False),

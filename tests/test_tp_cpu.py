@@ -29,3 +29,38 @@ def test_seq_major_layout_is_rank_chunks():
         assert v.is_contiguous() and v.shape == (4, B, 3, 5)
         for r in range(4):
             assert torch.equal(v[r], x[:, 3 * r:3 * (r + 1)])
+
+
+def test_reduce_scatter_semantics_on_seq_major_b_gt_1():
+    """Emulates RCCL reduce_scatter_tensor on the rank-major input (output r = sum over ranks of flat chunk r)
+    for B > 1 and checks it equals the all-reduce result sliced to rank r's sequence rows."""
+    import torch
+    from shai_amd.parallel.comm import _seq_major
+    n, B, S, d = 4, 3, 16, 6
+    parts = [torch.randn(B, S, d, dtype=torch.float64) for _ in range(n)]
+    full = sum(parts)
+    flats = [_seq_major(p, n).reshape(n, -1) for p in parts]        # what the collective sees: n flat chunks
+    s = S // n
+    for r in range(n):
+        out = sum(f[r] for f in flats).view(B, s, d)
+        assert torch.allclose(out, full[:, r * s:(r + 1) * s])
+
+
+def _rs_no_alias_worker(rank, world, port):
+    import os
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from shai_amd.parallel.comm import reduce_scatter_seq
+    g = dist.new_group(list(range(world)))
+    x = torch.full((2, 4, 3), float(rank + 1))
+    keep = x.clone()
+    y = reduce_scatter_seq(x, group=g)
+    assert torch.equal(x, keep), "reduce_scatter_seq modified its input"
+    assert torch.allclose(y, torch.full((2, 2, 3), 3.0))
+    dist.destroy_process_group()
+
+
+def test_reduce_scatter_seq_gloo_keeps_input():
+    mp.spawn(_rs_no_alias_worker, args=(2, _port()), nprocs=2, join=True)
