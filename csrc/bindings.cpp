@@ -92,6 +92,14 @@ int max_splits_for(const shai::GemmArgs& g) {
 // Choice.cfg of the skinny streaming kernel (csrc/kernels/gemv.hip); Choice.splits = its K-group count
 constexpr int kSkinnyCfg = 1000;
 
+// Last resort when neither the tuner nor the planner produced a usable config: the highest-numbered
+// config that supports the problem (the v2 128x64 tile supports everything v2 runs).
+Choice fallback_choice(const shai::GemmArgs& g) {
+  for (int c = shai::gemm2_num_cfgs() - 1; c >= 0; --c)
+    if (shai::gemm2_cfg_supported(g, c)) return Choice{c, 1};
+  return Choice{0, 1};
+}
+
 bool stream_capturing() {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   hipStreamIsCapturing(stream(), &cs);
@@ -139,7 +147,7 @@ void launch_choice(const shai::GemmArgs& g, const Tensor& like, Choice c) {
     // the cache key does not encode the epilogue: a problem of the same shape with a fused epilogue
     // falls back to the planner's tile config
     shai::gemm2_plan(g, &c.cfg, &c.splits);
-    if (!shai::gemm2_cfg_supported(g, c.cfg)) c = Choice{shai::gemm2_num_cfgs() - 1, 1};
+    if (!shai::gemm2_cfg_supported(g, c.cfg)) c = fallback_choice(g);
   }
   if (c.cfg == kSkinnyCfg) {
     launch_skinny_choice(g, like, c.splits);
@@ -259,7 +267,7 @@ void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_
         c = Choice{kSkinnyCfg, shai::skinny_kgroups(g)};
       } else {
         shai::gemm2_plan(g, &c.cfg, &c.splits);
-        if (!shai::gemm2_cfg_supported(g, c.cfg)) c = Choice{shai::gemm2_num_cfgs() - 1, 1};
+        if (!shai::gemm2_cfg_supported(g, c.cfg)) c = fallback_choice(g);
       }
     }
   }

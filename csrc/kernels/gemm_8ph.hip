@@ -1,0 +1,490 @@
+// bf16 GEMM / implicit-GEMM convolution, v4: 8-phase ping-pong schedule, 256x256 / 256x320 tile, BK = 64.
+//
+//   C[b,m,n] = gate * act(alpha * sum_k A[b,m,k] * W[b,n,k] + bias[n] + bias2d) + res_alpha * Res[b,m,n]
+//
+// Why a fourth kernel: v3 (gemm_pipe.hip) keeps several K-tiles of LDS-DMA in flight, but every K-step
+// still starts with all 8 waves issuing their fragment reads at once, so each SIMD's matrix pipe idles
+// for the LDS latency of both of its waves once per 32-deep step (measured 1.08-1.2 PF on large plain
+// GEMMs vs 1.5-1.6 PF for hipBLASLt).  Here the two waves that share a SIMD run half a phase apart:
+//
+// * 8 waves = 2 groups (waves 0-3 and 4-7; wave w and w+4 share a SIMD).  Group 1 executes one extra
+//   s_barrier up front, so while one group runs its 16-MFMA "compute" segment the other runs its
+//   "load" segment (fragment ds_reads + LDS-DMA issue), and the roles swap at every barrier.  The
+//   matrix pipe of each SIMD sees back-to-back MFMA segments from alternating waves.
+// * 256 x BN output tile (BN = 256, or 320: every SD2.1 UNet channel count is a multiple of 320), each
+//   wave 128 (M) x BN/4 (N) = 8 x NJ blocks of v_mfma_f32_16x16x32_bf16 (NJ = 4 / 5) with the W
+//   fragment as the A operand (each lane owns 4 consecutive output columns of one row).
+// * A K-tile (64 deep) is 4 phases: (k-substep 0|1) x (M half 0|1), 4 x NJ MFMAs each.  W fragments
+//   (NJ ds_read_b128) are read in the first phase of each k-substep and held for the second; X
+//   fragments (4 ds_read_b128) are read every phase.
+// * 2 LDS buffers of (A 256x64 + W BNx64) bf16 = 128 / 144 KB.  Tile t+1 is staged into the other
+//   buffer by LDS-DMA (`buffer_load ... lds`, 16 B per lane; 4 A + NJ W instructions per wave per
+//   K-tile, A and W interleaved) over phases 0-1 of tile t; every wave retires its own DMA with vmcnt(0)
+//   at the end of its phase-3 load segment, which precedes (in barrier order) every wave's first read
+//   of tile t+1.
+// * Each load segment ends with lgkmcnt(0) BEFORE its barrier, so when a group starts restaging a
+//   buffer the other group's reads of it have completed (WAR across the half-phase stagger).
+// * LDS image lane-linear per DMA wave-instruction (8 rows x 128 B); bank swizzle (16-B chunk ^=
+//   (row >> 1) & 7) applied to the per-lane SOURCE address and to the ds_read address: every 16-lane
+//   ds_read_b128 group touches 16 distinct 16-B bank slots (conflict-free).
+// * Implicit-GEMM conv when Cin (and the concat split Cin1) are multiples of 64: each K-tile then lies
+//   inside one filter tap and one source tensor, so only (ih, iw) of the lane's 4 rows change per tile.
+// * Range-checked buffer descriptors give the zero fill (M/N/K tails, conv padding); XCD-aware
+//   bijective block remap + grouped M ordering.
+#include "gemm_epilogue.h"
+
+namespace shai {
+
+typedef __bf16 bf16x8q __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void g4_lds_void;
+
+constexpr int G4_BM = 256, G4_BK = 64;
+template <int BN>
+struct G4T {
+  static constexpr int STAGE = (G4_BM + BN) * G4_BK;  // elements per LDS buffer (64 / 72 KB)
+  static constexpr int NJ = BN / 64;                   // 16-column MFMA blocks per wave (4 / 5)
+  static constexpr int WC = BN / 4;                    // columns per wave (64 / 80)
+  static constexpr int NWJ = BN / 64;                  // W DMA instructions (8 rows each) per wave per tile
+  static constexpr int GT = 4 + NWJ;                   // DMA instructions per wave per tile
+};
+constexpr uint32_t G4_OOB = 0x80000000u;
+
+__device__ __forceinline__ int g4_swz(int row, int ch) { return row * G4_BK + ((ch ^ ((row >> 1) & 7)) << 3); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t g4_rsrc(const void* base, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)min(bytes, 0x7fffffffL),
+                                           0x00020000);
+}
+
+__device__ __forceinline__ void g4_glds(__amdgpu_buffer_rsrc_t r, bf16_t* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (g4_lds_void*)lds, 16, off, 0, 0, 0);
+}
+
+// Schedule variants (lab A/B; 0 = production):
+//   bit 0: no stagger (both wave groups in lockstep)
+//   bit 1: static priority (waves 4-7 at prio 1 for the whole loop) instead of per-segment setprio
+//   bit 2: LDS-DMA issued over phases 0-1 (halves) instead of over phases 0-2 (quarter, half, quarter)
+// Phase p of a K-tile issues the DMA instructions g in [G_p, G_{p+1}) of the next tile.
+template <int VAR, int GT>
+struct G4Sched {
+  static constexpr int G1 = (VAR & 4) ? (GT + 1) / 2 : GT / 4, G2 = (VAR & 4) ? GT : (3 * GT) / 4;
+};
+
+// Scalar (wave-uniform) position of a K-tile inside the implicit-GEMM conv: filter tap (kh, kw) and
+// channel base c (Cin % 64 == 0, so a 64-deep K-tile never straddles a tap or the concat split).
+struct G4ConvPos {
+  int kh, kw, c;
+};
+
+// CONV: 0 plain GEMM, 1 implicit-GEMM conv, 2 implicit-GEMM conv over a nearest-2x upsampled input.
+template <int CONV, bool GLU, int ACT, bool SPLITK, int VAR, int BN>
+__global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __restrict__ ws, int k_per_split) {
+  constexpr bool STAGGER = !(VAR & 1), STATIC_PRIO = (VAR & 2) != 0;
+  constexpr int G4_STAGE = G4T<BN>::STAGE, NJ = G4T<BN>::NJ, WC = G4T<BN>::WC, NWJ = G4T<BN>::NWJ;
+  constexpr int GT = G4T<BN>::GT;
+  constexpr int G4_G0 = 0, G4_G1 = G4Sched<VAR, GT>::G1, G4_G2 = G4Sched<VAR, GT>::G2, G4_G3 = GT;
+  extern __shared__ __attribute__((aligned(16))) bf16_t g4_smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;  // wm = ping-pong group = M half of the tile
+
+  // ---- tile mapping (XCD remap + grouped M ordering)
+  const int tiles_m = (p.M + G4_BM - 1) / G4_BM, tiles_n = (p.N + BN - 1) / BN;
+  const int total = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int xcd = bid & 7, q = total >> 3, r = total & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  constexpr int GROUP = 8;
+  const int group = bid / (GROUP * tiles_n);
+  const int first_m = group * GROUP;
+  const int gsize = min(tiles_m - first_m, GROUP);
+  const int in_group = bid - group * GROUP * tiles_n;
+  const int m0 = (first_m + in_group % gsize) * G4_BM;
+  const int n0 = (in_group / gsize) * BN;
+  const int b = SPLITK ? 0 : blockIdx.y;
+  const int kz = SPLITK ? blockIdx.y : 0;
+  const int k_begin = kz * k_per_split;
+  const int k_end = min(p.K, k_begin + k_per_split);
+
+  const bf16_t* A = p.A + (long)b * p.batch_a;
+  const bf16_t* Wt = p.W + (long)b * p.batch_w;
+  const __amdgpu_buffer_rsrc_t rW = g4_rsrc(Wt, (long)p.N * p.ldw * 2);
+  __amdgpu_buffer_rsrc_t rA, rA2;
+  if constexpr (CONV != 0) {
+    rA = g4_rsrc(A, (long)p.Nimg * p.H * p.Wd * (p.A2 ? p.Cin1 : p.Cin) * 2);
+    rA2 = p.A2 ? g4_rsrc(p.A2, (long)p.Nimg * p.H * p.Wd * (p.Cin - p.Cin1) * 2) : rA;
+  } else {
+    rA = g4_rsrc(A, (long)p.M * p.lda * 2);
+    rA2 = rA;
+  }
+
+  // ---- staging geometry: DMA wave-instruction j fills 8 LDS rows x 128 B (lane-linear); the lane's
+  // source chunk is the swizzled one.  Per-row byte offsets are precomputed; an invalid row's offset
+  // carries the OOB bit, which survives the per-tile additions (< 2^31) and reads as zero fill.
+  const int lrow = lane >> 3, lpos = lane & 7;
+  int kch[4];            // k offset of the lane's source chunk within the K-tile (A rows)
+  int kchw[NWJ];         // same for the W rows
+  uint32_t woff[NWJ];    // W row byte offset + chunk
+  uint32_t aoff[4];      // plain GEMM: A row byte offset + chunk
+  int ih0[4], iw0[4];    // conv: top-left input tap position of the output pixel (upsampled grid for CONV 2)
+  int pix[4];            // conv (CONV 1): pixel index of (ih0, iw0); CONV 2: n * H
+#pragma unroll
+  for (int j = 0; j < NWJ; ++j) {
+    const int row = wid * (BN / 8) + j * 8 + lrow;
+    kchw[j] = (lpos ^ ((row >> 1) & 7)) * 8;
+    const int n = n0 + row;
+    woff[j] = n < p.N ? (uint32_t)(((long)n * p.ldw + kchw[j]) * 2) : G4_OOB;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = wid * 32 + j * 8 + lrow;
+    kch[j] = (lpos ^ ((row >> 1) & 7)) * 8;
+    const int m = m0 + row;
+    if constexpr (CONV == 0) {
+      aoff[j] = m < p.M ? (uint32_t)(((long)m * p.lda + kch[j]) * 2) : G4_OOB;
+    } else {
+      const int hw = p.OH * p.OW;
+      const int mm = m < p.M ? m : 0;
+      const int cn = mm / hw;
+      const int rem = mm - cn * hw;
+      const int coh = rem / p.OW, cow = rem - coh * p.OW;
+      if constexpr (CONV == 1) {
+        ih0[j] = m < p.M ? coh * p.stride - p.pad : -(1 << 24);
+        iw0[j] = cow * p.stride - p.pad;
+        pix[j] = (cn * p.H + ih0[j]) * p.Wd + iw0[j];
+      } else {
+        ih0[j] = m < p.M ? coh - p.pad : -(1 << 24);
+        iw0[j] = cow - p.pad;
+        pix[j] = cn * p.H;
+      }
+      aoff[j] = (uint32_t)kch[j] * 2;
+    }
+  }
+  const int cs_a = p.A2 ? p.Cin1 : p.Cin;  // channel stride (elements per pixel) of source A / A2
+  const int cs_b = p.Cin - p.Cin1;
+
+  // Issue DMA g of the K-tile at k0 (conv position cp) into buffer buf: g < 8: even = A rows j = g / 2,
+  // odd = W rows j = g / 2 (A and W interleave so every phase that stages issues both kinds); g = 8: W
+  // rows 4 (BN = 320).
+  auto stage_one = [&](int buf, int k0, const G4ConvPos& cp, int g) {
+    bf16_t* sa = g4_smem + buf * G4_STAGE;
+    const int j = g >> 1;
+    const bool ktail = k0 + G4_BK > k_end;  // uniform: only the last K-tile of a ragged K checks chunks
+    if ((g & 1) || g == 8) {
+      uint32_t off = woff[j] + (uint32_t)k0 * 2;
+      if (ktail && k0 + kchw[j] >= k_end) off = G4_OOB;
+      g4_glds(rW, sa + G4_BM * G4_BK + (wid * (BN / 8) + j * 8) * G4_BK, off);
+      return;
+    }
+    if constexpr (CONV == 0) {
+      uint32_t off = aoff[j] + (uint32_t)k0 * 2;
+      if (ktail && k0 + kch[j] >= k_end) off = G4_OOB;
+      g4_glds(rA, sa + (wid * 32 + j * 8) * G4_BK, off);
+    } else {
+      const bool second = p.A2 != nullptr && cp.c >= p.Cin1;
+      const int cs = second ? cs_b : cs_a;
+      const int cb = second ? cp.c - p.Cin1 : cp.c;
+      const int ih = ih0[j] + cp.kh, iw = iw0[j] + cp.kw;
+      uint32_t off;
+      if constexpr (CONV == 1) {
+        const bool ok = ((unsigned)ih < (unsigned)p.H) & ((unsigned)iw < (unsigned)p.Wd);
+        const int tapd = cp.kh * p.Wd + cp.kw;
+        off = ok ? (uint32_t)((pix[j] + tapd) * cs + cb) * 2 + aoff[j] : G4_OOB;
+      } else {
+        const bool ok = ((unsigned)ih < (unsigned)(2 * p.H)) & ((unsigned)iw < (unsigned)(2 * p.Wd));
+        const int px = (pix[j] + (ih >> 1)) * p.Wd + (iw >> 1);
+        off = ok ? (uint32_t)(px * cs + cb) * 2 + aoff[j] : G4_OOB;
+      }
+      if (k0 >= k_end) off = G4_OOB;
+      g4_glds(second ? rA2 : rA, sa + (wid * 32 + j * 8) * G4_BK, off);
+    }
+  };
+  auto conv_pos = [&](int k0) {
+    G4ConvPos cp{0, 0, 0};
+    if constexpr (CONV != 0) {
+      const int tap = k0 / p.Cin;
+      cp.c = k0 - tap * p.Cin;
+      cp.kh = tap / p.KW;
+      cp.kw = tap - cp.kh * p.KW;
+    }
+    return cp;
+  };
+  auto conv_advance = [&](G4ConvPos& cp) {
+    if constexpr (CONV != 0) {
+      cp.c += G4_BK;
+      if (cp.c >= p.Cin) {
+        cp.c = 0;
+        if (++cp.kw == p.KW) {
+          cp.kw = 0;
+          ++cp.kh;
+        }
+      }
+    }
+  };
+
+  float4_ acc[8][NJ];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = k_end > k_begin ? (k_end - k_begin + G4_BK - 1) / G4_BK : 0;
+
+  // prologue: tile 0 -> buffer 0
+  G4ConvPos cpos = conv_pos(k_begin);
+  if (nk > 0) {
+#pragma unroll
+    for (int g = 0; g < GT; ++g) stage_one(0, k_begin, cpos, g);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (STAGGER && wm == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs half a phase behind
+  if (STATIC_PRIO && wm == 1) __builtin_amdgcn_s_setprio(1);
+  __builtin_amdgcn_sched_barrier(0);
+
+  bf16x8q wf[NJ], xf[4];
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    const bool pre = t + 1 < nk;
+    const int knext = k_begin + (t + 1) * G4_BK;
+    conv_advance(cpos);  // position of tile t + 1
+    const bf16_t* sa = g4_smem + cur * G4_STAGE;
+    const bf16_t* sw = sa + G4_BM * G4_BK;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int ks = ph >> 1, mh = ph & 1;
+      // ---- load segment
+      const int g_lo = ph == 0 ? G4_G0 : ph == 1 ? G4_G1 : ph == 2 ? G4_G2 : G4_G3;
+      const int g_hi = ph == 0 ? G4_G1 : ph == 1 ? G4_G2 : ph == 2 ? G4_G3 : GT;
+      if (pre) {
+#pragma unroll
+        for (int g = g_lo; g < g_hi; ++g) stage_one(cur ^ 1, knext, cpos, g);
+      }
+      if (mh == 0) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          wf[j] = *reinterpret_cast<const bf16x8q*>(sw + g4_swz(wn * WC + j * 16 + fr, ks * 4 + fq));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        xf[i] = *reinterpret_cast<const bf16x8q*>(sa + g4_swz(wm * 128 + (mh * 4 + i) * 16 + fr, ks * 4 + fq));
+      if (ph == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t+1 landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- compute segment
+      if (!STATIC_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[mh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[mh * 4 + i][j], 0, 0, 0);
+      if (!STATIC_PRIO) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (STATIC_PRIO) __builtin_amdgcn_s_setprio(0);
+  if (STAGGER && wm == 0) __builtin_amdgcn_s_barrier();  // un-stagger: equal barrier counts on exit
+
+  // ---- epilogue: D[n][m] blocks -> lane owns row m = fr, columns n..n+3 = 4 fq + reg
+  if constexpr (SPLITK) {
+    float* Wp = ws + (long)kz * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wm * 128 + i * 16 + fr;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + wn * WC + j * 16 + 4 * fq;
+        if (n + 3 < p.N) {
+          *reinterpret_cast<float4_*>(Wp + (long)m * p.N + n) = acc[i][j];
+        } else {
+          for (int e = 0; e < 4 && n + e < p.N; ++e) Wp[(long)m * p.N + n + e] = acc[i][j][e];
+        }
+      }
+    }
+  } else {
+    bf16_t* __restrict__ C = p.C + (long)b * p.batch_c;
+    const bf16_t* __restrict__ R = p.residual ? p.residual + (long)b * p.batch_r : nullptr;
+    const bool fast = m0 + G4_BM <= p.M && n0 + BN <= p.N && p.bias2d == nullptr && p.gate == nullptr &&
+                      (p.ldc & 3) == 0 && (R == nullptr || (p.ldr & 3) == 0);
+    if (fast) {
+      // interior tile: per-column bias hoisted, residual rows prefetched in groups of IG row blocks (all 8
+      // at NJ = 4; 2 at NJ = 5, where 160 accumulator registers leave no room for 80 more)
+      const bf16_t* __restrict__ bias = p.bias;
+      float bj[NJ][4];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + wn * WC + j * 16 + 4 * fq;
+        if (bias) {
+          const uint2_ bb = *reinterpret_cast<const uint2_*>(bias + n);
+          bj[j][0] = bf2f(bb[0] & 0xffff); bj[j][1] = bf2f(bb[0] >> 16);
+          bj[j][2] = bf2f(bb[1] & 0xffff); bj[j][3] = bf2f(bb[1] >> 16);
+        } else {
+          bj[j][0] = bj[j][1] = bj[j][2] = bj[j][3] = 0.f;
+        }
+      }
+      constexpr int IG = NJ == 4 ? 8 : 2;
+      if constexpr (!GLU) {
+#pragma unroll
+        for (int i0 = 0; i0 < 8; i0 += IG) {
+          uint2_ rr[IG][NJ];
+          if (R) {
+#pragma unroll
+            for (int ii = 0; ii < IG; ++ii)
+#pragma unroll
+              for (int j = 0; j < NJ; ++j)
+                rr[ii][j] = *reinterpret_cast<const uint2_*>(R + (long)(m0 + wm * 128 + (i0 + ii) * 16 + fr) * p.ldr +
+                                                             n0 + wn * WC + j * 16 + 4 * fq);
+          }
+#pragma unroll
+          for (int ii = 0; ii < IG; ++ii) {
+            const int i = i0 + ii;
+            const int m = m0 + wm * 128 + i * 16 + fr;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              const int n = n0 + wn * WC + j * 16 + 4 * fq;
+              float v[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = apply_act<ACT>(acc[i][j][e] * p.alpha + bj[j][e]);
+              if (R) {
+                v[0] += bf2f(rr[ii][j][0] & 0xffff) * p.res_alpha; v[1] += bf2f(rr[ii][j][0] >> 16) * p.res_alpha;
+                v[2] += bf2f(rr[ii][j][1] & 0xffff) * p.res_alpha; v[3] += bf2f(rr[ii][j][1] >> 16) * p.res_alpha;
+              }
+              uint2_ o;
+              o[0] = pack2(v[0], v[1]);
+              o[1] = pack2(v[2], v[3]);
+              *reinterpret_cast<uint2_*>(C + (long)m * p.ldc + n) = o;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i0 = 0; i0 < 8; i0 += IG) {
+          uint32_t rr[IG][NJ];
+          if (R) {
+#pragma unroll
+            for (int ii = 0; ii < IG; ++ii)
+#pragma unroll
+              for (int j = 0; j < NJ; ++j)
+                rr[ii][j] = *reinterpret_cast<const uint32_t*>(R + (long)(m0 + wm * 128 + (i0 + ii) * 16 + fr) * p.ldr +
+                                                              ((n0 + wn * WC + j * 16 + 4 * fq) >> 1));
+          }
+#pragma unroll
+          for (int ii = 0; ii < IG; ++ii) {
+            const int i = i0 + ii;
+            const int m = m0 + wm * 128 + i * 16 + fr;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              const int nc = (n0 + wn * WC + j * 16 + 4 * fq) >> 1;
+              float o0 = (acc[i][j][0] * p.alpha + bj[j][0]) * apply_act<ACT>(acc[i][j][1] * p.alpha + bj[j][1]);
+              float o1 = (acc[i][j][2] * p.alpha + bj[j][2]) * apply_act<ACT>(acc[i][j][3] * p.alpha + bj[j][3]);
+              if (R) {
+                o0 += bf2f(rr[ii][j] & 0xffff) * p.res_alpha;
+                o1 += bf2f(rr[ii][j] >> 16) * p.res_alpha;
+              }
+              *reinterpret_cast<uint32_t*>(C + (long)m * p.ldc + nc) = pack2(o0, o1);
+            }
+          }
+        }
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wm * 128 + i * 16 + fr;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = n0 + wn * WC + j * 16 + 4 * fq;
+        if (n >= p.N) continue;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        epilogue4<GLU, ACT>(p, C, R, m, n, v, b);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- host side
+bool gemm4_supported(const GemmArgs& a) {
+  if (a.in_scale != nullptr) return false;
+  if (a.K % 8 != 0 || a.lda % 8 != 0 || a.ldw % 8 != 0) return false;  // 16-B source chunks
+  if (a.conv) {
+    if (a.Cin % 64 != 0) return false;
+    if (a.A2 != nullptr && a.Cin1 % 64 != 0) return false;
+  }
+  return true;
+}
+
+template <int CONV, bool GLU, int ACT, int VAR = 4>
+static void g4_launch(const GemmArgs& a, float* ws, int splits, int kps, int bn, hipStream_t s) {
+  dim3 grid(1, splits > 1 ? splits : (a.batch > 0 ? a.batch : 1));
+  if (bn == 320) {
+    grid.x = ((a.M + G4_BM - 1) / G4_BM) * ((a.N + 319) / 320);
+    const size_t lds = (size_t)2 * G4T<320>::STAGE * sizeof(bf16_t);
+    if (splits > 1) gemm4_kernel<CONV, GLU, ACT, true, VAR, 320><<<grid, 512, lds, s>>>(a, ws, kps);
+    else gemm4_kernel<CONV, GLU, ACT, false, VAR, 320><<<grid, 512, lds, s>>>(a, ws, kps);
+  } else {
+    grid.x = ((a.M + G4_BM - 1) / G4_BM) * ((a.N + 255) / 256);
+    const size_t lds = (size_t)2 * G4T<256>::STAGE * sizeof(bf16_t);
+    if (splits > 1) gemm4_kernel<CONV, GLU, ACT, true, VAR, 256><<<grid, 512, lds, s>>>(a, ws, kps);
+    else gemm4_kernel<CONV, GLU, ACT, false, VAR, 256><<<grid, 512, lds, s>>>(a, ws, kps);
+  }
+}
+
+// splits > 1 requires ws ([splits][M][N] fp32); the split-K fold + epilogue runs afterwards.
+void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t s) {
+  if (ws == nullptr) splits = 1;
+  const long kt = (a.K + G4_BK - 1) / G4_BK;
+  const int kps = (int)(((kt + splits - 1) / splits) * G4_BK);
+  if (a.conv) {
+    if (a.upsample) {
+      if (a.act == ACT_SILU) g4_launch<2, false, ACT_SILU>(a, ws, splits, kps, bn, s);
+      else g4_launch<2, false, ACT_NONE>(a, ws, splits, kps, bn, s);
+    } else {
+      if (a.act == ACT_SILU) g4_launch<1, false, ACT_SILU>(a, ws, splits, kps, bn, s);
+      else g4_launch<1, false, ACT_NONE>(a, ws, splits, kps, bn, s);
+    }
+  } else if (a.glu) {
+    if (a.act == ACT_SILU) g4_launch<0, true, ACT_SILU>(a, ws, splits, kps, bn, s);
+    else if (a.act == ACT_GELU_TANH) g4_launch<0, true, ACT_GELU_TANH>(a, ws, splits, kps, bn, s);
+    else g4_launch<0, true, ACT_GELU>(a, ws, splits, kps, bn, s);
+  } else {
+    switch (a.act) {
+      case ACT_SILU: g4_launch<0, false, ACT_SILU>(a, ws, splits, kps, bn, s); break;
+      case ACT_GELU: g4_launch<0, false, ACT_GELU>(a, ws, splits, kps, bn, s); break;
+      case ACT_GELU_TANH: g4_launch<0, false, ACT_GELU_TANH>(a, ws, splits, kps, bn, s); break;
+      case ACT_QUICK_GELU: g4_launch<0, false, ACT_QUICK_GELU>(a, ws, splits, kps, bn, s); break;
+      case ACT_RELU: g4_launch<0, false, ACT_RELU>(a, ws, splits, kps, bn, s); break;
+      default: g4_launch<0, false, ACT_NONE>(a, ws, splits, kps, bn, s); break;
+    }
+  }
+  if (splits > 1) launch_splitk_epilogue(a, ws, splits, s);
+}
+
+// Lab entry: schedule variant `var` (see G4Sched) of the plain / conv no-activation kernel, no split-K.
+void launch_gemm4_var(const GemmArgs& a, int var, int bn, hipStream_t s) {
+  const int kps = (int)(((a.K + G4_BK - 1) / G4_BK) * G4_BK);
+#define SHAI_G4V(V)                                                               \
+  case V:                                                                         \
+    if (a.conv) {                                                                 \
+      if (a.upsample) g4_launch<2, false, ACT_NONE, V>(a, nullptr, 1, kps, bn, s); \
+      else g4_launch<1, false, ACT_NONE, V>(a, nullptr, 1, kps, bn, s);            \
+    } else {                                                                      \
+      g4_launch<0, false, ACT_NONE, V>(a, nullptr, 1, kps, bn, s);                \
+    }                                                                             \
+    break;
+  switch (var) {
+    SHAI_G4V(0) SHAI_G4V(4) SHAI_G4V(6)
+    default: break;
+  }
+#undef SHAI_G4V
+}
+
+}  // namespace shai

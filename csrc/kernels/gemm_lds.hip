@@ -350,6 +350,10 @@ struct TileCfg {
 static const TileCfg kCfgs[] = {{256, 320, 1.00f}, {256, 256, 1.00f}, {256, 128, 0.90f}, {128, 128, 0.75f},
                                 {128, 64, 0.55f}};
 constexpr int kNumCfgs = 5;
+// Config index space: [0, kNumCfgs) this file's tile configs; kNumCfgs + 0..3 the pipelined v3 kernel
+// (gemm_pipe.hip); kNumCfgs + 4 / + 5 the 8-phase ping-pong v4 kernel (gemm_8ph.hip) with 256 / 320 wide tiles.
+constexpr int kV4Cfg = kNumCfgs + 4;
+
 
 template <bool CONV, bool FAST, bool GLU, int ACT>
 static void launch_tiles(const GemmArgs& a, int cfg, float* ws, int splits, int kps, hipStream_t s) {
@@ -413,6 +417,12 @@ void gemm2_plan(const GemmArgs& a, int* cfg, int* splits) {
   }
   *cfg = bc;
   *splits = bs;
+  // v4 (8-phase ping-pong) outruns every v2 tile on problems that fill the chip with 256-row tiles
+  if (forced < 0 && gemm4_supported(a) && bs == 1) {
+    const int bn = (N % 320 == 0 && N % 256 != 0) ? 320 : 256;
+    const long tiles = ((M + 255) / 256) * ((N + bn - 1) / bn) * batch;
+    if (tiles >= 192 && K >= 256) *cfg = kV4Cfg + (bn == 320 ? 1 : 0);
+  }
 }
 
 size_t gemm2_workspace_bytes(const GemmArgs& a) {
@@ -452,6 +462,10 @@ static void launch_all(const GemmArgs& a, float* ws, int cfg, int splits, hipStr
 }
 
 void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStream_t s) {
+  if (cfg >= kV4Cfg) {
+    launch_gemm4(a, ws, splits, cfg == kV4Cfg + 1 ? 320 : 256, s);
+    return;
+  }
   if (cfg >= kNumCfgs) {  // pipelined kernel (gemm_pipe.hip): 256x256 / 256x320 tile, 4- / 2-stage ring
     const int v = cfg - kNumCfgs;
     launch_gemm3(a, ws, splits, (v & 1) ? 2 : 4, s, v >= 2 ? 320 : 256);
@@ -484,16 +498,22 @@ void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipS
   }
 }
 
-int gemm2_num_cfgs() { return kNumCfgs + 4; }
+int gemm2_num_cfgs() { return kV4Cfg + 2; }
 
 bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
-  if (cfg >= kNumCfgs) return cfg < kNumCfgs + 4 && gemm3_supported(a);
+  if (cfg >= kV4Cfg) return cfg < kV4Cfg + 2 && gemm4_supported(a);
+  if (cfg >= kNumCfgs) return gemm3_supported(a);
   if (a.in_scale != nullptr) return false;
   if (a.conv && a.A2 != nullptr && (a.Cin % 64 != 0 || a.Cin1 % 64 != 0)) return false;  // 64-wide K tiles
   return cfg >= 0 && cfg < kNumCfgs;
 }
 
 void gemm2_cfg_info(int cfg, int* bm, int* bn) {
+  if (cfg >= kV4Cfg) {  // 8-phase v4 kernel: reported as "8x-<BN>"
+    *bm = 8;
+    *bn = cfg == kV4Cfg + 1 ? -320 : -256;
+    return;
+  }
   if (cfg >= kNumCfgs) {
     const int v = cfg - kNumCfgs;
     *bm = (v & 1) ? 2 : 4;  // pipelined v3 kernel: stages

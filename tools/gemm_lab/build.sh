@@ -1,0 +1,17 @@
+#!/bin/bash
+# Build the standalone GEMM lab (tools/gemm_lab/gemm_lab.cpp + the GEMM kernel sources) for gfx950.
+set -euo pipefail
+ROOT=$(cd "$(dirname "$0")/../.." && pwd)
+OUT=$ROOT/build/gemm_lab
+mkdir -p "$OUT"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=fast -I$ROOT/csrc"
+for src in gemm_lds gemm_pipe gemm_8ph; do
+  # incremental: rebuild an object only when its source or a shared header is newer
+  if [ ! -f "$OUT/$src.o" ] || [ -n "$(find "$ROOT/csrc/kernels/$src.hip" "$ROOT/csrc/kernels/"*.h -newer "$OUT/$src.o")" ]; then
+    hipcc $FLAGS -c "$ROOT/csrc/kernels/$src.hip" -o "$OUT/$src.o" &
+  fi
+done
+hipcc $FLAGS -x hip -c "$ROOT/tools/gemm_lab/gemm_lab.cpp" -o "$OUT/gemm_lab.o" &
+wait
+mkdir -p "$ROOT/tools/gemm_lab/bin" && hipcc --offload-arch=gfx950 "$OUT"/*.o -o "$ROOT/tools/gemm_lab/bin/gemm_lab"
+echo "built tools/gemm_lab/bin/gemm_lab"
