@@ -20,6 +20,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <cstdlib>
+
 namespace shai {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -267,6 +269,11 @@ __global__ void __launch_bounds__(256, 2) flash_fwd_kernel(const AttnArgs p) {
 }
 
 void launch_flash_attn(const AttnArgs& a, hipStream_t s) {
+  static const bool v1_only = getenv("SHAI_FLASH_V1") != nullptr;  // A/B and tests: pin the v1 kernel
+  if (!v1_only && flash2_supported(a)) {  // 8-wave ping-pong kernel (attention2.hip)
+    launch_flash2(a, s);
+    return;
+  }
   dim3 grid((a.Sq + 127) / 128, a.Hq, a.B);
   const size_t lds = (size_t)4 * 64 * a.D * sizeof(bf16_t);
   if (a.D == 128) flash_fwd_kernel<128><<<grid, 256, lds, s>>>(a);

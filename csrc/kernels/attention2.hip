@@ -1,0 +1,339 @@
+// Flash attention forward, v2: 8-wave ping-pong (gfx950).
+//
+// Why a second kernel: v1 (attention.hip, 4 waves x 32 queries, register-staged K/V) is VALU-bound on
+// the softmax for D = 64 (~125 VALU instructions vs 16 MFMAs per wave per 64-key tile) and its waves
+// overlap MFMA and VALU poorly: the measured wave cycles were about the SUM of MFMA and VALU time.  Here
+// the two waves that share a SIMD (wave w and w + 4 of an 8-wave workgroup) run in alternating roles,
+// separated by raw s_barriers, with group 1 one segment behind group 0:
+//
+//   group 0:  [M(t)   ][V(t+1) ][M(t+1) ][V(t+2) ] ...
+//   group 1:  [V(t)   ][M(t)   ][V(t+1) ][M(t+1) ] ...
+//
+//   M(t): S(t+1) = K(t+1) Q^T and O += V(t)^T P(t)       (MFMA segment, 2 x D/16 + 2 x D/16 MFMAs)
+//   V(t): online softmax of S(t) -> P(t), O / l rescale   (VALU segment)
+//
+// so each SIMD's matrix pipe runs one wave's MFMA segment while its partner runs the softmax.
+//
+// * 256 queries per workgroup, 32 per wave.  Scores are computed swapped (S^T = K Q^T with
+//   v_mfma_f32_32x32x16_bf16) so every lane holds one query's scores; P stays in registers and feeds
+//   O^T = V^T P^T as the B operand; V^T fragments come from ds_read_b64_tr_b16 (as in v1).
+// * K/V tiles (64 keys) arrive by LDS-DMA (`buffer_load ... lds`, 16 B per lane; 2 / 4 per wave per tile
+//   at D = 64 / 128) into a 4-slot ring, three tiles ahead; the bank swizzles of v1 are applied to the
+//   per-lane SOURCE chunk.  Buffer descriptors sized to kv_len give zero fill past the sequence end.
+//   Each wave waits for its own DMA of tile t+2 (counted vmcnt, tile t+3 stays in flight) at the end of
+//   barrier interval 2t+1, before the first read of tile t+2 in interval 2t+2.
+// * Max-free softmax fast path: P = exp2(S * scale * log2e - m_run) with the running max m_run left
+//   unchanged; if any lane's partial row sum of the tile exceeds 2^8 (or is not finite), or a row has no
+//   max yet, the wave takes the exact path for that tile (tile max, O / l rescale, recompute P).  P is
+//   therefore bounded by 2^8 in the fast path (bf16 P, fp32 O / l absorb it), as with v1's deferred max.
+// * Causal masking (with offset), per-batch q / kv lengths, GQA.  Additive bias and paged K/V stay on v1.
+#include "common.h"
+#include "launchers.h"
+
+namespace shai {
+
+typedef __bf16 bf16x8a __attribute__((ext_vector_type(8)));
+typedef short s4a __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void fa2_lds_void;
+
+constexpr float kF2Log2e = 1.4426950408889634f;
+constexpr float kF2SumThr = 256.f;  // fast path while every lane's partial tile row sum <= 2^8
+
+template <int D>
+__device__ __forceinline__ int f2_kswz(int row, int ch) {
+  if constexpr (D == 128) return row * 128 + ((ch ^ (row & 15)) << 3);
+  else return row * 64 + ((ch ^ ((row >> 1) & 7)) << 3);
+}
+template <int D>
+__device__ __forceinline__ int f2_kch(int row, int ch) {  // source chunk stored at physical chunk ch
+  if constexpr (D == 128) return ch ^ (row & 15);
+  else return ch ^ ((row >> 1) & 7);
+}
+template <int D>
+__device__ __forceinline__ int f2_vswz(int row, int ch) {
+  if constexpr (D == 128) return row * 128 + ((ch ^ ((row & 3) << 2)) << 3);
+  else return row * 64 + ((ch ^ (((row >> 1) & 1) << 2)) << 3);
+}
+template <int D>
+__device__ __forceinline__ int f2_vch(int row, int ch) {
+  if constexpr (D == 128) return ch ^ ((row & 3) << 2);
+  else return ch ^ (((row >> 1) & 1) << 2);
+}
+
+// ds_read_b64_tr_b16 through inline asm: the builtin carries no alias information, so hipcc's waitcnt
+// pass drains every pending LDS-DMA (vmcnt(0)) before it -- the prefetch of tile t+3 issued at the top
+// of the same segment.  The asm is invisible to that pass; its results are waited for explicitly
+// (lgkmcnt(0) + sched_barrier, guide rule 18).
+__device__ __forceinline__ s4a f2_tr_read(const bf16_t* ptr) {
+  s4a r;
+  const uint32_t a = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)ptr);
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+
+template <int D, bool CAUSAL>
+__global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
+  constexpr int KT = 64;                 // keys per tile
+  constexpr int NS = D / 16;             // k-steps of QK^T
+  constexpr int ND = D / 32;             // 32-wide d blocks of O
+  constexpr int CPR = D / 8;             // 16-byte chunks per row
+  constexpr int RPI = 64 / CPR;          // rows per DMA wave-instruction (1 KB)
+  constexpr int NPI = KT / RPI;          // DMA instructions per operand per tile
+  constexpr int NPW = 2 * NPI / 8;       // DMA instructions per wave per tile (K and V)
+  constexpr int TILE = 2 * KT * D;       // ring slot: K tile then V tile (elements)
+  static_assert(NPW >= 1 && (2 * NPI) % 8 == 0, "bad D");
+  extern __shared__ __attribute__((aligned(16))) bf16_t f2_smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wid >> 2;
+  const int fr = lane & 31, fh = lane >> 5;
+  const int b = blockIdx.z, hq = blockIdx.y;
+  const int hk = hq / (p.Hq / p.Hkv);
+  const int q_len = p.q_lens ? p.q_lens[b] : p.Sq;
+  const int kv_len = p.kv_lens ? p.kv_lens[b] : p.Skv;
+  const int c_off = p.q_lens ? kv_len - q_len : p.causal_offset;
+  const int q0 = blockIdx.x * 256;
+  if (q0 >= q_len) return;  // whole workgroup, before any barrier
+  const int qi = q0 + wid * 32 + fr;
+
+  // ---- Q fragments (B operand of S^T = K Q^T): Q[qi][16 s + 8 fh .. +7]
+  bf16x8a qf[NS];
+  {
+    const bf16_t* qp = p.q + (long)b * p.q_bs + (long)min(qi, q_len - 1) * p.q_ts + (long)hq * D;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      uint4_ v = *reinterpret_cast<const uint4_*>(qp + 16 * s + 8 * fh);
+      if (qi >= q_len) v = uint4_{0u, 0u, 0u, 0u};
+      qf[s] = __builtin_bit_cast(bf16x8a, v);
+    }
+  }
+
+  int kv_end = kv_len;
+  if (CAUSAL) kv_end = min(kv_end, q0 + 255 + c_off + 1);
+  const int nt = kv_end > 0 ? (kv_end + KT - 1) / KT : 0;
+
+  // ---- LDS-DMA staging: this wave's NPW instructions per tile (global index gi = wid * NPW + j:
+  // operand gi / NPI (0 = K, 1 = V), piece gi % NPI = RPI consecutive key rows)
+  const bf16_t* kbase = p.k + (long)b * p.k_bs + (long)hk * D;
+  const bf16_t* vbase = p.v + (long)b * p.v_bs + (long)hk * D;
+  const __amdgpu_buffer_rsrc_t rK = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(kbase), (short)0, (int)min((long)kv_len * p.k_ts * 2, 0x7fffffffL), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rV = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(vbase), (short)0, (int)min((long)kv_len * p.v_ts * 2, 0x7fffffffL), 0x00020000);
+  uint32_t soff[NPW];
+#pragma unroll
+  for (int j = 0; j < NPW; ++j) {
+    const int gi = wid * NPW + j;
+    const int op = gi / NPI, piece = gi % NPI;
+    const int row = piece * RPI + lane / CPR, ch = lane % CPR;
+    const int src = op ? f2_vch<D>(row, ch) : f2_kch<D>(row, ch);
+    soff[j] = (uint32_t)(((long)row * (op ? p.v_ts : p.k_ts) + src * 8) * 2);
+  }
+  auto stage = [&](int t) {  // always issued (tiles past the end read as zeros) so vmcnt counts are fixed
+    bf16_t* slot = f2_smem + (t & 3) * TILE;
+#pragma unroll
+    for (int j = 0; j < NPW; ++j) {
+      const int gi = wid * NPW + j;
+      const int op = gi / NPI, piece = gi % NPI;
+      const uint32_t toff = (uint32_t)((long)t * KT * (op ? p.v_ts : p.k_ts) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(op ? rV : rK, (fa2_lds_void*)(slot + op * KT * D + piece * RPI * D),
+                                               16, soff[j] + toff, 0, 0, 0);
+    }
+  };
+
+  float16_ o[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+  const float sl2 = p.scale * kF2Log2e;
+  float16_ sacc[2];
+  bf16x8a pf[2][2];
+
+  auto qk = [&](int t) {  // S^T(t) = K(t) Q^T for two 32-key blocks
+    const bf16_t* ks = f2_smem + (t & 3) * TILE;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[kb][r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const bf16x8a kf = *reinterpret_cast<const bf16x8a*>(ks + f2_kswz<D>(kb * 32 + fr, 2 * s + fh));
+        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kb], 0, 0, 0);
+      }
+    }
+  };
+  const int g16 = lane >> 4, i16 = lane & 15;
+  const int tq = i16 >> 2, tp = i16 & 3;
+  // V(t)^T fragments of key block kb: ND x 2 (16-key halves) x 2 (row groups) transposed reads
+  auto vreads = [&](int t, int kb, s4a (&vr)[ND][2][2]) {
+    const bf16_t* vs = f2_smem + (t & 3) * TILE + KT * D;
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r0 = kb * 32 + 16 * s + 4 * fh + tq;
+        const int col = d * 32 + 16 * (g16 & 1) + 4 * tp;
+        const int ch = col >> 3, half = (col >> 2) & 1;
+        vr[d][s][0] = f2_tr_read(vs + f2_vswz<D>(r0, ch) + 4 * half);
+        vr[d][s][1] = f2_tr_read(vs + f2_vswz<D>(r0 + 8, ch) + 4 * half);
+      }
+  };
+  auto pv_mfma = [&](int kb, const s4a (&vr)[ND][2][2]) {  // O^T += V^T P^T for key block kb
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        short8 vv;
+        vv[0] = vr[d][s][0][0]; vv[1] = vr[d][s][0][1]; vv[2] = vr[d][s][0][2]; vv[3] = vr[d][s][0][3];
+        vv[4] = vr[d][s][1][0]; vv[5] = vr[d][s][1][1]; vv[6] = vr[d][s][1][2]; vv[7] = vr[d][s][1][3];
+        o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8a, vv), pf[kb][s], o[d], 0, 0, 0);
+      }
+  };
+  // P(t) from S(t) with running max m; returns this lane's partial row sum
+  auto expo = [&](float m) {
+    float ls4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8a v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(sacc[kb][8 * s + j], sl2, -m));
+          ls4[j & 3] += e;
+          v[j] = (__bf16)e;
+        }
+        pf[kb][s] = v;
+      }
+    return (ls4[0] + ls4[1]) + (ls4[2] + ls4[3]);
+  };
+  auto softmax = [&](int t) {
+    const int key0 = t * KT;
+    const bool need_mask = (key0 + KT > kv_len) || (CAUSAL && key0 + KT - 1 > q0 + c_off);
+    if (need_mask) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          const bool bad = key >= kv_len || (CAUSAL && key > qi + c_off);
+          sacc[kb][r] = bad ? -INFINITY : sacc[kb][r];
+        }
+    }
+    float ls = 0.f;
+    bool slow = __any(m_run == -INFINITY);
+    if (!slow) {
+      ls = expo(m_run);
+      slow = __any(!(ls <= kF2SumThr));
+    }
+    if (slow) {  // exact path: tile max, rescale O and l, recompute P
+      float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) m4[r & 3] = fmaxf(m4[r & 3], sacc[kb][r]);
+      float mloc = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64)) * sl2;  // scale > 0: max commutes with scaling
+      const float m_new = fmaxf(m_run, mloc);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);  // 0 when m_run = -inf
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+      l_run *= alpha;
+      m_run = m_new;
+      ls = expo(m_use);
+    }
+    l_run += ls;
+  };
+
+  // ---- prologue: tiles 0..2 in flight, 0 and 1 landed; S(0), P(0) by every wave
+  stage(0);
+  stage(1);
+  stage(2);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (nt > 0) {
+    qk(0);
+    softmax(0);
+  }
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs one segment behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  for (int t = 0; t < nt; ++t) {
+    // ---- M segment: S(t+1) = K(t+1) Q^T, O += V(t)^T P(t); DMA of tile t+3
+    stage(t + 3);
+    s4a vr0[ND][2][2], vr1[ND][2][2];
+    vreads(t, 0, vr0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < nt) qk(t + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    vreads(t, 1, vr1);
+    pv_mfma(0, vr0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    pv_mfma(1, vr1);
+    if (grp == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");  // tile t+2 landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- V segment: softmax of S(t+1)
+    if (t + 1 < nt) softmax(t + 1);
+    if (grp == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");  // tile t+2 landed
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // un-stagger: equal barrier counts on exit
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the over-issued tail DMA before exit
+
+  // ---- epilogue
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (qi < q_len) {
+    bf16_t* op = p.o + (long)b * p.o_bs + (long)qi * p.o_ts + (long)hq * D;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int dd = d * 32 + 8 * g + 4 * fh;
+        uint2_ w;
+        w[0] = pack2(o[d][4 * g] * inv, o[d][4 * g + 1] * inv);
+        w[1] = pack2(o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv);
+        *reinterpret_cast<uint2_*>(op + dd) = w;
+      }
+    }
+  }
+}
+
+bool flash2_supported(const AttnArgs& a) {
+  if (a.bias != nullptr || a.block_table != nullptr) return false;
+  if (a.D != 64 && a.D != 128) return false;
+  if (a.Sq < 512) return false;  // 256-query workgroups; v1's 128-query blocks waste less on short rows
+  // 16-B aligned rows for the DMA source chunks
+  if ((a.k_ts | a.v_ts | a.q_ts) & 7) return false;
+  return true;
+}
+
+void launch_flash2(const AttnArgs& a, hipStream_t s) {
+  dim3 grid((a.Sq + 255) / 256, a.Hq, a.B);
+  const size_t lds = (size_t)4 * 2 * 64 * a.D * sizeof(bf16_t);
+  if (a.D == 128) {
+    if (a.causal) flash2_kernel<128, true><<<grid, 512, lds, s>>>(a);
+    else flash2_kernel<128, false><<<grid, 512, lds, s>>>(a);
+  } else {
+    if (a.causal) flash2_kernel<64, true><<<grid, 512, lds, s>>>(a);
+    else flash2_kernel<64, false><<<grid, 512, lds, s>>>(a);
+  }
+}
+
+}  // namespace shai

@@ -162,6 +162,9 @@ struct AttnArgs {
   long kc_bs, kc_hs;        // cache strides: block stride, head stride (elements); token stride = D
 };
 void launch_flash_attn(const AttnArgs& a, hipStream_t s);
+// v2 (attention2.hip): 8-wave ping-pong, LDS-DMA K/V ring; launch_flash_attn dispatches to it when supported
+bool flash2_supported(const AttnArgs& a);
+void launch_flash2(const AttnArgs& a, hipStream_t s);
 
 struct DecodeAttnArgs {
   const bf16_t* q;          // [B, Hq, D]

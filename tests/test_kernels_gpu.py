@@ -230,6 +230,45 @@ def test_flash_attn_spike_forces_rescale(cuda, S, D):
     close(ops.attention(q, k, v), ref.attention(q, k, v, 1 / math.sqrt(D)), 2e-2)
 
 
+@pytest.mark.parametrize("D", [64, 128])
+def test_flash2_spike_late_and_first_tile(cuda, D):
+    """flash2 (Sq >= 512): a huge score in the first tile, late spikes past the fast-path sum bound (exact
+    path: tile max + O / l rescale) and a moderate growth that stays on the max-free fast path."""
+    torch.manual_seed(13)
+    B, S, H = 2, 1100, 2
+    q, k, v = rnd(B, S, H, D), rnd(B, S, H, D), rnd(B, S, H, D)
+    k[:, 3] = q[:, 700] * 3
+    k[:, 900] = q[:, 10] * 5
+    k[:, S - 2] = q[:, S - 300] * 5
+    k[:, 513] = q[:, 600] * 0.7
+    close(ops.attention(q, k, v), ref.attention(q, k, v, 1 / math.sqrt(D)), 2e-2)
+
+
+@pytest.mark.parametrize("D,causal", [(64, False), (128, True), (64, True)])
+def test_flash2_varlen_strided_gqa(cuda, D, causal):
+    """flash2 with packed (strided) q/k/v rows, per-batch q / kv lengths and GQA 4:1."""
+    torch.manual_seed(14)
+    B, S, Hq, Hkv = 3, 777, 8, 2
+    qkv = rnd(B, S, Hq + 2 * Hkv, D)
+    q, k, v = qkv[:, :, :Hq], qkv[:, :, Hq:Hq + Hkv], qkv[:, :, Hq + Hkv:]
+    kl = torch.tensor([777, 600, 65], device="cuda", dtype=torch.int32)
+    ql = kl.clone() if causal else None
+    o = ops.attention(q, k, v, causal=causal, kv_lens=kl, q_lens=ql)
+    orf = ref.attention(q, k, v, 1 / math.sqrt(D), causal, 0, kl, ql)
+    for b in range(B):  # rows past q_len are unspecified
+        n = int((ql if ql is not None else torch.full_like(kl, S))[b])
+        close(o[b, :n], orf[b, :n], 2e-2)
+
+
+def test_flash2_causal_offset_chunk(cuda):
+    """Chunked-prefill shape: 600 new queries attending causally over 1500 keys (offset 900)."""
+    torch.manual_seed(15)
+    B, Sq, Skv, H, D = 1, 600, 1500, 4, 128
+    q, k, v = rnd(B, Sq, H, D), rnd(B, Skv, H, D), rnd(B, Skv, H, D)
+    o = ops.attention(q, k, v, causal=True, causal_offset=Skv - Sq)
+    close(o, ref.attention(q, k, v, 1 / math.sqrt(D), True, Skv - Sq), 2e-2)
+
+
 def test_flash_attn_bias_d64_long(cuda):
     torch.manual_seed(12)
     B, S, H, D = 1, 520, 2, 64
