@@ -71,6 +71,12 @@ __device__ __forceinline__ s4a f2_tr_read(const bf16_t* ptr) {
   return r;
 }
 
+// LDS-DMA through a device helper: a direct call of the target builtin inside the kernel template's
+// lambda makes the host pass drop the kernel's launch stubs (undefined __device_stub__ at load time).
+__device__ __forceinline__ void f2_glds(__amdgpu_buffer_rsrc_t r, bf16_t* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (fa2_lds_void*)lds, 16, off, 0, 0, 0);
+}
+
 template <int D, bool CAUSAL>
 __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
   constexpr int KT = 64;                 // keys per tile
@@ -137,8 +143,7 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
       const int gi = wid * NPW + j;
       const int op = gi / NPI, piece = gi % NPI;
       const uint32_t toff = (uint32_t)((long)t * KT * (op ? p.v_ts : p.k_ts) * 2);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(op ? rV : rK, (fa2_lds_void*)(slot + op * KT * D + piece * RPI * D),
-                                               16, soff[j] + toff, 0, 0, 0);
+      f2_glds(op ? rV : rK, slot + op * KT * D + piece * RPI * D, soff[j] + toff);
     }
   };
 
@@ -152,17 +157,21 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
   float16_ sacc[2];
   bf16x8a pf[2][2];
 
-  auto qk = [&](int t) {  // S^T(t) = K(t) Q^T for two 32-key blocks
+  auto qk = [&](int t) {  // S^T(t) = K(t) Q^T for two 32-key blocks; every K fragment read issued first
     const bf16_t* ks = f2_smem + (t & 3) * TILE;
+    bf16x8a kf[2][NS];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        kf[kb][s] = *reinterpret_cast<const bf16x8a*>(ks + f2_kswz<D>(kb * 32 + fr, 2 * s + fh));
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) sacc[kb][r] = 0.f;
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const bf16x8a kf = *reinterpret_cast<const bf16x8a*>(ks + f2_kswz<D>(kb * 32 + fr, 2 * s + fh));
-        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kb], 0, 0, 0);
-      }
+      for (int s = 0; s < NS; ++s) sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][s], qf[s], sacc[kb], 0, 0, 0);
     }
   };
   const int g16 = lane >> 4, i16 = lane & 15;
@@ -319,6 +328,10 @@ bool flash2_supported(const AttnArgs& a) {
   if (a.bias != nullptr || a.block_table != nullptr) return false;
   if (a.D != 64 && a.D != 128) return false;
   if (a.Sq < 512) return false;  // 256-query workgroups; v1's 128-query blocks waste less on short rows
+  if (a.Skv < 512) return false;  // a few key tiles: v1 has less per-workgroup setup (cross-attention to 77 tokens)
+  // measured on MI355X (tools/bench_kernels.py): D = 128 +11..18 % over v1; D = 64 +4 % at 4096 x 4096 but
+  // -17 % at 1024 x 1024 (its softmax segment outlasts the 16-MFMA segment), so D = 64 only for long rows
+  if (a.D == 64 && (a.Sq < 2048 || a.Skv < 2048)) return false;
   // 16-B aligned rows for the DMA source chunks
   if ((a.k_ts | a.v_ts | a.q_ts) & 7) return false;
   return true;
