@@ -50,7 +50,7 @@ class SamplingParams:
     seed: Optional[int] = None
 
 
-@dataclass
+@dataclass(eq=False)  # identity semantics: membership tests must not deep-compare prompts (O(B^2))
 class Sequence_:
     seq_id: int
     prompt: List[int]
@@ -75,6 +75,10 @@ class Sequence_:
     @property
     def length(self) -> int:
         return len(self.prompt) + len(self.output)
+
+    @property
+    def last_token(self) -> int:
+        return self.output[-1] if self.output else self.prompt[-1]
 
 
 def _chain_hash(prev: int, toks: Sequence[int]) -> int:
@@ -423,12 +427,13 @@ class LLMEngine:
                 s.output = []
                 self.running.remove(s)
                 self.waiting.insert(0, s)
-        seqs = [s for s in seqs if s in self.running]
+        running = set(map(id, self.running))
+        seqs = [s for s in seqs if id(s) in running]
         if not seqs:
             return
         B = len(seqs)
         pos, slots, lens, bt = build_decode([s.length - 1 for s in seqs], [s.blocks for s in seqs], self.max_blocks)
-        ids = [s.tokens[-1] for s in seqs]
+        ids = [s.last_token for s in seqs]
         Bc = 1 << max(0, math.ceil(math.log2(B)))
         cross = self._cross_tables(seqs) if any(s.cross_blocks for s in seqs) else None
         key = (Bc, cross is not None)
