@@ -71,13 +71,25 @@ __device__ __forceinline__ s4a f2_tr_read(const bf16_t* ptr) {
   return r;
 }
 
+__device__ __forceinline__ bf16x8a f2_b128_read(const bf16_t* ptr) {
+  bf16x8a r;
+  const uint32_t a = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)ptr);
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+
 // LDS-DMA through a device helper: a direct call of the target builtin inside the kernel template's
 // lambda makes the host pass drop the kernel's launch stubs (undefined __device_stub__ at load time).
 __device__ __forceinline__ void f2_glds(__amdgpu_buffer_rsrc_t r, bf16_t* lds, uint32_t off) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (fa2_lds_void*)lds, 16, off, 0, 0, 0);
 }
 
-template <int D, bool CAUSAL>
+// Lab-only diagnostics (EXP != 0, never instantiated by launch_flash2): bit 0 skips the loop's softmax,
+// bit 1 skips the loop's MFMAs (results are then wrong; timing ablations), bit 2 records s_memtime stamps of
+// waves 0 and 4 of workgroup (0, 0, 0) at every segment boundary into g_f2_stamps.
+__device__ unsigned long long g_f2_stamps[2][2048];
+
+template <int D, bool CAUSAL, int EXP = 0>
 __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
   constexpr int KT = 64;                 // keys per tile
   constexpr int NS = D / 16;             // k-steps of QK^T
@@ -202,7 +214,15 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
       }
   };
   // P(t) from S(t) with running max m; returns this lane's partial row sum
+  // All 32 exponentials first, then the sums and bf16 packs: consuming each v_exp result right away
+  // made hipcc pad every one with an s_nop (transcendental-result hazard).
   auto expo = [&](float m) {
+    float e[2][16];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) e[kb][r] = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], sl2, -m));
+    __builtin_amdgcn_sched_barrier(0);
     float ls4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -211,9 +231,8 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
         bf16x8a v;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float e = __builtin_amdgcn_exp2f(fmaf(sacc[kb][8 * s + j], sl2, -m));
-          ls4[j & 3] += e;
-          v[j] = (__bf16)e;
+          ls4[j & 3] += e[kb][8 * s + j];
+          v[j] = (__bf16)e[kb][8 * s + j];
         }
         pf[kb][s] = v;
       }
@@ -272,37 +291,94 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
     softmax(0);
   }
   if (grp == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs one segment behind
+  // static priority for the second-dispatched half (waves 4-7), which otherwise loses every issue
+  // arbitration to its older partner (MI355X_MICROARCH "Two waves per SIMD", item 4); EXP & 8 disables it
+  if (!(EXP & 8) && grp == 1) __builtin_amdgcn_s_setprio(1);
   __builtin_amdgcn_sched_barrier(0);
 
+  const bool stamper = (EXP & 4) && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && (wid & 3) == 0;
+  int ns = 0;
+  auto stamp = [&]() {
+    if constexpr ((EXP & 4) != 0) {
+      const unsigned long long ts = __builtin_amdgcn_s_memtime();
+      if (stamper && lane == 0 && ns < 2048) g_f2_stamps[grp][ns] = ts;
+      ++ns;
+    }
+  };
   for (int t = 0; t < nt; ++t) {
     // ---- M segment: S(t+1) = K(t+1) Q^T, O += V(t)^T P(t); DMA of tile t+3
+    stamp();
     stage(t + 3);
     s4a vr0[ND][2][2], vr1[ND][2][2];
-    vreads(t, 0, vr0);
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < nt) qk(t + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    vreads(t, 1, vr1);
-    pv_mfma(0, vr0);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    pv_mfma(1, vr1);
+    if constexpr (D == 64) {
+      // every fragment read issued by asm in consumption order (K kb0, K kb1, V^T kb0 | V^T kb1), counted
+      // lgkmcnt waits before each 4-MFMA group (LDS returns in order; at most 15 outstanding)
+      const bool more = t + 1 < nt;
+      const bf16_t* ks = f2_smem + ((t + 1) & 3) * TILE;
+      bf16x8a kf[2][NS];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) kf[kb][s] = f2_b128_read(ks + f2_kswz<D>(kb * 32 + fr, 2 * s + fh));
+      vreads(t, 0, vr0);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");  // K kb0
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(EXP & 2) && more) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[0][r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) sacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[0][s], qf[s], sacc[0], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // K kb1
+      __builtin_amdgcn_sched_barrier(0);
+      vreads(t, 1, vr1);
+      if (!(EXP & 2) && more) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[1][r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) sacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[1][s], qf[s], sacc[1], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // V^T kb0
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(EXP & 2)) pv_mfma(0, vr0);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // V^T kb1
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(EXP & 2)) pv_mfma(1, vr1);
+    } else {
+      vreads(t, 0, vr0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(EXP & 2) && t + 1 < nt) qk(t + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      vreads(t, 1, vr1);
+      if (!(EXP & 2)) pv_mfma(0, vr0);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(EXP & 2)) pv_mfma(1, vr1);
+    }
     if (grp == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");  // tile t+2 landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    stamp();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     // ---- V segment: softmax of S(t+1)
-    if (t + 1 < nt) softmax(t + 1);
+    stamp();
+    if (!(EXP & 1) && t + 1 < nt) softmax(t + 1);
     if (grp == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");  // tile t+2 landed
     __builtin_amdgcn_sched_barrier(0);
+    stamp();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();  // un-stagger: equal barrier counts on exit
+  __builtin_amdgcn_s_setprio(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the over-issued tail DMA before exit
 
   // ---- epilogue
@@ -347,6 +423,27 @@ void launch_flash2(const AttnArgs& a, hipStream_t s) {
     if (a.causal) flash2_kernel<64, true><<<grid, 512, lds, s>>>(a);
     else flash2_kernel<64, false><<<grid, 512, lds, s>>>(a);
   }
+}
+
+// Lab entry: copy the EXP & 4 stamps ([2][2048] s_memtime values) to the host.
+void flash2_read_stamps(unsigned long long* host) {
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_f2_stamps), sizeof(g_f2_stamps));
+}
+
+// Lab entry (tools/gemm_lab/attn_lab.cpp): diagnostic variant EXP of the non-causal kernel.
+void launch_flash2_exp(const AttnArgs& a, int exp, hipStream_t s) {
+  dim3 grid((a.Sq + 255) / 256, a.Hq, a.B);
+  const size_t lds = (size_t)4 * 2 * 64 * a.D * sizeof(bf16_t);
+#define SHAI_F2X(E)                                                          \
+  case E:                                                                    \
+    if (a.D == 128) flash2_kernel<128, false, E><<<grid, 512, lds, s>>>(a);  \
+    else flash2_kernel<64, false, E><<<grid, 512, lds, s>>>(a);              \
+    break;
+  switch (exp) {
+    SHAI_F2X(0) SHAI_F2X(1) SHAI_F2X(2) SHAI_F2X(4) SHAI_F2X(8) SHAI_F2X(12)
+    default: break;
+  }
+#undef SHAI_F2X
 }
 
 }  // namespace shai
