@@ -91,6 +91,10 @@ int max_splits_for(const shai::GemmArgs& g) {
 
 // Choice.cfg of the skinny streaming kernel (csrc/kernels/gemv.hip); Choice.splits = its K-group count
 constexpr int kSkinnyCfg = 1000;
+// same kernel, split-K partials reduced inside the launch by the last-arriving K group of each tile
+// (no separate fold kernel); tuned against the fold form per shape
+constexpr int kSkinnyFixCfg = 1100;
+inline bool is_skinny(int cfg) { return cfg == kSkinnyCfg || cfg == kSkinnyFixCfg; }
 
 // Last resort when neither the tuner nor the planner produced a usable config: the highest-numbered
 // config that supports the problem (the v2 128x64 tile supports everything v2 runs).
@@ -106,7 +110,7 @@ bool stream_capturing() {
   return cs != hipStreamCaptureStatusNone;
 }
 
-void launch_skinny_choice(const shai::GemmArgs& g, const Tensor& like, int kg) {
+void launch_skinny_choice(const shai::GemmArgs& g, const Tensor& like, int kg, bool fixup) {
   Tensor ws;
   float* wsp = nullptr;
   const size_t bytes = shai::skinny_workspace_bytes_kg(g, kg);
@@ -114,7 +118,7 @@ void launch_skinny_choice(const shai::GemmArgs& g, const Tensor& like, int kg) {
     ws = at::empty({(long)(bytes / sizeof(float))}, like.options().dtype(at::kFloat));
     wsp = ws.data_ptr<float>();
   }
-  shai::launch_skinny_kg(g, wsp, kg, stream());
+  shai::launch_skinny_kg(g, wsp, kg, stream(), fixup);
 }
 
 // Choice.cfg of the library path: plain GEMMs (no fused epilogue beyond a bias or an unscaled residual) may
@@ -149,8 +153,8 @@ void launch_choice(const shai::GemmArgs& g, const Tensor& like, Choice c) {
     shai::gemm2_plan(g, &c.cfg, &c.splits);
     if (!shai::gemm2_cfg_supported(g, c.cfg)) c = fallback_choice(g);
   }
-  if (c.cfg == kSkinnyCfg) {
-    launch_skinny_choice(g, like, c.splits);
+  if (is_skinny(c.cfg)) {
+    launch_skinny_choice(g, like, c.splits, c.cfg == kSkinnyFixCfg);
     return;
   }
   Tensor ws;
@@ -185,7 +189,10 @@ Choice tune(const shai::GemmArgs& g_real, const Tensor& like, bool skinny_only =
     }
   }
   if (shai::skinny_supported(g))
-    for (int kg = 1; kg <= shai::skinny_max_kgroups(g); kg *= 2) cands.push_back({kSkinnyCfg, kg});
+    for (int kg = 1; kg <= shai::skinny_max_kgroups(g); kg *= 2) {
+      cands.push_back({kSkinnyCfg, kg});
+      if (kg > 1) cands.push_back({kSkinnyFixCfg, kg});
+    }
   // residual epilogues are in place (C aliases the residual): timing them into the scratch output is not
   // equivalent, so only bias-or-nothing problems race the library
   if (!skinny_only && lib_enabled() && lib_supported(g_real) && !g_real.residual) cands.push_back({kLibCfg, 1});
@@ -220,7 +227,7 @@ void run_skinny(const shai::GemmArgs& g, const Tensor& like) {
   {
     std::lock_guard<std::mutex> lk(g_tune_mu);
     auto it = g_tuned.find(key);
-    if (it != g_tuned.end() && it->second.cfg == kSkinnyCfg) c = it->second;
+    if (it != g_tuned.end() && is_skinny(it->second.cfg)) c = it->second;
   }
   if (c.cfg < 0) {
     if (!stream_capturing() && autotune_enabled()) {
@@ -278,8 +285,9 @@ std::vector<std::string> gemm_tuning_table() {
   std::lock_guard<std::mutex> lk(g_tune_mu);
   std::vector<std::string> out;
   for (auto& kv : g_tuned) {
-    if (kv.second.cfg == kSkinnyCfg) {
-      out.push_back(kv.first + " -> skinny kg=" + std::to_string(kv.second.splits));
+    if (is_skinny(kv.second.cfg)) {
+      out.push_back(kv.first + " -> skinny kg=" + std::to_string(kv.second.splits) +
+                    (kv.second.cfg == kSkinnyFixCfg ? " (in-kernel fixup)" : ""));
       continue;
     }
     if (kv.second.cfg == kLibCfg) {
@@ -568,17 +576,24 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
       g.rms = 1;
       g.rms_eps = (float)rms_eps;
     }
-    SHAI_CHECK(force_cfg < 0 || (force_cfg >= kSkinnyCfg && force_cfg <= kSkinnyCfg + 64),
-               "fp8 gemm: force_cfg must be 1000 (+ kg, 1 <= kg <= 64): only the skinny kernel takes fp8 weights");
-    if (force_cfg > kSkinnyCfg) launch_choice(g, a, Choice{kSkinnyCfg, (int)(force_cfg - kSkinnyCfg)});
+    SHAI_CHECK(force_cfg < 0 || (force_cfg >= kSkinnyCfg && force_cfg <= kSkinnyCfg + 64) ||
+                   (force_cfg > kSkinnyFixCfg && force_cfg <= kSkinnyFixCfg + 64),
+               "fp8 gemm: force_cfg must be 1000 (+ kg) or 1100 + kg (1 <= kg <= 64): only the skinny kernel takes "
+               "fp8 weights");
+    if (force_cfg > kSkinnyFixCfg) launch_choice(g, a, Choice{kSkinnyFixCfg, (int)(force_cfg - kSkinnyFixCfg)});
+    else if (force_cfg > kSkinnyCfg) launch_choice(g, a, Choice{kSkinnyCfg, (int)(force_cfg - kSkinnyCfg)});
     else run_skinny(g, a);
     return;
   }
   const long a_bytes = (batched ? (long)a.size(0) * a.stride(0) : (long)g.M * g.lda) * 2;
   // tests / tools bypass the tuner: force_cfg = gemm2 config, 1000 = skinny kernel (heuristic K groups),
-  // 1000 + kg = skinny kernel with kg K groups
+  // 1000 + kg = skinny kernel with kg K groups (separate fold), 1100 + kg = the same with the in-kernel fixup
   const bool force_skinny = force_cfg >= kSkinnyCfg && force_cfg != kLibCfg;
-  const int force_kg = force_cfg > kSkinnyCfg ? (int)(force_cfg - kSkinnyCfg) : shai::skinny_kgroups(g);
+  const bool force_fix = force_cfg > kSkinnyFixCfg && force_cfg != kLibCfg;
+  const int force_kg = force_fix ? (int)(force_cfg - kSkinnyFixCfg)
+                       : force_cfg > kSkinnyCfg ? (int)(force_cfg - kSkinnyCfg)
+                                                : shai::skinny_kgroups(g);
+  const int force_skcfg = force_fix ? kSkinnyFixCfg : kSkinnyCfg;
   if (rms_eps >= 0) {
     // RMSNorm(a) folded in (norm gain pre-multiplied into w): fused into the skinny kernel for
     // decode-shaped problems, otherwise an explicit unweighted RMSNorm pass feeds the GEMM.
@@ -586,7 +601,7 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
     if (shai::skinny_supported(g) && (force_cfg < 0 || force_skinny)) {
       g.rms = 1;
       g.rms_eps = (float)rms_eps;
-      if (force_skinny) launch_choice(g, a, Choice{kSkinnyCfg, force_kg});
+      if (force_skinny) launch_choice(g, a, Choice{force_skcfg, force_kg});
       else run_skinny(g, a);
       return;
     }
@@ -615,7 +630,7 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
     if (force_skinny) {
       SHAI_CHECK(shai::skinny_supported(g) && force_kg >= 1 && force_kg <= 64,
                  "skinny kernel does not support this problem");
-      launch_choice(g, a, Choice{kSkinnyCfg, force_kg});
+      launch_choice(g, a, Choice{force_skcfg, force_kg});
     } else {
       SHAI_CHECK(force_cfg < shai::gemm2_num_cfgs() && shai::gemm2_cfg_supported(g, force_cfg), "bad force_cfg");
       launch_choice(g, a, Choice{(int)force_cfg, 1});
@@ -943,7 +958,7 @@ int64_t gemm_tuning_import(const std::vector<std::string>& entries) {
     if (eq == std::string::npos || cm == std::string::npos || cm < eq) continue;
     const int cfg = atoi(e.substr(eq + 1, cm - eq - 1).c_str());
     const int sp = atoi(e.substr(cm + 1).c_str());
-    if ((cfg < 0 || cfg >= shai::gemm2_num_cfgs()) && cfg != kSkinnyCfg && cfg != kLibCfg) continue;
+    if ((cfg < 0 || cfg >= shai::gemm2_num_cfgs()) && !is_skinny(cfg) && cfg != kLibCfg) continue;
     if (cfg == kLibCfg && !lib_enabled()) continue;
     if (sp < 1) continue;
     g_tuned[e.substr(0, eq)] = Choice{cfg, sp};

@@ -32,6 +32,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <cstdlib>
+
 namespace shai {
 
 typedef __bf16 bf16x8s __attribute__((ext_vector_type(8)));
@@ -59,6 +61,14 @@ __device__ __forceinline__ int sk_swz(int row, int ch) { return row * SK_BK + ((
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t sk_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+// write-through (sc1) 4-byte store / load for the in-kernel split-K hand-off (cache policy bit sc1 = 16)
+__device__ __forceinline__ void sk_store_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)off, 0, 16);
+}
+__device__ __forceinline__ float sk_load_wt(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 16));
 }
 
 template <int PER, int N>
@@ -134,7 +144,7 @@ __device__ __forceinline__ int sk_f8_off(int row, int c8) {
 
 template <int MB, bool GLU, int ACT, bool RMS, bool F8>
 __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmArgs p, float* __restrict__ ws,
-                                                                    int kg_steps) {
+                                                                    int kg_steps, unsigned* __restrict__ cnt) {
   using G = SkGeom<MB, F8>;
   constexpr int XG = G::XG;
   extern __shared__ __attribute__((aligned(16))) bf16_t sk_smem[];
@@ -288,12 +298,84 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
     sk_epilogue<MB, GLU, ACT>(p, n0, wsum);
     return;
   }
+  if (cnt != nullptr) {
+    // ---- split-K fixed up in this launch (no reduce kernel, no fences): every K group writes its 64 x MB
+    // partial slab (+ MB row sums of squares) write-through (sc1), drains (vmcnt 0 in every wave), joins
+    // the workgroup barrier, then one lane takes a ticket (relaxed agent atomic); the workgroup that draws
+    // KG-1 re-arms the ticket and reduces the KG slabs with sc1 loads before the fused epilogue.
+    // (MI355X_MICROARCH / hip guide "Projection GEMM at M = 256" item 2, write-through form.)
+    constexpr int SLAB = 64 * MB + MB, PT = 64 * MB / 256;
+    const __amdgpu_buffer_rsrc_t rws = sk_rsrc(ws, 0x7fffffffu);
+    const uint32_t tile_base = (uint32_t)((long)tile * KG * SLAB * 4);
+    const uint32_t my_base = tile_base + (uint32_t)(kg * SLAB * 4);
+    float part[PT];  // element idx = tid + 256 it <-> (m = idx >> 6, nl = idx & 63), kept for the fixup
+#pragma unroll
+    for (int it = 0; it < PT; ++it) {
+      const int idx = tid + it * 256;
+      part[it] = wsum(idx & 63, idx >> 6);
+      sk_store_wt(rws, my_base + idx * 4, part[it]);
+    }
+    float ssv = 0.f;
+    if constexpr (RMS) {
+      if (tid < MB) {
+        ssv = row_ss(tid);
+        sk_store_wt(rws, my_base + (64 * MB + tid) * 4, ssv);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ unsigned sk_last;
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sk_last = old == (unsigned)(KG - 1);
+    }
+    __syncthreads();
+    if (sk_last == 0u) return;
+    if (tid == 0) __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // add the other KG-1 slabs, four at a time with every load issued before the first add
+    // (the padding lanes of the last group re-read this group's own slab and drop it)
+    for (int u0 = 0; u0 < KG - 1; u0 += 4) {
+      float t[4][PT], ts[4];
+      bool ok[4];
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) {
+        const int u = u0 + uu;
+        ok[uu] = u < KG - 1;
+        const int q = !ok[uu] ? kg : (u < kg ? u : u + 1);
+        const uint32_t b = tile_base + (uint32_t)(q * SLAB * 4);
+#pragma unroll
+        for (int it = 0; it < PT; ++it) t[uu][it] = sk_load_wt(rws, b + (tid + it * 256) * 4);
+        ts[uu] = 0.f;
+        if constexpr (RMS) ts[uu] = sk_load_wt(rws, b + (64 * MB + (tid & (MB - 1))) * 4);
+      }
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) {
+        if (ok[uu]) {
+#pragma unroll
+          for (int it = 0; it < PT; ++it) part[it] += t[uu][it];
+          ssv += ts[uu];
+        }
+      }
+    }
+    if constexpr (RMS) {
+      if (tid < MB) rstd_s[tid] = rsqrtf(ssv / p.K + p.rms_eps);
+    }
+    float* sum = reinterpret_cast<float*>(sk_smem);  // the reduction image is dead past the ticket barrier
+#pragma unroll
+    for (int it = 0; it < PT; ++it) sum[tid + it * 256] = part[it];
+    __syncthreads();
+    auto fsum = [&](int nl, int m) {
+      float v = sum[m * 64 + nl];
+      if constexpr (RMS) v *= rstd_s[m];
+      return v;
+    };
+    sk_epilogue<MB, GLU, ACT>(p, n0, fsum);
+    return;
+  }
   if constexpr (RMS) {  // row sum-of-squares partials for the fold (one tile per K group writes them)
     if (tile == 0 && tid < p.M) ws[(long)KG * p.M * p.N + (long)kg * p.M + tid] = row_ss(tid);
   }
   // ---- split-K over workgroups: fp32 partials [kg][M][N]; launch_splitk_epilogue folds them.
-  // (An in-kernel last-arrival fixup needs a device-scope release per workgroup, i.e. an
-  // L2 writeback on this chip, and measured ~5x slower than the separate fold.)
   float* part = ws + (long)kg * p.M * p.N;
 #pragma unroll
   for (int it = 0; it < 64 * MB / 256; ++it) {
@@ -348,7 +430,11 @@ int skinny_kgroups(const GemmArgs& a) {
 }
 
 size_t skinny_workspace_bytes_kg(const GemmArgs& a, int kg) {
-  return kg > 1 ? ((size_t)kg * a.M * a.N + (a.rms ? (size_t)kg * a.M : 0)) * sizeof(float) : 0;
+  if (kg <= 1) return 0;
+  const size_t fold = (size_t)kg * a.M * a.N + (a.rms ? (size_t)kg * a.M : 0);    // [kg][M][N] + row sums
+  const int MB = a.M <= 32 ? 32 : 64;
+  const size_t fix = (size_t)((a.N + SK_BN - 1) / SK_BN) * kg * (64 * MB + MB);  // [tile][kg] slabs
+  return (fold > fix ? fold : fix) * sizeof(float);
 }
 
 size_t skinny_workspace_bytes(const GemmArgs& a) { return skinny_workspace_bytes_kg(a, skinny_kgroups(a)); }
@@ -360,16 +446,33 @@ int skinny_max_kgroups(const GemmArgs& a) {
   return kg;
 }
 
+// Per-device arrival tickets of the in-kernel split-K fixup: zeroed once, re-armed by every last arriver.
+constexpr int kSkTickets = 4096;
+static unsigned* sk_tickets(hipStream_t s) {
+  static unsigned* tickets[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (tickets[dev] == nullptr) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;  // never allocate inside a graph capture
+    unsigned* p = nullptr;
+    if (hipMalloc(&p, kSkTickets * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, kSkTickets * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
+    tickets[dev] = p;
+  }
+  return tickets[dev];
+}
+
 template <int MB, bool F8>
-static void launch_skinny_mb(const GemmArgs& a, float* ws, int kg, hipStream_t s) {
+static void launch_skinny_mb(const GemmArgs& a, float* ws, int kg, unsigned* cnt, hipStream_t s) {
   const int ksteps = (a.K + SK_BK - 1) / SK_BK;
   const int kg_steps = (ksteps + kg - 1) / kg;
   dim3 grid((a.N + SK_BN - 1) / SK_BN, kg), block(SK_WAVES * 64);
   const size_t lds = SkGeom<MB, F8>::LDS;
 #define SK(G, A)                                                                                  \
   do {                                                                                            \
-    if (a.rms) skinny_gemm_kernel<MB, G, A, true, F8><<<grid, block, lds, s>>>(a, ws, kg_steps);  \
-    else skinny_gemm_kernel<MB, G, A, false, F8><<<grid, block, lds, s>>>(a, ws, kg_steps);       \
+    if (a.rms) skinny_gemm_kernel<MB, G, A, true, F8><<<grid, block, lds, s>>>(a, ws, kg_steps, cnt);  \
+    else skinny_gemm_kernel<MB, G, A, false, F8><<<grid, block, lds, s>>>(a, ws, kg_steps, cnt);       \
   } while (0)
 #define SK_ACT(G)                                      \
   switch (a.act) {                                     \
@@ -390,18 +493,21 @@ static void launch_skinny_mb(const GemmArgs& a, float* ws, int kg, hipStream_t s
 }
 
 // kg K groups (split-K over workgroups; needs ws of skinny_workspace_bytes_kg, else kg = 1)
-void launch_skinny_kg(const GemmArgs& a, float* ws, int kg, hipStream_t s) {
+void launch_skinny_kg(const GemmArgs& a, float* ws, int kg, hipStream_t s, bool fixup) {
   const int ksteps = (a.K + SK_BK - 1) / SK_BK;
   if (ws == nullptr || kg < 1) kg = 1;
   if (kg > ksteps) kg = ksteps;
+  // split-K: fixed up inside the launch when asked for and tickets are available, else a separate fold
+  unsigned* cnt = nullptr;
+  if (kg > 1 && fixup && (a.N + SK_BN - 1) / SK_BN <= kSkTickets) cnt = sk_tickets(s);
   if (a.w_scale) {
-    if (a.M <= 32) launch_skinny_mb<32, true>(a, ws, kg, s);
-    else launch_skinny_mb<64, true>(a, ws, kg, s);
+    if (a.M <= 32) launch_skinny_mb<32, true>(a, ws, kg, cnt, s);
+    else launch_skinny_mb<64, true>(a, ws, kg, cnt, s);
   } else {
-    if (a.M <= 32) launch_skinny_mb<32, false>(a, ws, kg, s);
-    else launch_skinny_mb<64, false>(a, ws, kg, s);
+    if (a.M <= 32) launch_skinny_mb<32, false>(a, ws, kg, cnt, s);
+    else launch_skinny_mb<64, false>(a, ws, kg, cnt, s);
   }
-  if (kg > 1) launch_splitk_epilogue(a, ws, kg, s);
+  if (kg > 1 && cnt == nullptr) launch_splitk_epilogue(a, ws, kg, s);
 }
 
 void launch_skinny(const GemmArgs& a, float* ws, hipStream_t s) {

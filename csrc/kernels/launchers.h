@@ -139,7 +139,7 @@ int skinny_max_kgroups(const GemmArgs& a);    // largest K-group count worth try
 size_t skinny_workspace_bytes(const GemmArgs& a);
 size_t skinny_workspace_bytes_kg(const GemmArgs& a, int kg);
 void launch_skinny(const GemmArgs& a, float* ws, hipStream_t s);
-void launch_skinny_kg(const GemmArgs& a, float* ws, int kg, hipStream_t s);
+void launch_skinny_kg(const GemmArgs& a, float* ws, int kg, hipStream_t s, bool fixup = false);
 void gemm2_cfg_info(int cfg, int* bm, int* bn);
 
 // ---------------------------------------------------------------- attention

@@ -187,19 +187,24 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 def gemm_into(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias=None, act=None, residual=None, gate=None,
               rows_per_gate: int = 1, alpha: float = 1.0, res_alpha: float = 1.0, glu: bool = False,
-              force_cfg: int = -1, rms_eps: float = -1.0) -> torch.Tensor:
+              force_cfg: int = -1, rms_eps: float = -1.0, w_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = gate[row // rows_per_gate] * act(alpha * x @ w^T + bias) + res_alpha * residual, written into ``out``.
     rms_eps >= 0: x is RMS-normalised first (unweighted; fold the gain into w).
+    w_scale: fp8 e4m3 ``w`` with per-row scales (skinny kernel only, as in ``linear``).
+    force_cfg (tests / tools): a tile config index, 1000 (+ kg) = skinny kernel with a separate split-K fold,
+    1100 + kg = skinny kernel reducing its K groups inside the launch, 2000 = hipBLASLt.
 
     x / out / residual are 2D [M, *] or 3D [B, M, *] views whose rows may be strided
     (e.g. the text / image halves of a joint-sequence buffer); the row index used
     for ``gate`` is the flattened b * M + m (AdaLN-Zero gates per image)."""
     if not _gpu(x):
+        if w_scale is not None:
+            w = dequant_fp8(w, w_scale)
         if rms_eps >= 0:
             x = ref.rmsnorm(x, None, rms_eps)[0]
         return ref.gemm_into(x, w, out, bias, act, residual, gate, rows_per_gate, alpha, res_alpha, glu)
     _K().gemm(x, w, out, bias, None, 1, residual, float(alpha), float(res_alpha), act_id(act), bool(glu), gate,
-              int(rows_per_gate), int(force_cfg), float(rms_eps))
+              int(rows_per_gate), int(force_cfg), float(rms_eps), w_scale)
     return out
 
 

@@ -55,6 +55,21 @@ def test_fp8_skinny_glu_rms(cuda, M):
     assert _rel(y, want) < 2e-2
 
 
+@pytest.mark.parametrize("cfg", [1004, 1104, 1108])
+def test_fp8_skinny_forced_k_groups(cuda, cfg):
+    """fp8 weights with split-K: separate fold (1000 + kg) and in-kernel fixup (1100 + kg), GLU + RMS."""
+    torch.manual_seed(cfg)
+    M, K, N = 48, 4096, 2 * 1024
+    x = torch.randn(M, K, device=cuda).bfloat16() * 3
+    w8, sc = ops.quantize_fp8_rows(torch.randn(N, K, device=cuda) / K ** 0.5)
+    wd = w8.float() * sc[:, None]
+    out = torch.empty(M, N // 2, device=cuda, dtype=torch.bfloat16)
+    ops.gemm_into(x, w8, out, act="silu", glu=True, rms_eps=1e-5, w_scale=sc, force_cfg=cfg)
+    xf = x.float()
+    h = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)) @ wd.t()
+    assert _rel(out, h[:, 0::2] * torch.nn.functional.silu(h[:, 1::2])) < 2e-2
+
+
 def test_fp8_large_m_dequant_path(cuda):
     """Prefill-shaped problems (M > 64) dequantise to bf16 and use the bf16 GEMMs."""
     torch.manual_seed(3)

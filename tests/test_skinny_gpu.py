@@ -6,6 +6,7 @@ from shai_amd import ops
 
 pytestmark = pytest.mark.gpu
 SKINNY = 1000
+SKINNY_FIX = 1100
 
 
 def _rel(a, b):
@@ -43,17 +44,19 @@ def test_skinny_glu_and_act(cuda, act, M):
     assert _rel(out2, f(y)) < 1e-2
 
 
+@pytest.mark.parametrize("fix", [False, True])
 @pytest.mark.parametrize("kg", [1, 2, 4, 8, 16])
 @pytest.mark.parametrize("M,N,K,rms", [(32, 4096, 4096, False), (64, 4096, 14336, False), (17, 6144, 4096, True),
-                                       (64, 28672, 4096, True)])
-def test_skinny_k_groups(cuda, kg, M, N, K, rms):
-    """Every K-group count the tuner may pick (force_cfg = 1000 + kg), incl. the folded-RMSNorm epilogue."""
+                                       (64, 28672, 4096, True), (40, 2080, 4096, False)])
+def test_skinny_k_groups(cuda, fix, kg, M, N, K, rms):
+    """Every K-group count the tuner may pick, with the separate fold (force_cfg = 1000 + kg) and the
+    in-kernel last-arriver fixup (1100 + kg), incl. the folded-RMSNorm epilogue and a ragged last tile."""
     torch.manual_seed(kg + M)
     x = (torch.randn(M, K, device=cuda) * 2).bfloat16()
     w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
     b = torch.randn(N, device=cuda).bfloat16()
     out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
-    ops.gemm_into(x, w, out, b, force_cfg=SKINNY + kg, rms_eps=1e-5 if rms else -1.0)
+    ops.gemm_into(x, w, out, b, force_cfg=(SKINNY_FIX if fix else SKINNY) + kg, rms_eps=1e-5 if rms else -1.0)
     xf = x.float()
     if rms:
         xf = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)
@@ -66,15 +69,16 @@ def test_skinny_graph_replay_rearms_tickets(cuda):
     x = torch.randn(M, K, device=cuda).bfloat16()
     w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
     out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
-    ops.gemm_into(x, w, out, force_cfg=SKINNY)  # eager first: allocates tickets
+    ops.gemm_into(x, w, out, force_cfg=SKINNY_FIX + 8)  # eager first: allocates tickets
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
-        ops.gemm_into(x, w, out, force_cfg=SKINNY)
+        ops.gemm_into(x, w, out, force_cfg=SKINNY_FIX + 8)
     torch.cuda.current_stream().wait_stream(s)
     with torch.cuda.graph(g):
-        ops.gemm_into(x, w, out, force_cfg=SKINNY)
+        for _ in range(3):  # back-to-back launches reuse the same tickets
+            ops.gemm_into(x, w, out, force_cfg=SKINNY_FIX + 8)
     for i in range(5):
         x.copy_(torch.randn(M, K, device=cuda).bfloat16())
         g.replay()
