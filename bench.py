@@ -14,6 +14,8 @@ the barrier / max-reduction), so per-GPU work is fixed: weak scaling.
 ``--workload mistral``: Mistral-7B bf16 decode throughput (tokens/s) through the
 native LLM engine at TP = N (see shai_amd.engines.llm).
 
+``--workload vit``: ViT-base/16 224x224 classification images/s at batch 32 per GPU.
+
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
         python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 Prints ONE JSON line on rank 0.
@@ -239,6 +241,46 @@ def bench_mllama(args, rank, world):
     }
 
 
+def bench_vit(args, rank, world):
+    """ViT-base/16 224x224 image classification (run-vit.py; BASELINE.json config 2: batch 32 per GPU).
+    One step = one batch: uint8 images -> normalise -> 12-layer encoder -> classifier -> argmax labels on
+    the host (a HIP graph per batch size).  The reference publishes no ViT number: vs_baseline is null."""
+    import torch
+    from shai_amd.engines.encoders import ImageClassifierEngine
+    from shai_amd.models.vit import ViTConfig
+
+    eng = ImageClassifierEngine(ViTConfig.vit_base(), device="cuda", seed=rank, use_graphs=not args.no_graphs)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(rank)
+    imgs = torch.randint(0, 256, (args.batch, 224, 224, 3), device="cuda", dtype=torch.uint8, generator=g)
+    for _ in range(max(1, args.warmup)):
+        eng.logits_u8(imgs).argmax(-1).cpu()
+    lat = []
+    for _ in range(args.latency_runs):  # single-image request latency (reference semantics), untimed
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.logits_u8(imgs[:1]).argmax(-1).cpu()
+        lat.append(time.perf_counter() - t0)
+    _barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        labels = eng.logits_u8(imgs).argmax(-1).cpu()
+    _barrier(world)
+    elapsed = _max_over_ranks(time.perf_counter() - t0, world)
+    value = args.batch * args.steps * world / elapsed
+    return {
+        "metric": "ViT-base/16 224x224 images/sec (image classification)", "value": round(value, 2),
+        "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic uint8 images, random-init weights",
+        "config": {"model": "google/vit-base-patch16-224 (architecture)", "global_batch": args.batch * world,
+                   "per_gpu_batch": args.batch, "seq_len": 197, "parallelism": f"dp{world}",
+                   "hip_graphs": not args.no_graphs},
+        "p50_latency_ms_bs1": round(1000 * statistics.median(lat), 3) if lat else None,
+        "labels_in_range": bool(((labels >= 0) & (labels < 1000)).all().item()),
+    }
+
+
 def bench_mistral(args, rank, world):
     import torch
     from shai_amd.engines.llm import bench_decode_throughput
@@ -250,7 +292,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="sd21", choices=["sd21", "mistral", "flux", "mllama"])
+    ap.add_argument("--workload", default="sd21", choices=["sd21", "mistral", "flux", "mllama", "vit"])
     ap.add_argument("--batch", type=int, default=None,
                     help="per-GPU batch: images per step (sd21: 32, flux: 1) / concurrent sequences (mistral: 64, "
                          "mllama: 8)")
@@ -265,12 +307,12 @@ def main():
     ap.add_argument("--gen-len", type=int, default=128)
     args = ap.parse_args()
     if args.batch is None:  # dynamic-batching caps a serving replica would use for each workload
-        args.batch = {"sd21": 32, "mistral": 64, "flux": 1, "mllama": 8}[args.workload]
+        args.batch = {"sd21": 32, "mistral": 64, "flux": 1, "mllama": 8, "vit": 32}[args.workload]
     import torch
     rank, world, local = _dist_init(args.gpus)
     with torch.inference_mode():
         fn = {"sd21": bench_sd21, "mistral": bench_mistral, "flux": bench_flux,
-              "mllama": bench_mllama}[args.workload]
+              "mllama": bench_mllama, "vit": bench_vit}[args.workload]
         res = fn(args, rank, world)
     if rank == 0:
         print(json.dumps(res), flush=True)

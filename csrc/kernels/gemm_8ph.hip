@@ -31,7 +31,15 @@
 //   inside one filter tap and one source tensor, so only (ih, iw) of the lane's 4 rows change per tile.
 // * Range-checked buffer descriptors give the zero fill (M/N/K tails, conv padding); XCD-aware
 //   bijective block remap + grouped M ordering.
+// * Persistent form (VAR bit 3, configs kV4Cfg + 2 / + 3): one workgroup per CU walks output tiles
+//   blockIdx.x + i * gridDim.x (gridDim.x % 8 == 0 keeps every tile of a workgroup on its XCD).  After
+//   a tile's last K-step both LDS buffers are free, so the first K-tile of the NEXT tile is put in flight
+//   before this tile's epilogue runs: on low-K problems (K = 320..1280, 5-20 K-tiles) the
+//   epilogue's residual reads / activation / stores overlap the next tile's operand fetch instead of
+//   leaving the matrix pipe idle for a full HBM round trip per tile.
 #include "gemm_epilogue.h"
+
+#include <algorithm>
 
 namespace shai {
 
@@ -64,6 +72,7 @@ __device__ __forceinline__ void g4_glds(__amdgpu_buffer_rsrc_t r, bf16_t* lds, u
 //   bit 0: no stagger (both wave groups in lockstep)
 //   bit 1: static priority (waves 4-7 at prio 1 for the whole loop) instead of per-segment setprio
 //   bit 2: LDS-DMA issued over phases 0-1 (halves) instead of over phases 0-2 (quarter, half, quarter)
+//   bit 3: persistent tile loop with the next tile's first K-tile prefetched under the epilogue
 // Phase p of a K-tile issues the DMA instructions g in [G_p, G_{p+1}) of the next tile.
 template <int VAR, int GT>
 struct G4Sched {
@@ -79,7 +88,7 @@ struct G4ConvPos {
 // CONV: 0 plain GEMM, 1 implicit-GEMM conv, 2 implicit-GEMM conv over a nearest-2x upsampled input.
 template <int CONV, bool GLU, int ACT, bool SPLITK, int VAR, int BN>
 __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __restrict__ ws, int k_per_split) {
-  constexpr bool STAGGER = !(VAR & 1), STATIC_PRIO = (VAR & 2) != 0;
+  constexpr bool STAGGER = !(VAR & 1), STATIC_PRIO = (VAR & 2) != 0, PERSIST = (VAR & 8) != 0 && !SPLITK;
   constexpr int G4_STAGE = G4T<BN>::STAGE, NJ = G4T<BN>::NJ, WC = G4T<BN>::WC, NWJ = G4T<BN>::NWJ;
   constexpr int GT = G4T<BN>::GT;
   constexpr int G4_G0 = 0, G4_G1 = G4Sched<VAR, GT>::G1, G4_G2 = G4Sched<VAR, GT>::G2, G4_G3 = GT;
@@ -91,18 +100,22 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
   // ---- tile mapping (XCD remap + grouped M ordering)
   const int tiles_m = (p.M + G4_BM - 1) / G4_BM, tiles_n = (p.N + BN - 1) / BN;
   const int total = tiles_m * tiles_n;
-  int bid = blockIdx.x;
-  {
-    const int xcd = bid & 7, q = total >> 3, r = total & 7;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
-  constexpr int GROUP = 8;
-  const int group = bid / (GROUP * tiles_n);
-  const int first_m = group * GROUP;
-  const int gsize = min(tiles_m - first_m, GROUP);
-  const int in_group = bid - group * GROUP * tiles_n;
-  const int m0 = (first_m + in_group % gsize) * G4_BM;
-  const int n0 = (in_group / gsize) * BN;
+  auto tile_origin = [&](int bid, int& tm0, int& tn0) {
+    {
+      const int xcd = bid & 7, q = total >> 3, r = total & 7;
+      bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    }
+    constexpr int GROUP = 8;
+    const int group = bid / (GROUP * tiles_n);
+    const int first_m = group * GROUP;
+    const int gsize = min(tiles_m - first_m, GROUP);
+    const int in_group = bid - group * GROUP * tiles_n;
+    tm0 = (first_m + in_group % gsize) * G4_BM;
+    tn0 = (in_group / gsize) * BN;
+  };
+  int vb = blockIdx.x;  // virtual block id of the current tile (persistent: + i * gridDim.x)
+  int m0, n0;
+  tile_origin(vb, m0, n0);
   const int b = SPLITK ? 0 : blockIdx.y;
   const int kz = SPLITK ? blockIdx.y : 0;
   const int k_begin = kz * k_per_split;
@@ -123,45 +136,52 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
   // ---- staging geometry: DMA wave-instruction j fills 8 LDS rows x 128 B (lane-linear); the lane's
   // source chunk is the swizzled one.  Per-row byte offsets are precomputed; an invalid row's offset
   // carries the OOB bit, which survives the per-tile additions (< 2^31) and reads as zero fill.
-  const int lrow = lane >> 3, lpos = lane & 7;
+  const int lrow0 = lane >> 3, lpos0 = lane & 7;
   int kch[4];            // k offset of the lane's source chunk within the K-tile (A rows)
   int kchw[NWJ];         // same for the W rows
   uint32_t woff[NWJ];    // W row byte offset + chunk
   uint32_t aoff[4];      // plain GEMM: A row byte offset + chunk
   int ih0[4], iw0[4];    // conv: top-left input tap position of the output pixel (upsampled grid for CONV 2)
   int pix[4];            // conv (CONV 1): pixel index of (ih0, iw0); CONV 2: n * H
+  // per-tile row offsets for the tile at (m0, n0); cheap enough to recompute rather than hold live
+  // across the persistent loop's epilogue
+  auto setup = [&]() {
+    int lrow = lrow0, lpos = lpos0;  // opaque copies: a repeated setup() is recomputed, not CSE'd and held live
+    if constexpr (PERSIST) asm volatile("" : "+v"(lrow), "+v"(lpos));
 #pragma unroll
-  for (int j = 0; j < NWJ; ++j) {
-    const int row = wid * (BN / 8) + j * 8 + lrow;
-    kchw[j] = (lpos ^ ((row >> 1) & 7)) * 8;
-    const int n = n0 + row;
-    woff[j] = n < p.N ? (uint32_t)(((long)n * p.ldw + kchw[j]) * 2) : G4_OOB;
-  }
+    for (int j = 0; j < NWJ; ++j) kchw[j] = (lpos ^ (((wid * (BN / 8) + j * 8 + lrow) >> 1) & 7)) * 8;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = wid * 32 + j * 8 + lrow;
-    kch[j] = (lpos ^ ((row >> 1) & 7)) * 8;
-    const int m = m0 + row;
-    if constexpr (CONV == 0) {
-      aoff[j] = m < p.M ? (uint32_t)(((long)m * p.lda + kch[j]) * 2) : G4_OOB;
-    } else {
-      const int hw = p.OH * p.OW;
-      const int mm = m < p.M ? m : 0;
-      const int cn = mm / hw;
-      const int rem = mm - cn * hw;
-      const int coh = rem / p.OW, cow = rem - coh * p.OW;
-      if constexpr (CONV == 1) {
-        ih0[j] = m < p.M ? coh * p.stride - p.pad : -(1 << 24);
-        iw0[j] = cow * p.stride - p.pad;
-        pix[j] = (cn * p.H + ih0[j]) * p.Wd + iw0[j];
-      } else {
-        ih0[j] = m < p.M ? coh - p.pad : -(1 << 24);
-        iw0[j] = cow - p.pad;
-        pix[j] = cn * p.H;
-      }
-      aoff[j] = (uint32_t)kch[j] * 2;
+    for (int j = 0; j < 4; ++j) kch[j] = (lpos ^ (((wid * 32 + j * 8 + lrow) >> 1) & 7)) * 8;
+#pragma unroll
+    for (int j = 0; j < NWJ; ++j) {
+      const int n = n0 + wid * (BN / 8) + j * 8 + lrow;
+      woff[j] = n < p.N ? (uint32_t)(((long)n * p.ldw + kchw[j]) * 2) : G4_OOB;
     }
-  }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + wid * 32 + j * 8 + lrow;
+      if constexpr (CONV == 0) {
+        aoff[j] = m < p.M ? (uint32_t)(((long)m * p.lda + kch[j]) * 2) : G4_OOB;
+      } else {
+        const int hw = p.OH * p.OW;
+        const int mm = m < p.M ? m : 0;
+        const int cn = mm / hw;
+        const int rem = mm - cn * hw;
+        const int coh = rem / p.OW, cow = rem - coh * p.OW;
+        if constexpr (CONV == 1) {
+          ih0[j] = m < p.M ? coh * p.stride - p.pad : -(1 << 24);
+          iw0[j] = cow * p.stride - p.pad;
+          pix[j] = (cn * p.H + ih0[j]) * p.Wd + iw0[j];
+        } else {
+          ih0[j] = m < p.M ? coh - p.pad : -(1 << 24);
+          iw0[j] = cow - p.pad;
+          pix[j] = cn * p.H;
+        }
+        aoff[j] = (uint32_t)kch[j] * 2;
+      }
+    }
+  };
+  setup();
   const int cs_a = p.A2 ? p.Cin1 : p.Cin;  // channel stride (elements per pixel) of source A / A2
   const int cs_b = p.Cin - p.Cin1;
 
@@ -224,190 +244,221 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
     }
   };
 
-  float4_ acc[8][NJ];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
-
   const int fr = lane & 15, fq = lane >> 4;
   const int nk = k_end > k_begin ? (k_end - k_begin + G4_BK - 1) / G4_BK : 0;
 
-  // prologue: tile 0 -> buffer 0
+  // prologue: K-tile 0 of the first output tile -> buffer 0
   G4ConvPos cpos = conv_pos(k_begin);
   if (nk > 0) {
 #pragma unroll
     for (int g = 0; g < GT; ++g) stage_one(0, k_begin, cpos, g);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (STAGGER && wm == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs half a phase behind
-  if (STATIC_PRIO && wm == 1) __builtin_amdgcn_s_setprio(1);
-  __builtin_amdgcn_sched_barrier(0);
-
   bf16x8q wf[NJ], xf[4];
-  for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
-    const bool pre = t + 1 < nk;
-    const int knext = k_begin + (t + 1) * G4_BK;
-    conv_advance(cpos);  // position of tile t + 1
-    const bf16_t* sa = g4_smem + cur * G4_STAGE;
-    const bf16_t* sw = sa + G4_BM * G4_BK;
-#pragma unroll
-    for (int ph = 0; ph < 4; ++ph) {
-      const int ks = ph >> 1, mh = ph & 1;
-      // ---- load segment
-      const int g_lo = ph == 0 ? G4_G0 : ph == 1 ? G4_G1 : ph == 2 ? G4_G2 : G4_G3;
-      const int g_hi = ph == 0 ? G4_G1 : ph == 1 ? G4_G2 : ph == 2 ? G4_G3 : GT;
-      if (pre) {
-#pragma unroll
-        for (int g = g_lo; g < g_hi; ++g) stage_one(cur ^ 1, knext, cpos, g);
-      }
-      if (mh == 0) {
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          wf[j] = *reinterpret_cast<const bf16x8q*>(sw + g4_swz(wn * WC + j * 16 + fr, ks * 4 + fq));
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        xf[i] = *reinterpret_cast<const bf16x8q*>(sa + g4_swz(wm * 128 + (mh * 4 + i) * 16 + fr, ks * 4 + fq));
-      if (ph == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t+1 landed
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      // ---- compute segment
-      if (!STATIC_PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          acc[mh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[mh * 4 + i][j], 0, 0, 0);
-      if (!STATIC_PRIO) __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  if (STATIC_PRIO) __builtin_amdgcn_s_setprio(0);
-  if (STAGGER && wm == 0) __builtin_amdgcn_s_barrier();  // un-stagger: equal barrier counts on exit
+  while (true) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (STAGGER && wm == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs half a phase behind
+    if (STATIC_PRIO && wm == 1) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_sched_barrier(0);
 
-  // ---- epilogue: D[n][m] blocks -> lane owns row m = fr, columns n..n+3 = 4 fq + reg
-  if constexpr (SPLITK) {
-    float* Wp = ws + (long)kz * p.M * p.N;
+    float4_ acc[8][NJ];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0 + wm * 128 + i * 16 + fr;
-      if (m >= p.M) continue;
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int n = n0 + wn * WC + j * 16 + 4 * fq;
-        if (n + 3 < p.N) {
-          *reinterpret_cast<float4_*>(Wp + (long)m * p.N + n) = acc[i][j];
-        } else {
-          for (int e = 0; e < 4 && n + e < p.N; ++e) Wp[(long)m * p.N + n + e] = acc[i][j][e];
+      for (int j = 0; j < NJ; ++j) acc[i][j] = float4_{0.f, 0.f, 0.f, 0.f};
+    // fragment-read lane coordinates made opaque per output tile: the ds_read addresses derived from them
+    // are then rebuilt per tile instead of being hoisted out of the persistent loop and held live
+    // (about 30 registers) across the epilogue
+    int frl = fr, fql = fq;
+    if constexpr (PERSIST) asm volatile("" : "+v"(frl), "+v"(fql));
+
+    for (int t = 0; t < nk; ++t) {
+      const int cur = t & 1;
+      const bool pre = t + 1 < nk;
+      const int knext = k_begin + (t + 1) * G4_BK;
+      conv_advance(cpos);  // position of tile t + 1
+      const bf16_t* sa = g4_smem + cur * G4_STAGE;
+      const bf16_t* sw = sa + G4_BM * G4_BK;
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) {
+        const int ks = ph >> 1, mh = ph & 1;
+        // ---- load segment
+        const int g_lo = ph == 0 ? G4_G0 : ph == 1 ? G4_G1 : ph == 2 ? G4_G2 : G4_G3;
+        const int g_hi = ph == 0 ? G4_G1 : ph == 1 ? G4_G2 : ph == 2 ? G4_G3 : GT;
+        if (pre) {
+#pragma unroll
+          for (int g = g_lo; g < g_hi; ++g) stage_one(cur ^ 1, knext, cpos, g);
         }
+        if (mh == 0) {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            wf[j] = *reinterpret_cast<const bf16x8q*>(sw + g4_swz(wn * WC + j * 16 + frl, ks * 4 + fql));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          xf[i] = *reinterpret_cast<const bf16x8q*>(sa + g4_swz(wm * 128 + (mh * 4 + i) * 16 + frl, ks * 4 + fql));
+        if (ph == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t+1 landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- compute segment
+        if (!STATIC_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[mh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[mh * 4 + i][j], 0, 0, 0);
+        if (!STATIC_PRIO) __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
-  } else {
-    bf16_t* __restrict__ C = p.C + (long)b * p.batch_c;
-    const bf16_t* __restrict__ R = p.residual ? p.residual + (long)b * p.batch_r : nullptr;
-    const bool fast = m0 + G4_BM <= p.M && n0 + BN <= p.N && p.bias2d == nullptr && p.gate == nullptr &&
-                      (p.ldc & 3) == 0 && (R == nullptr || (p.ldr & 3) == 0);
-    if (fast) {
-      // interior tile: per-column bias hoisted, residual rows prefetched in groups of IG row blocks (all 8
-      // at NJ = 4; 2 at NJ = 5, where 160 accumulator registers leave no room for 80 more)
-      const bf16_t* __restrict__ bias = p.bias;
-      float bj[NJ][4];
+    if (STATIC_PRIO) __builtin_amdgcn_s_setprio(0);
+    if (STAGGER && wm == 0) __builtin_amdgcn_s_barrier();  // un-stagger: equal barrier counts on exit
+
+    // every wave is past its last LDS read of this tile (lgkmcnt(0) precedes each load-segment barrier):
+    // both buffers are free, so the next tile's first K-tile goes in flight under this epilogue
+    const int em0 = m0, en0 = n0;
+    bool more = false;
+    if constexpr (PERSIST) {
+      more = vb + (int)gridDim.x < total;
+      if (more) {
+        vb += gridDim.x;
+        tile_origin(vb, m0, n0);
+        setup();
+        cpos = conv_pos(k_begin);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int n = n0 + wn * WC + j * 16 + 4 * fq;
-        if (bias) {
-          const uint2_ bb = *reinterpret_cast<const uint2_*>(bias + n);
-          bj[j][0] = bf2f(bb[0] & 0xffff); bj[j][1] = bf2f(bb[0] >> 16);
-          bj[j][2] = bf2f(bb[1] & 0xffff); bj[j][3] = bf2f(bb[1] >> 16);
-        } else {
-          bj[j][0] = bj[j][1] = bj[j][2] = bj[j][3] = 0.f;
-        }
+        for (int g = 0; g < GT; ++g) stage_one(0, k_begin, cpos, g);
       }
-      constexpr int IG = NJ == 4 ? 8 : 2;
-      if constexpr (!GLU) {
-#pragma unroll
-        for (int i0 = 0; i0 < 8; i0 += IG) {
-          uint2_ rr[IG][NJ];
-          if (R) {
-#pragma unroll
-            for (int ii = 0; ii < IG; ++ii)
-#pragma unroll
-              for (int j = 0; j < NJ; ++j)
-                rr[ii][j] = *reinterpret_cast<const uint2_*>(R + (long)(m0 + wm * 128 + (i0 + ii) * 16 + fr) * p.ldr +
-                                                             n0 + wn * WC + j * 16 + 4 * fq);
-          }
-#pragma unroll
-          for (int ii = 0; ii < IG; ++ii) {
-            const int i = i0 + ii;
-            const int m = m0 + wm * 128 + i * 16 + fr;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-              const int n = n0 + wn * WC + j * 16 + 4 * fq;
-              float v[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = apply_act<ACT>(acc[i][j][e] * p.alpha + bj[j][e]);
-              if (R) {
-                v[0] += bf2f(rr[ii][j][0] & 0xffff) * p.res_alpha; v[1] += bf2f(rr[ii][j][0] >> 16) * p.res_alpha;
-                v[2] += bf2f(rr[ii][j][1] & 0xffff) * p.res_alpha; v[3] += bf2f(rr[ii][j][1] >> 16) * p.res_alpha;
-              }
-              uint2_ o;
-              o[0] = pack2(v[0], v[1]);
-              o[1] = pack2(v[2], v[3]);
-              *reinterpret_cast<uint2_*>(C + (long)m * p.ldc + n) = o;
+    }
+    auto epilogue = [&, fr0 = fr, fq0 = fq](const int m0, const int n0) {
+      // opaque lane coordinates: the epilogue's per-lane addressing is built here, not hoisted above the
+      // persistent loop's main loop where it would pin registers for the whole K sweep
+      int fr = fr0, fq = fq0;
+      if constexpr (PERSIST) asm volatile("" : "+v"(fr), "+v"(fq));
+      // ---- epilogue: D[n][m] blocks -> lane owns row m = fr, columns n..n+3 = 4 fq + reg
+      if constexpr (SPLITK) {
+        float* Wp = ws + (long)kz * p.M * p.N;
+    #pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = m0 + wm * 128 + i * 16 + fr;
+          if (m >= p.M) continue;
+    #pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const int n = n0 + wn * WC + j * 16 + 4 * fq;
+            if (n + 3 < p.N) {
+              *reinterpret_cast<float4_*>(Wp + (long)m * p.N + n) = acc[i][j];
+            } else {
+              for (int e = 0; e < 4 && n + e < p.N; ++e) Wp[(long)m * p.N + n + e] = acc[i][j][e];
             }
           }
         }
       } else {
-#pragma unroll
-        for (int i0 = 0; i0 < 8; i0 += IG) {
-          uint32_t rr[IG][NJ];
-          if (R) {
-#pragma unroll
-            for (int ii = 0; ii < IG; ++ii)
-#pragma unroll
-              for (int j = 0; j < NJ; ++j)
-                rr[ii][j] = *reinterpret_cast<const uint32_t*>(R + (long)(m0 + wm * 128 + (i0 + ii) * 16 + fr) * p.ldr +
-                                                              ((n0 + wn * WC + j * 16 + 4 * fq) >> 1));
-          }
-#pragma unroll
-          for (int ii = 0; ii < IG; ++ii) {
-            const int i = i0 + ii;
-            const int m = m0 + wm * 128 + i * 16 + fr;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-              const int nc = (n0 + wn * WC + j * 16 + 4 * fq) >> 1;
-              float o0 = (acc[i][j][0] * p.alpha + bj[j][0]) * apply_act<ACT>(acc[i][j][1] * p.alpha + bj[j][1]);
-              float o1 = (acc[i][j][2] * p.alpha + bj[j][2]) * apply_act<ACT>(acc[i][j][3] * p.alpha + bj[j][3]);
-              if (R) {
-                o0 += bf2f(rr[ii][j] & 0xffff) * p.res_alpha;
-                o1 += bf2f(rr[ii][j] >> 16) * p.res_alpha;
-              }
-              *reinterpret_cast<uint32_t*>(C + (long)m * p.ldc + nc) = pack2(o0, o1);
+        bf16_t* __restrict__ C = p.C + (long)b * p.batch_c;
+        const bf16_t* __restrict__ R = p.residual ? p.residual + (long)b * p.batch_r : nullptr;
+        const bool fast = m0 + G4_BM <= p.M && n0 + BN <= p.N && p.bias2d == nullptr && p.gate == nullptr &&
+                          (p.ldc & 3) == 0 && (R == nullptr || (p.ldr & 3) == 0);
+        if (fast) {
+          // interior tile: per-column bias hoisted, residual rows prefetched in groups of IG row blocks (all 8
+          // at NJ = 4; 2 at NJ = 5, where 160 accumulator registers leave no room for 80 more)
+          const bf16_t* __restrict__ bias = p.bias;
+          float bj[NJ][4];
+    #pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const int n = n0 + wn * WC + j * 16 + 4 * fq;
+            if (bias) {
+              const uint2_ bb = *reinterpret_cast<const uint2_*>(bias + n);
+              bj[j][0] = bf2f(bb[0] & 0xffff); bj[j][1] = bf2f(bb[0] >> 16);
+              bj[j][2] = bf2f(bb[1] & 0xffff); bj[j][3] = bf2f(bb[1] >> 16);
+            } else {
+              bj[j][0] = bj[j][1] = bj[j][2] = bj[j][3] = 0.f;
             }
+          }
+          constexpr int IG = NJ == 4 ? 8 : 2;
+          if constexpr (!GLU) {
+    #pragma unroll
+            for (int i0 = 0; i0 < 8; i0 += IG) {
+              uint2_ rr[IG][NJ];
+              if (R) {
+    #pragma unroll
+                for (int ii = 0; ii < IG; ++ii)
+    #pragma unroll
+                  for (int j = 0; j < NJ; ++j)
+                    rr[ii][j] = *reinterpret_cast<const uint2_*>(R + (long)(m0 + wm * 128 + (i0 + ii) * 16 + fr) * p.ldr +
+                                                                 n0 + wn * WC + j * 16 + 4 * fq);
+              }
+    #pragma unroll
+              for (int ii = 0; ii < IG; ++ii) {
+                const int i = i0 + ii;
+                const int m = m0 + wm * 128 + i * 16 + fr;
+    #pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                  const int n = n0 + wn * WC + j * 16 + 4 * fq;
+                  float v[4];
+    #pragma unroll
+                  for (int e = 0; e < 4; ++e) v[e] = apply_act<ACT>(acc[i][j][e] * p.alpha + bj[j][e]);
+                  if (R) {
+                    v[0] += bf2f(rr[ii][j][0] & 0xffff) * p.res_alpha; v[1] += bf2f(rr[ii][j][0] >> 16) * p.res_alpha;
+                    v[2] += bf2f(rr[ii][j][1] & 0xffff) * p.res_alpha; v[3] += bf2f(rr[ii][j][1] >> 16) * p.res_alpha;
+                  }
+                  uint2_ o;
+                  o[0] = pack2(v[0], v[1]);
+                  o[1] = pack2(v[2], v[3]);
+                  *reinterpret_cast<uint2_*>(C + (long)m * p.ldc + n) = o;
+                }
+              }
+            }
+          } else {
+    #pragma unroll
+            for (int i0 = 0; i0 < 8; i0 += IG) {
+              uint32_t rr[IG][NJ];
+              if (R) {
+    #pragma unroll
+                for (int ii = 0; ii < IG; ++ii)
+    #pragma unroll
+                  for (int j = 0; j < NJ; ++j)
+                    rr[ii][j] = *reinterpret_cast<const uint32_t*>(R + (long)(m0 + wm * 128 + (i0 + ii) * 16 + fr) * p.ldr +
+                                                                  ((n0 + wn * WC + j * 16 + 4 * fq) >> 1));
+              }
+    #pragma unroll
+              for (int ii = 0; ii < IG; ++ii) {
+                const int i = i0 + ii;
+                const int m = m0 + wm * 128 + i * 16 + fr;
+    #pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                  const int nc = (n0 + wn * WC + j * 16 + 4 * fq) >> 1;
+                  float o0 = (acc[i][j][0] * p.alpha + bj[j][0]) * apply_act<ACT>(acc[i][j][1] * p.alpha + bj[j][1]);
+                  float o1 = (acc[i][j][2] * p.alpha + bj[j][2]) * apply_act<ACT>(acc[i][j][3] * p.alpha + bj[j][3]);
+                  if (R) {
+                    o0 += bf2f(rr[ii][j] & 0xffff) * p.res_alpha;
+                    o1 += bf2f(rr[ii][j] >> 16) * p.res_alpha;
+                  }
+                  *reinterpret_cast<uint32_t*>(C + (long)m * p.ldc + nc) = pack2(o0, o1);
+                }
+              }
+            }
+          }
+          return;
+        }
+    #pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int m = m0 + wm * 128 + i * 16 + fr;
+          if (m >= p.M) continue;
+    #pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const int n = n0 + wn * WC + j * 16 + 4 * fq;
+            if (n >= p.N) continue;
+            float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+            epilogue4<GLU, ACT>(p, C, R, m, n, v, b);
           }
         }
       }
-      return;
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0 + wm * 128 + i * 16 + fr;
-      if (m >= p.M) continue;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int n = n0 + wn * WC + j * 16 + 4 * fq;
-        if (n >= p.N) continue;
-        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        epilogue4<GLU, ACT>(p, C, R, m, n, v, b);
-      }
-    }
+    };
+    epilogue(em0, en0);
+    if (!more) break;
+    setup();  // the next tile's offsets again (dead across the epilogue, so they cost no registers there)
   }
 }
 
@@ -422,16 +473,32 @@ bool gemm4_supported(const GemmArgs& a) {
   return true;
 }
 
+// persistent grid width: the CU count rounded down to a multiple of 8 (one workgroup per CU; every tile
+// of a workgroup stays on its XCD)
+static int g4_persist_width() {
+  static int w = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 8)
+      cus = 256;
+    return cus & ~7;
+  }();
+  return w;
+}
+
 template <int CONV, bool GLU, int ACT, int VAR = 4>
 static void g4_launch(const GemmArgs& a, float* ws, int splits, int kps, int bn, hipStream_t s) {
   dim3 grid(1, splits > 1 ? splits : (a.batch > 0 ? a.batch : 1));
+  const auto width = [&](long tiles) {  // persistent: at most one workgroup per CU, tiles walked in a loop
+    return (unsigned)((VAR & 8) && splits <= 1 ? std::min<long>(tiles, g4_persist_width()) : tiles);
+  };
   if (bn == 320) {
-    grid.x = ((a.M + G4_BM - 1) / G4_BM) * ((a.N + 319) / 320);
+    grid.x = width(((a.M + G4_BM - 1) / G4_BM) * ((a.N + 319) / 320));
     const size_t lds = (size_t)2 * G4T<320>::STAGE * sizeof(bf16_t);
     if (splits > 1) gemm4_kernel<CONV, GLU, ACT, true, VAR, 320><<<grid, 512, lds, s>>>(a, ws, kps);
     else gemm4_kernel<CONV, GLU, ACT, false, VAR, 320><<<grid, 512, lds, s>>>(a, ws, kps);
   } else {
-    grid.x = ((a.M + G4_BM - 1) / G4_BM) * ((a.N + 255) / 256);
+    grid.x = width(((a.M + G4_BM - 1) / G4_BM) * ((a.N + 255) / 256));
     const size_t lds = (size_t)2 * G4T<256>::STAGE * sizeof(bf16_t);
     if (splits > 1) gemm4_kernel<CONV, GLU, ACT, true, VAR, 256><<<grid, 512, lds, s>>>(a, ws, kps);
     else gemm4_kernel<CONV, GLU, ACT, false, VAR, 256><<<grid, 512, lds, s>>>(a, ws, kps);
@@ -439,33 +506,42 @@ static void g4_launch(const GemmArgs& a, float* ws, int splits, int kps, int bn,
 }
 
 // splits > 1 requires ws ([splits][M][N] fp32); the split-K fold + epilogue runs afterwards.
-void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t s) {
+template <int VAR>
+static void g4_dispatch(const GemmArgs& a, float* ws, int splits, int kps, int bn, hipStream_t s);
+
+void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t s, bool persist) {
   if (ws == nullptr) splits = 1;
   const long kt = (a.K + G4_BK - 1) / G4_BK;
   const int kps = (int)(((kt + splits - 1) / splits) * G4_BK);
+  if (persist && splits <= 1) g4_dispatch<12>(a, ws, splits, kps, bn, s);
+  else g4_dispatch<4>(a, ws, splits, kps, bn, s);
+  if (splits > 1) launch_splitk_epilogue(a, ws, splits, s);
+}
+
+template <int VAR>
+static void g4_dispatch(const GemmArgs& a, float* ws, int splits, int kps, int bn, hipStream_t s) {
   if (a.conv) {
     if (a.upsample) {
-      if (a.act == ACT_SILU) g4_launch<2, false, ACT_SILU>(a, ws, splits, kps, bn, s);
-      else g4_launch<2, false, ACT_NONE>(a, ws, splits, kps, bn, s);
+      if (a.act == ACT_SILU) g4_launch<2, false, ACT_SILU, VAR>(a, ws, splits, kps, bn, s);
+      else g4_launch<2, false, ACT_NONE, VAR>(a, ws, splits, kps, bn, s);
     } else {
-      if (a.act == ACT_SILU) g4_launch<1, false, ACT_SILU>(a, ws, splits, kps, bn, s);
-      else g4_launch<1, false, ACT_NONE>(a, ws, splits, kps, bn, s);
+      if (a.act == ACT_SILU) g4_launch<1, false, ACT_SILU, VAR>(a, ws, splits, kps, bn, s);
+      else g4_launch<1, false, ACT_NONE, VAR>(a, ws, splits, kps, bn, s);
     }
   } else if (a.glu) {
-    if (a.act == ACT_SILU) g4_launch<0, true, ACT_SILU>(a, ws, splits, kps, bn, s);
-    else if (a.act == ACT_GELU_TANH) g4_launch<0, true, ACT_GELU_TANH>(a, ws, splits, kps, bn, s);
-    else g4_launch<0, true, ACT_GELU>(a, ws, splits, kps, bn, s);
+    if (a.act == ACT_SILU) g4_launch<0, true, ACT_SILU, VAR>(a, ws, splits, kps, bn, s);
+    else if (a.act == ACT_GELU_TANH) g4_launch<0, true, ACT_GELU_TANH, VAR>(a, ws, splits, kps, bn, s);
+    else g4_launch<0, true, ACT_GELU, VAR>(a, ws, splits, kps, bn, s);
   } else {
     switch (a.act) {
-      case ACT_SILU: g4_launch<0, false, ACT_SILU>(a, ws, splits, kps, bn, s); break;
-      case ACT_GELU: g4_launch<0, false, ACT_GELU>(a, ws, splits, kps, bn, s); break;
-      case ACT_GELU_TANH: g4_launch<0, false, ACT_GELU_TANH>(a, ws, splits, kps, bn, s); break;
-      case ACT_QUICK_GELU: g4_launch<0, false, ACT_QUICK_GELU>(a, ws, splits, kps, bn, s); break;
-      case ACT_RELU: g4_launch<0, false, ACT_RELU>(a, ws, splits, kps, bn, s); break;
-      default: g4_launch<0, false, ACT_NONE>(a, ws, splits, kps, bn, s); break;
+      case ACT_SILU: g4_launch<0, false, ACT_SILU, VAR>(a, ws, splits, kps, bn, s); break;
+      case ACT_GELU: g4_launch<0, false, ACT_GELU, VAR>(a, ws, splits, kps, bn, s); break;
+      case ACT_GELU_TANH: g4_launch<0, false, ACT_GELU_TANH, VAR>(a, ws, splits, kps, bn, s); break;
+      case ACT_QUICK_GELU: g4_launch<0, false, ACT_QUICK_GELU, VAR>(a, ws, splits, kps, bn, s); break;
+      case ACT_RELU: g4_launch<0, false, ACT_RELU, VAR>(a, ws, splits, kps, bn, s); break;
+      default: g4_launch<0, false, ACT_NONE, VAR>(a, ws, splits, kps, bn, s); break;
     }
   }
-  if (splits > 1) launch_splitk_epilogue(a, ws, splits, s);
 }
 
 // Lab entry: schedule variant `var` (see G4Sched) of the plain / conv no-activation kernel, no split-K.
@@ -481,7 +557,7 @@ void launch_gemm4_var(const GemmArgs& a, int var, int bn, hipStream_t s) {
     }                                                                             \
     break;
   switch (var) {
-    SHAI_G4V(0) SHAI_G4V(4) SHAI_G4V(6)
+    SHAI_G4V(0) SHAI_G4V(4) SHAI_G4V(6) SHAI_G4V(12)
     default: break;
   }
 #undef SHAI_G4V

@@ -351,7 +351,8 @@ static const TileCfg kCfgs[] = {{256, 320, 1.00f}, {256, 256, 1.00f}, {256, 128,
                                 {128, 64, 0.55f}};
 constexpr int kNumCfgs = 5;
 // Config index space: [0, kNumCfgs) this file's tile configs; kNumCfgs + 0..3 the pipelined v3 kernel
-// (gemm_pipe.hip); kNumCfgs + 4 / + 5 the 8-phase ping-pong v4 kernel (gemm_8ph.hip) with 256 / 320 wide tiles.
+// (gemm_pipe.hip); kNumCfgs + 4 / + 5 the 8-phase ping-pong v4 kernel (gemm_8ph.hip) with 256 / 320 wide tiles,
+// kNumCfgs + 6 / + 7 the same in its persistent form (next tile's operands prefetched under the epilogue).
 constexpr int kV4Cfg = kNumCfgs + 4;
 
 
@@ -463,7 +464,8 @@ static void launch_all(const GemmArgs& a, float* ws, int cfg, int splits, hipStr
 
 void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStream_t s) {
   if (cfg >= kV4Cfg) {
-    launch_gemm4(a, ws, splits, cfg == kV4Cfg + 1 ? 320 : 256, s);
+    const int v = cfg - kV4Cfg;
+    launch_gemm4(a, ws, splits, (v & 1) ? 320 : 256, s, v >= 2);
     return;
   }
   if (cfg >= kNumCfgs) {  // pipelined kernel (gemm_pipe.hip): 256x256 / 256x320 tile, 4- / 2-stage ring
@@ -498,10 +500,10 @@ void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipS
   }
 }
 
-int gemm2_num_cfgs() { return kV4Cfg + 2; }
+int gemm2_num_cfgs() { return kV4Cfg + 4; }
 
 bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
-  if (cfg >= kV4Cfg) return cfg < kV4Cfg + 2 && gemm4_supported(a);
+  if (cfg >= kV4Cfg) return cfg < kV4Cfg + 4 && gemm4_supported(a);
   if (cfg >= kNumCfgs) return gemm3_supported(a);
   if (a.in_scale != nullptr) return false;
   if (a.conv && a.A2 != nullptr && (a.Cin % 64 != 0 || a.Cin1 % 64 != 0)) return false;  // 64-wide K tiles
@@ -509,9 +511,9 @@ bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
 }
 
 void gemm2_cfg_info(int cfg, int* bm, int* bn) {
-  if (cfg >= kV4Cfg) {  // 8-phase v4 kernel: reported as "8x-<BN>"
-    *bm = 8;
-    *bn = cfg == kV4Cfg + 1 ? -320 : -256;
+  if (cfg >= kV4Cfg) {  // 8-phase v4 kernel: reported as "8x-<BN>" ("9x-<BN>" persistent)
+    *bm = cfg >= kV4Cfg + 2 ? 9 : 8;
+    *bn = ((cfg - kV4Cfg) & 1) ? -320 : -256;
     return;
   }
   if (cfg >= kNumCfgs) {

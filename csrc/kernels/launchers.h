@@ -131,7 +131,7 @@ void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipS
 // v4: 8-phase ping-pong 256x256 / 256x320 LDS-DMA GEMM / conv (gemm_8ph.hip); config indices
 // gemm2_num_cfgs() - 2 (bn 256) and - 1 (bn 320)
 bool gemm4_supported(const GemmArgs& a);
-void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t s);
+void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t s, bool persist = false);
 // skinny (decode-shaped, M <= 64) streaming GEMM; ws: skinny_workspace_bytes (fp32 split-K partials)
 bool skinny_supported(const GemmArgs& a);
 int skinny_kgroups(const GemmArgs& a);        // heuristic K-group count

@@ -14,7 +14,7 @@ import torch
 from shai_amd import ops
 
 pytestmark = pytest.mark.gpu
-CFGS = [5, 7, 8, 9, 10]
+CFGS = [5, 7, 8, 9, 10, 11, 12]
 
 
 def _rel(a, b):
@@ -23,7 +23,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 4096, 4096), (300, 520, 200), (1000, 256, 96), (257, 1024, 2048),
-                                   (65536, 320, 320), (777, 650, 136)])
+                                   (65536, 320, 320), (777, 650, 136), (70000, 700, 192)])
 @pytest.mark.parametrize("cfg", CFGS)
 def test_gemm3_plain_bias_residual(cuda, M, N, K, cfg):
     torch.manual_seed(M)
@@ -69,7 +69,9 @@ cases = [(2, 32, 32, 64, 128, 3, 1, 1, False, 0), (2, 16, 16, 320, 320, 3, 1, 1,
          (1, 16, 16, 64, 96, 3, 2, 1, False, 0), (2, 8, 8, 128, 64, 3, 1, 1, True, 0),
          (2, 16, 16, 96, 64, 3, 1, 1, False, 64), (2, 16, 16, 64, 64, 1, 1, 0, False, 0),
          (2, 32, 32, 320, 640, 3, 1, 1, False, 320), (2, 8, 8, 640, 320, 3, 1, 1, True, 640),
-         (3, 12, 12, 128, 256, 3, 2, 1, False, 0)]
+         (3, 12, 12, 128, 256, 3, 2, 1, False, 0),
+         # > 256 output tiles: the persistent configs walk several tiles per workgroup
+         (20, 64, 64, 320, 320, 3, 1, 1, False, 0), (8, 48, 48, 128, 256, 3, 1, 1, True, 0)]
 worst = 0.0
 for N, H, C, Co, k, stride, pad, up, c2 in [(c[0], c[1], c[3], c[4], c[5], c[6], c[7], c[8], c[9]) for c in cases]:
     x = torch.randn(N, H, H, C, device="cuda").bfloat16()

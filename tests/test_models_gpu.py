@@ -148,3 +148,15 @@ def test_encoder_engines_gpu(cuda):
     te = TextEmbeddingEngine(cfg=T5Config.tiny())
     e = te.embed(["hello world"], 32)
     assert e.shape[-1] == T5Config.tiny().d_model and np.isfinite(e).all()
+
+
+def test_vit_graph_replay_matches_eager(cuda):
+    """The classifier's captured HIP graph gives the eager forward's logits, across replays with new inputs."""
+    from shai_amd.engines.encoders import ImageClassifierEngine
+    from shai_amd.models.vit import ViTConfig
+    eng = ImageClassifierEngine(ViTConfig.vit_base(), device=cuda, seed=0)
+    for i in range(3):
+        x = torch.randint(0, 256, (4, 224, 224, 3), device=cuda, dtype=torch.uint8)
+        got = eng.logits_u8(x).float().clone()
+        want = eng._forward_u8(x).float()
+        assert torch.allclose(got, want, atol=1e-2, rtol=1e-2), i

@@ -15,7 +15,7 @@
 #include "kernels/launchers.h"
 
 namespace shai {
-void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t s);
+void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t s, bool persist);
 bool gemm4_supported(const GemmArgs& a);
 void launch_gemm4_var(const GemmArgs& a, int var, int bn, hipStream_t s);
 }  // namespace shai
