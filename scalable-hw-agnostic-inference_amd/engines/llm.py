@@ -89,15 +89,22 @@ def _chain_hash(prev: int, toks: Sequence[int]) -> int:
 
 
 def sample(logits: torch.Tensor, temps: torch.Tensor, top_k: torch.Tensor, top_p: torch.Tensor,
-           gen: Optional[torch.Generator] = None, all_greedy: Optional[bool] = None) -> torch.Tensor:
+           gen: Optional[torch.Generator] = None, all_greedy: Optional[bool] = None,
+           uniforms: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Temperature / top-k / top-p sampling; rows with temperature 0 are greedy (an all-greedy batch
-    skips the sort / multinomial path entirely)."""
+    skips the sort / multinomial path entirely).  ``uniforms`` (one U[0,1) per row) makes the draw a
+    pure function of its inputs -- what the captured decode step uses (the engine draws them on the host);
+    without it they come from ``gen``.  ``out`` (int32) receives the GPU sampler's tokens in place."""
     if all_greedy:
         return logits.float().argmax(-1)
     if logits.is_cuda and logits.dim() == 2 and os.environ.get("SHAI_TORCH_SAMPLER", "0") != "1":
         # (top_k <= 0 / > 1024 rows keep their 1024 most likely tokens before the top-p cut)
-        # fused on-device sampler (csrc/kernels/sampling.hip); uniforms from the engine's generator
-        u = torch.rand(logits.shape[0], device=logits.device, generator=gen)
+        # fused on-device sampler (csrc/kernels/sampling.hip)
+        u = uniforms if uniforms is not None else torch.rand(logits.shape[0], device=logits.device, generator=gen)
+        if out is not None:
+            ops.sample(logits.contiguous(), temps.float().contiguous(), top_k.int().contiguous(),
+                       top_p.float().contiguous(), u, out)
+            return out
         out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)
         ops.sample(logits.contiguous(), temps.float().contiguous(), top_k.int().contiguous(),
                    top_p.float().contiguous(), u, out)
@@ -120,24 +127,55 @@ def sample(logits: torch.Tensor, temps: torch.Tensor, top_k: torch.Tensor, top_p
     cum = probs.cumsum(-1)
     probs = probs.masked_fill((cum - probs) > top_p.unsqueeze(-1), 0.0)
     probs = probs / probs.sum(-1, keepdim=True)
-    pick = torch.multinomial(probs, 1, generator=gen).squeeze(-1)
+    if uniforms is not None:  # inverse CDF at the supplied uniform (the GPU sampler's rule)
+        cdf = probs.cumsum(-1)
+        pick = torch.searchsorted(cdf, (uniforms.float() * cdf[:, -1]).unsqueeze(-1).contiguous(), right=True)
+        pick = pick.clamp_(max=K - 1).squeeze(-1)
+    else:
+        pick = torch.multinomial(probs, 1, generator=gen).squeeze(-1)
     sampled = idx.gather(-1, pick.unsqueeze(-1)).squeeze(-1)
     return torch.where(temps <= 0, greedy, sampled)
 
 
 class _DecodeGraph:
-    def __init__(self, engine: "LLMEngine", Bc: int, cross: bool = False):
+    """One decode step for batch bucket ``Bc`` as a single captured program (HIP graph on the GPU):
+    token feedback -> model forward -> sampling -> publish tokens.
+
+    Every per-step input (token ids, positions, KV slots, context lengths, sampling parameters, host-drawn
+    uniforms, the feedback row map and the block table) lives in ONE int32 device buffer that is filled by
+    ONE pinned host->device copy per step (double-buffered host side).  Sampling runs inside the graph, so a
+    step's only device->host traffic is the ``Bc`` sampled token ids, copied asynchronously behind an event.
+
+    Token feedback: row ``i`` with ``rowmap[i] >= 0`` takes its input token from row ``rowmap[i]`` of the
+    previous decode step's output (``engine.last_tokens``) instead of the host id.  This is what lets the
+    engine enqueue step t+1 before it has read step t's tokens back (``LLMEngine.async_decode``)."""
+
+    NF = 9  # per-row int32 fields before the block table
+
+    def __init__(self, engine: "LLMEngine", Bc: int, cross: bool = False, greedy: bool = False):
         self.Bc = Bc
         dev = engine.device
         mb = engine.max_blocks
-        self.ids = torch.zeros(Bc, dtype=torch.int32, device=dev)
-        self.pos = torch.zeros(Bc, dtype=torch.int32, device=dev)
-        self.slots = torch.full((Bc,), -1, dtype=torch.int32, device=dev)
-        self.lens = torch.ones(Bc, dtype=torch.int32, device=dev)
-        self.bt = torch.zeros(Bc, mb, dtype=torch.int32, device=dev)
+        self.words = Bc * (self.NF + mb)
+        self.dbuf = torch.zeros(self.words, dtype=torch.int32, device=dev)
+        f = lambda i: self.dbuf[i * Bc:(i + 1) * Bc]
+        self.ids, self.pos, self.slots, self.lens, self.topk = f(0), f(1), f(2), f(3), f(4)
+        self.temps, self.topp, self.u = f(5).view(torch.float32), f(6).view(torch.float32), f(7).view(torch.float32)
+        self.rowmap = f(8)
+        self.bt = self.dbuf[self.NF * Bc:].view(Bc, mb)
+        self.slots.fill_(-1)
+        self.lens.fill_(1)
+        self.rowmap.fill_(-1)
+        self.toks = torch.zeros(Bc, dtype=torch.int32, device=dev)
+        pin = dev.type == "cuda"
+        self.host = [torch.zeros(self.words, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self.host_np = [h.numpy() for h in self.host]
+        self.host_ev = [None, None]
+        self.flip = 0
         self.splits = ops.decode_splits(Bc, engine.model.kv_heads_local, engine.max_model_len)
         self.batch = Batch(self.ids, self.pos, self.slots, self.bt, self.lens, None, Bc, 1, False, self.splits)
         self.cross = cross
+        self.greedy = greedy
         if cross:  # static image-K/V inputs of the cross-attention layers
             b = self.batch
             b.cross_bt = torch.zeros(Bc, engine.max_cross_blocks, dtype=torch.int32, device=dev)
@@ -148,27 +186,64 @@ class _DecodeGraph:
         self.graph = None
         self.engine = engine
         if engine.use_graphs:
+            # the warm-up runs publish junk tokens: keep the in-flight step's feedback tokens intact
+            saved = engine.last_tokens.clone()
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
                 for _ in range(2):
-                    engine.model(self.batch, engine.kv)
+                    self._program()
             torch.cuda.current_stream().wait_stream(s)
             self.graph = new_graph(dev)
             with torch.cuda.graph(self.graph):
-                self.logits = engine.model(self.batch, engine.kv)
+                self._program()
+            engine.last_tokens.copy_(saved)
 
-    def run(self, ids, pos, slots, lens, bt, cross=None):
-        B = len(ids)
-        self.ids[:B].copy_(torch.from_numpy(np.asarray(ids, dtype=np.int32)), non_blocking=True)
-        self.pos[:B].copy_(torch.from_numpy(pos), non_blocking=True)
-        self.slots[:B].copy_(torch.from_numpy(slots), non_blocking=True)
-        self.lens[:B].copy_(torch.from_numpy(lens), non_blocking=True)
-        self.bt[:B].copy_(torch.from_numpy(bt), non_blocking=True)
-        if B < self.Bc:
-            self.slots[B:].fill_(-1)
-            self.lens[B:].fill_(1)
-            self.bt[B:].zero_()
+    def _program(self):
+        eng = self.engine
+        prev = eng.last_tokens.index_select(0, self.rowmap.clamp(min=0))
+        self.ids.copy_(torch.where(self.rowmap >= 0, prev, self.ids))
+        logits = eng.model(self.batch, eng.kv)
+        if self.greedy:
+            self.toks.copy_(logits.float().argmax(-1))
+        elif logits.is_cuda:
+            sample(logits, self.temps, self.topk, self.topp, uniforms=self.u, out=self.toks)
+        else:
+            self.toks.copy_(sample(logits, self.temps, self.topk, self.topp, uniforms=self.u))
+        eng.last_tokens[:self.Bc].copy_(self.toks)
+
+    def launch(self, seqs, pos, slots, lens, bt, ids, rowmap, uniforms, cross=None):
+        """Enqueue one decode step; returns (host int32 token view, completion event or None)."""
+        B, Bc = len(seqs), self.Bc
+        i = self.flip
+        self.flip ^= 1
+        if self.host_ev[i] is not None:  # the copy that last read this host buffer has completed
+            self.host_ev[i].synchronize()
+        h = self.host_np[i]
+        v = lambda k: h[k * Bc:(k + 1) * Bc]
+        v(0)[:B] = ids
+        v(1)[:B] = pos
+        v(2)[:B] = slots
+        v(3)[:B] = lens
+        v(4)[:B] = [s.params.top_k for s in seqs]
+        v(5).view(np.float32)[:B] = [s.params.temperature for s in seqs]
+        v(6).view(np.float32)[:B] = [s.params.top_p for s in seqs]
+        v(7).view(np.float32)[:B] = uniforms
+        v(8)[:B] = rowmap
+        btv = h[self.NF * Bc:].reshape(Bc, -1)
+        btv[:B] = bt
+        if B < Bc:  # padding rows: no KV write, one-token context, greedy, no feedback
+            v(0)[B:] = 0
+            v(1)[B:] = 0
+            v(2)[B:] = -1
+            v(3)[B:] = 1
+            v(4)[B:] = 1
+            v(5).view(np.float32)[B:] = 0.0
+            v(6).view(np.float32)[B:] = 1.0
+            v(7).view(np.float32)[B:] = 0.0
+            v(8)[B:] = -1
+            btv[B:] = 0
+        self.dbuf.copy_(self.host[i], non_blocking=True)
         if self.cross:
             cbt, clens, has = cross
             b = self.batch
@@ -177,15 +252,36 @@ class _DecodeGraph:
             hb = torch.from_numpy(has)
             b.cross_attn_rows[:B].copy_(hb, non_blocking=True)
             b.cross_mlp_rows[:B].copy_(hb, non_blocking=True)
-            if B < self.Bc:
+            if B < Bc:
                 b.cross_bt[B:].zero_()
                 b.cross_lens[B:].fill_(1)
                 b.cross_attn_rows[B:].fill_(False)
                 b.cross_mlp_rows[B:].fill_(False)
+        if self.dbuf.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+            self.host_ev[i] = ev
         if self.graph is not None:
             self.graph.replay()
-            return self.logits[:B]
-        return self.engine.model(self.batch, self.engine.kv)[:B]
+        else:
+            self._program()
+        eng = self.engine
+        out = eng.tok_host[eng.tok_flip][:Bc]
+        eng.tok_flip ^= 1
+        out.copy_(self.toks, non_blocking=True)
+        done = None
+        if self.dbuf.is_cuda:
+            done = torch.cuda.Event()
+            done.record()
+        return out, done
+
+
+class _Inflight:
+    """A decode step that has been enqueued but whose tokens the host has not consumed yet."""
+    __slots__ = ("seqs", "toks", "event", "cross")
+
+    def __init__(self, seqs, toks, event, cross):
+        self.seqs, self.toks, self.event, self.cross = seqs, toks, event, cross
 
 
 class LLMEngine:
@@ -193,7 +289,7 @@ class LLMEngine:
                  max_num_seqs: int = 64, max_model_len: int = 4096, num_kv_blocks: Optional[int] = None,
                  gpu_memory_utilization: float = 0.85, prefill_token_budget: int = 8192, use_graphs: bool = True,
                  enable_prefix_caching: bool = True, prefill_chunk: Optional[int] = None,
-                 quantization: Optional[str] = None):
+                 quantization: Optional[str] = None, async_decode: Optional[bool] = None):
         from ..models.mllama import MllamaConfig, MllamaForConditionalGeneration
         from ..runtime import BlockManager
         self.mcfg = cfg if isinstance(cfg, MllamaConfig) else None
@@ -245,6 +341,17 @@ class LLMEngine:
         self._graphs: Dict[tuple, _DecodeGraph] = {}
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
+        self.rng = np.random.default_rng(seed)  # sampling uniforms (host-drawn: identical on every TP rank)
+        # decode steps run one ahead of the host (step t+1 enqueued before step t's tokens are read back)
+        if async_decode is None:
+            async_decode = os.environ.get("SHAI_ASYNC_DECODE", "1") != "0"
+        self.async_decode = bool(async_decode)
+        self._inflight: Optional[_Inflight] = None
+        bmax = 1 << max(0, math.ceil(math.log2(max(1, max_num_seqs))))
+        self.last_tokens = torch.zeros(bmax, dtype=torch.int32, device=self.device)
+        pin = self.device.type == "cuda"
+        self.tok_host = [torch.zeros(bmax, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self.tok_flip = 0
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "steps": 0, "prefix_hit_tokens": 0}
         self.eos = {cfg.eos_token_id}
 
@@ -271,7 +378,7 @@ class LLMEngine:
         return s
 
     def has_work(self) -> bool:
-        return bool(self.waiting or self.running)
+        return bool(self.waiting or self.running or self._inflight is not None)
 
     # ------------------------------------------------------------------ kv blocks
     def _ensure_blocks(self, s: Sequence_, n_tokens: int) -> bool:
@@ -415,8 +522,9 @@ class LLMEngine:
         batch.cross_attn_rows = t(attn_rows.reshape(-1))
         batch.cross_mlp_rows = t((attn_rows & ~pre_rows).reshape(-1))
 
-    def _decode(self, seqs: List[Sequence_]):
-        from ..runtime import build_decode
+    def _decode(self, seqs: List[Sequence_]) -> Optional[_Inflight]:
+        """Enqueue one decode step of ``seqs`` (host-known token ids); the tokens are consumed by
+        :meth:`_finish_decode`."""
         for s in seqs:
             if not self._ensure_blocks(s, s.length):
                 # preempt (recompute later): free blocks, requeue at the front
@@ -430,29 +538,75 @@ class LLMEngine:
         running = set(map(id, self.running))
         seqs = [s for s in seqs if id(s) in running]
         if not seqs:
-            return
+            return None
+        return self._launch(seqs, [s.length - 1 for s in seqs], [s.last_token for s in seqs], [-1] * len(seqs))
+
+    def _launch(self, seqs, ctx_before, ids, rowmap) -> _Inflight:
+        from ..runtime import build_decode
         B = len(seqs)
-        pos, slots, lens, bt = build_decode([s.length - 1 for s in seqs], [s.blocks for s in seqs], self.max_blocks)
-        ids = [s.last_token for s in seqs]
+        pos, slots, lens, bt = build_decode(ctx_before, [s.blocks for s in seqs], self.max_blocks)
         Bc = 1 << max(0, math.ceil(math.log2(B)))
         cross = self._cross_tables(seqs) if any(s.cross_blocks for s in seqs) else None
-        key = (Bc, cross is not None)
+        greedy = all(s.params.temperature <= 0 for s in seqs)
+        key = (Bc, cross is not None, greedy)
         g = self._graphs.get(key)
         if g is None:
-            g = self._graphs[key] = _DecodeGraph(self, Bc, cross=cross is not None)
-        logits = g.run(ids, pos, slots, lens, bt, cross)
+            g = self._graphs[key] = _DecodeGraph(self, Bc, cross=cross is not None, greedy=greedy)
+        u = self.rng.random(B, dtype=np.float32) if not greedy else np.zeros(B, np.float32)
+        toks, ev = g.launch(seqs, pos, slots, lens, bt, ids, rowmap, u, cross)
         self.stats["decode_tokens"] += B
-        for s in seqs:
+        return _Inflight(seqs, toks, ev, cross is not None)
+
+    def _finish_decode(self, h: _Inflight):
+        """Consume an enqueued decode step's tokens (rows of sequences that finished meanwhile -- the
+        look-ahead step past an EOS -- are dropped)."""
+        if h.event is not None:
+            h.event.synchronize()
+        toks = h.toks[:len(h.seqs)].tolist()
+        live = [(s, t) for s, t in zip(h.seqs, toks) if not s.finished]
+        for s, _ in live:
             s.n_cached = s.length
-        self._sample_and_append(seqs, logits)
+        self._append([s for s, _ in live], [t for _, t in live])
+
+    def _lookahead(self, prev: _Inflight) -> Optional[_Inflight]:
+        """Enqueue the next decode step before ``prev``'s tokens are read back, feeding ``prev``'s sampled
+        tokens on the device.  Only in steady-state decode (nothing waiting, no prefill chunk pending, no
+        image cross-attention); sequences that ``prev`` completes by length are left out, and a sequence
+        that ``prev`` ends by a stop token produces one extra token that :meth:`_finish_decode` drops."""
+        if not self.async_decode or prev.cross or self.waiting:
+            return None
+        if any(s.n_cached < len(s.prompt) for s in self.running):
+            return None
+        in_prev = set(map(id, prev.seqs))
+        if any(id(s) not in in_prev for s in self.running if not s.finished):
+            return None
+        nxt, rows = [], []
+        for i, s in enumerate(prev.seqs):
+            if s.finished:
+                continue
+            n_out = len(s.output) + 1           # after prev's token
+            if n_out >= s.params.max_tokens or s.length + 1 >= self.max_model_len:
+                continue
+            nxt.append(s)
+            rows.append(i)
+        if not nxt:
+            return None
+        for s in nxt:  # blocks for the token fed at position s.length (prev's output)
+            if not self._ensure_blocks(s, s.length + 1):
+                return None
+        return self._launch(nxt, [s.length for s in nxt], [0] * len(nxt), rows)
 
     def _sample_and_append(self, seqs, logits):
         d = self.device
         temps = torch.tensor([s.params.temperature for s in seqs], dtype=torch.float32, device=d)
         tk = torch.tensor([s.params.top_k for s in seqs], dtype=torch.int64, device=d)
         tpp = torch.tensor([s.params.top_p for s in seqs], dtype=torch.float32, device=d)
-        toks = sample(logits, temps, tk, tpp, self.gen,
-                      all_greedy=all(s.params.temperature <= 0 for s in seqs)).tolist()
+        greedy = all(s.params.temperature <= 0 for s in seqs)
+        u = None if greedy else torch.from_numpy(self.rng.random(len(seqs), dtype=np.float32)).to(d)
+        toks = sample(logits, temps, tk, tpp, self.gen, all_greedy=greedy, uniforms=u).tolist()
+        self._append(seqs, toks)
+
+    def _append(self, seqs, toks):
         now = time.perf_counter()
         for s, tok in zip(seqs, toks):
             s.output.append(int(tok))
@@ -466,12 +620,27 @@ class LLMEngine:
             if s.finished:
                 s.finish_time = now
 
+    def _reap(self) -> List[Sequence_]:
+        done = [s for s in self.running if s.finished]
+        if done:
+            fin = set(map(id, done))
+            for s in done:
+                self._free(s)
+            self.running = [s for s in self.running if id(s) not in fin]
+        return done
+
     def step(self) -> List[Sequence_]:
         """Run one engine iteration; returns sequences that finished in it."""
         self.stats["steps"] += 1
+        prev = self._inflight
+        if prev is not None:
+            self._inflight = self._lookahead(prev)   # step t+1 enqueued while step t is on the GPU
+            self._finish_decode(prev)
+            if self._inflight is not None:
+                return self._reap()
         adm = self._admit()
         pending = [s for s in self.running if s.n_cached < len(s.prompt)]     # mid chunked prefill
-        decodable = [s for s in self.running if s.n_cached >= len(s.prompt)]
+        decodable = [s for s in self.running if s.n_cached >= len(s.prompt) and not s.finished]
         # new prompts and remaining prefill chunks alternate with decode steps of the running batch
         if adm or (pending and (not decodable or self._last_step != "prefill")):
             self.running += adm
@@ -480,19 +649,22 @@ class LLMEngine:
             self._last_step = "prefill"
         elif decodable:
             with prof.range_("llm_decode"):
-                self._decode(decodable)
+                h = self._decode(decodable)
+            if h is not None:
+                if self.async_decode and not h.cross:
+                    self._inflight = h   # tokens consumed by the next step (after it enqueues its own)
+                else:
+                    self._finish_decode(h)
             self._last_step = "decode"
-        done = [s for s in self.running if s.finished]
-        for s in done:
-            self._free(s)
-            self.running.remove(s)
-        return done
+        return self._reap()
 
     @torch.inference_mode()
     def generate(self, prompts: Sequence[Sequence[int]], params: Optional[SamplingParams] = None) -> List[Sequence_]:
         seqs = [self.add_request(p, params) for p in prompts]
         while any(not s.finished for s in seqs):
             self.step()
+        if self._inflight is not None and not any(not s.finished for s in self._inflight.seqs):
+            self.step()  # a look-ahead step past the last stop token: retire it (its tokens are dropped)
         return seqs
 
 

@@ -136,3 +136,36 @@ def test_fp8_engine_cpu_generates():
     assert len(out) == 4
     with pytest.raises(ValueError):
         LLMEngine(c, device="cpu", max_num_seqs=2, max_model_len=128, quantization="int3")
+
+
+def test_async_lookahead_decode_matches_sync():
+    """Decode steps enqueued one ahead of the host (device-side token feedback, look-ahead step past a stop
+    token dropped) produce exactly the tokens of the synchronous engine: greedy with stop tokens that end
+    sequences at different steps, and seeded top-k/top-p sampling; every KV block is returned."""
+    c = LlamaConfig.tiny()
+    prompts = [[3, 17, 99, 250, 7], [5, 6, 7], [400, 12, 13, 14, 15, 16], [9, 9]]
+    mk = lambda a: LLMEngine(c, device="cpu", max_num_seqs=4, max_model_len=256, enable_prefix_caching=False,
+                             seed=5, async_decode=a)
+    g = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True)
+    ref = [s.output for s in mk(False).generate(prompts, g)]
+    stops = [ref[0][4], ref[2][7]]  # end two sequences early, at different steps
+    gs = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True, stop_token_ids=stops)
+    e_sync, e_async = mk(False), mk(True)
+    want = [s.output for s in e_sync.generate(prompts, gs)]
+    got_seqs = e_async.generate(prompts, gs)
+    assert [s.output for s in got_seqs] == want
+    assert any(len(o) < 12 for o in want)
+    assert e_async._inflight is None and e_async.bm.num_free == e_async.num_kv_blocks
+    sp = SamplingParams(max_tokens=10, temperature=0.8, top_k=20, top_p=0.9, ignore_eos=True)
+    a = [s.output for s in mk(False).generate(prompts, sp)]
+    b = [s.output for s in mk(True).generate(prompts, sp)]
+    assert a == b and all(len(o) == 10 for o in a)
+    # the async engine really ran ahead: decode steps were enqueued while a previous one was in flight
+    e = mk(True)
+    for p in prompts:
+        e.add_request(p, g)
+    ahead = 0
+    while e.has_work():
+        e.step()
+        ahead += e._inflight is not None
+    assert ahead >= 8

@@ -50,6 +50,36 @@ def test_llama_engine_gpu_matches_transformers(cuda, graphs):
         assert s.output[:2] == g[:2], (s.output, g)
 
 
+def test_llm_engine_async_decode_gpu(cuda):
+    """HIP-graph decode steps enqueued one ahead of the host (device-side token feedback, in-graph fused
+    sampler, one pinned input copy per step) give exactly the synchronous engine's tokens: greedy with a
+    stop token ending one sequence early (the batch stays in one graph bucket), and seeded sampling."""
+    from shai_amd.engines.llm import LLMEngine, SamplingParams
+    from shai_amd.models.llama import LlamaConfig
+    c = LlamaConfig.tiny()
+    prompts = [[3, 17, 99, 250, 7], [5, 6, 7], [400, 12, 13, 14, 15, 16], [9, 9]]
+    mk = lambda a: LLMEngine(c, device="cuda", max_num_seqs=4, max_model_len=256, enable_prefix_caching=False,
+                             seed=3, async_decode=a)
+    g = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True)
+    ref = [s.output for s in mk(False).generate(prompts, g)]
+    # a stop token that ends exactly one sequence, after its 4th token (so the batch stays in one bucket)
+    cand = [(j, i, t) for j, o in enumerate(ref) for i, t in enumerate(o)
+            if i >= 3 and t not in o[:i] and all(t not in q for k, q in enumerate(ref) if k != j)]
+    if not cand:
+        pytest.skip("no token unique to one sequence in this random model's greedy outputs")
+    j, i, t = cand[0]
+    gs = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True, stop_token_ids=[t])
+    want = [s.output for s in mk(False).generate(prompts, gs)]
+    e = mk(True)
+    got = [s.output for s in e.generate(prompts, gs)]
+    assert got == want and len(want[j]) == i + 1
+    assert e._inflight is None and e.bm.num_free == e.num_kv_blocks
+    sp = SamplingParams(max_tokens=16, temperature=0.8, top_k=40, top_p=0.9, ignore_eos=True)
+    a = [s.output for s in mk(False).generate(prompts, sp)]
+    b = [s.output for s in mk(True).generate(prompts, sp)]
+    assert a == b and all(len(o) == 16 for o in a)
+
+
 def test_llama_prefill_logits_gpu(cuda):
     """Full-sequence logits of the paged prefill path vs HF (bf16 tolerance)."""
     from shai_amd.models.llama import Batch

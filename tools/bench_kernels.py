@@ -51,7 +51,7 @@ def bench_decode(rows):
     """Decode-shaped GEMMs (Mistral-7B TP1, batch M): skinny kernel vs each tile config vs hipBLASLt,
     reported as achieved weight bandwidth."""
     cfgs = int(os.environ.get("SHAI_NUM_CFGS", "5"))
-    for M in (1, 8, 32):
+    for M in [int(m) for m in os.environ.get("SHAI_DECODE_M", "1,8,32,64").split(",")]:
         for N, K in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (32768, 4096)]:
             # rotate over enough weight copies to defeat the 256 MB Infinity Cache (decode streams
             # 14.5 GB of weights per token, so every GEMM reads HBM)
