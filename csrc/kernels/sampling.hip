@@ -7,8 +7,8 @@
 // (six launches and a [B, V] fp32 copy) with one kernel:
 //   1. exact K-th largest logit by 4-pass byte radix select over order-preserving
 //      uint32 keys (wave-private LDS histograms, row re-read from L2 each pass);
-//   2. gather exactly K candidates (ties broken by arrival) into LDS;
-//   3. bitonic sort of the candidates (descending);
+//   2. gather exactly K candidates (of the keys equal to the K-th, the lowest indices) into LDS;
+//   3. bitonic sort of the candidates (descending value, ascending index: deterministic);
 //   4. p_i = exp((l_i - l_0) / T), inclusive block scan, nucleus cut at top_p
 //      (keep i while the mass BEFORE i is <= top_p of the total -- the same rule
 //      as the torch reference path), draw with a host-supplied uniform.
@@ -44,7 +44,7 @@ __global__ void __launch_bounds__(SMP_T) sample_kernel(const void* __restrict__ 
   __shared__ float cval[SMP_MAXK];
   __shared__ int cidx[SMP_MAXK];
   __shared__ float scan[SMP_MAXK];
-  __shared__ uint32_t s_prefix, s_k, s_cnt, s_tie;
+  __shared__ uint32_t s_prefix, s_k, s_cnt, s_eq;
   const int row = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const char* base = reinterpret_cast<const char*>(logits) + (long)row * ld * (BF16 ? 2 : 4);
   const float T = temps[row];
@@ -85,30 +85,46 @@ __global__ void __launch_bounds__(SMP_T) sample_kernel(const void* __restrict__ 
       }
       s_k = k - above;
       s_prefix = prefix | ((uint32_t)b << sh);
+      s_eq = tot[b];  // after the last pass: how many elements equal the threshold key
     }
     mask |= 255u << sh;
     __syncthreads();
   }
   const uint32_t thr = s_prefix;
   const uint32_t ties = s_k;  // how many elements equal to thr to keep
-  // ---- 2. gather exactly K candidates
-  if (tid == 0) {
-    s_cnt = 0;
-    s_tie = 0;
-  }
+  // ---- 2. gather exactly K candidates: every key above the threshold, and of the keys equal to it the
+  // `ties` with the lowest vocabulary indices (deterministic; when every equal key is kept -- the common
+  // case -- no ordering is needed, otherwise wave 0 walks the row in index order with ballots)
+  const bool all_ties = s_eq <= ties;
+  if (tid == 0) s_cnt = 0;
   __syncthreads();
   for (int i = tid; i < V; i += SMP_T) {
     const float v = smp_load<BF16>(base, i);
     const uint32_t key = f2key(v);
-    bool take = key > thr;
-    if (key == thr) take = atomicAdd(&s_tie, 1u) < ties;
-    if (take) {
+    if (key > thr || (all_ties && key == thr)) {
       const uint32_t slot = atomicAdd(&s_cnt, 1u);
       if (slot < (uint32_t)SMP_MAXK) {
         cval[slot] = v;
         cidx[slot] = i;
       }
     }
+  }
+  __syncthreads();
+  if (!all_ties && w == 0) {
+    uint32_t taken = 0, base_slot = s_cnt;
+    for (int i0 = 0; i0 < V && taken < ties; i0 += 64) {
+      const int i = i0 + lane;
+      const float v = i < V ? smp_load<BF16>(base, i) : 0.f;
+      const bool eq = i < V && f2key(v) == thr;
+      const unsigned long long bal = __ballot(eq);
+      const uint32_t rank = taken + __popcll(bal & ((1ull << lane) - 1ull));
+      if (eq && rank < ties && base_slot + rank < (uint32_t)SMP_MAXK) {
+        cval[base_slot + rank] = v;
+        cidx[base_slot + rank] = i;
+      }
+      taken += __popcll(bal);
+    }
+    if (lane == 0) s_cnt = base_slot + min(taken, ties);
   }
   __syncthreads();
   const int n = min((int)s_cnt, SMP_MAXK);
@@ -120,7 +136,8 @@ __global__ void __launch_bounds__(SMP_T) sample_kernel(const void* __restrict__ 
       cidx[i] = -1;
     }
   __syncthreads();
-  // ---- 3. bitonic sort, descending by value
+  // ---- 3. bitonic sort, descending by value, ties by ascending index (a total order: the result does not
+  // depend on the gather's slot order)
   for (int k2 = 2; k2 <= P; k2 <<= 1) {
     for (int j = k2 >> 1; j > 0; j >>= 1) {
       for (int i = tid; i < P; i += SMP_T) {
@@ -128,7 +145,11 @@ __global__ void __launch_bounds__(SMP_T) sample_kernel(const void* __restrict__ 
         if (ixj > i) {
           const bool desc = (i & k2) == 0;
           const float a = cval[i], b = cval[ixj];
-          if (desc ? (a < b) : (a > b)) {
+          const int ia = cidx[i], ib = cidx[ixj];
+          // "b ranks before a": larger value, or equal value and smaller index (padding: -inf, index -1)
+          const bool b_first = b > a || (b == a && (unsigned)ib < (unsigned)ia);
+          const bool a_first = a > b || (a == b && (unsigned)ia < (unsigned)ib);
+          if (desc ? b_first : a_first) {
             cval[i] = b;
             cval[ixj] = a;
             const int t = cidx[i];

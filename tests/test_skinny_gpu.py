@@ -63,6 +63,23 @@ def test_skinny_k_groups(cuda, fix, kg, M, N, K, rms):
     assert _rel(out, xf @ w.float().t() + b.float()) < 1e-2
 
 
+@pytest.mark.parametrize("rms", [False, True])
+def test_skinny_fixup_bitwise_deterministic(cuda, rms):
+    """The in-kernel split-K fixup sums the K-group slabs in group order whichever group arrives last, so
+    repeated launches are bitwise identical (seeded sampling downstream depends on it)."""
+    M, N, K = 64, 6144, 4096
+    torch.manual_seed(7)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
+    outs = []
+    for _ in range(12):
+        out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+        ops.gemm_into(x, w, out, force_cfg=SKINNY_FIX + 8, rms_eps=1e-5 if rms else -1.0)
+        outs.append(out)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+
+
 def test_skinny_graph_replay_rearms_tickets(cuda):
     """Split-K fixup tickets must re-arm so graph replays stay correct."""
     M, N, K = 48, 1024, 8192   # few tiles, long K -> several K groups (two 32-row X groups)
@@ -163,3 +180,26 @@ def test_fused_sampler_distribution(cuda):
     # row 2: empirical vs softmax over top-5 at T=1
     p = torch.softmax(lb[2, top5], 0)
     assert (counts[2, top5] / 400 - p).abs().max() < 0.1
+
+
+def test_fused_sampler_deterministic_with_ties(cuda):
+    """bf16 logits are full of exact ties: the fused sampler keeps the lowest-index tied candidates and
+    sorts ties by index, so a fixed uniform always draws the same token, and greedy rows pick the first
+    maximal index (torch.argmax)."""
+    torch.manual_seed(3)
+    B, V = 8, 32768
+    logits = (torch.randn(B, V, device=cuda) * 0.5).round().bfloat16()   # few distinct values
+    logits[:, 100] = logits.max() + 1
+    logits[:, 7] = logits.max()                                          # tied row maxima at 7 and 100
+    temps = torch.tensor([0.0, 0.7, 1.0, 0.7, 0.0, 1.3, 0.7, 0.7], device=cuda)
+    tk = torch.tensor([1, 50, 40, 1000, 5, 0, 3, 64], device=cuda, dtype=torch.int32)
+    tp = torch.tensor([1.0, 0.9, 0.95, 0.9, 1.0, 0.8, 1.0, 0.5], device=cuda)
+    u = torch.rand(B, device=cuda)
+    outs = []
+    for _ in range(10):
+        o = torch.empty(B, dtype=torch.int32, device=cuda)
+        ops.sample(logits, temps, tk, tp, u, o)
+        outs.append(o.cpu())
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    assert outs[0][0].item() == 7 and outs[0][4].item() == 7
