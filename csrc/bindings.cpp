@@ -967,6 +967,14 @@ int64_t gemm_tuning_import(const std::vector<std::string>& entries) {
   return n;
 }
 
+void token_feedback(const Tensor& ids, const Tensor& rowmap, const Tensor& prev) {
+  SHAI_CHECK(ids.scalar_type() == at::kInt && rowmap.scalar_type() == at::kInt && prev.scalar_type() == at::kInt &&
+                 ids.is_contiguous() && rowmap.is_contiguous() && prev.is_contiguous() && rowmap.numel() == ids.numel(),
+             "token_feedback: int32 contiguous ids / rowmap of one length");
+  shai::launch_token_feedback(ids.data_ptr<int>(), rowmap.data_ptr<int>(), prev.data_ptr<int>(), (int)ids.numel(),
+                              stream());
+}
+
 void embedding(const Tensor& ids, const Tensor& table, const Tensor& out) {
   check_i32(ids, "ids");
   check_bf16(table, "table");
@@ -1010,6 +1018,7 @@ TORCH_LIBRARY(shai, m) {
   m.def("sched_step(Tensor model_out, Tensor(a!) latents, bool cfg, float guidance, int pred_type, float a_t, float a_prev, float dt) -> ()");
   m.def("softmax_(Tensor(a!) x, float scale) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out) -> ()");
+  m.def("token_feedback(Tensor(a!) ids, Tensor rowmap, Tensor prev) -> ()");
   m.def("gemm_tuning() -> str[]", &gemm_tuning);
   m.def("gemm_tuning_export() -> str[]", &gemm_tuning_export);
   m.def("gemm_tuning_import(str[] entries) -> int", &gemm_tuning_import);
@@ -1037,4 +1046,5 @@ TORCH_LIBRARY_IMPL(shai, CUDA, m) {
   m.impl("sched_step", &sched_step);
   m.impl("softmax_", &softmax_);
   m.impl("embedding", &embedding);
+  m.impl("token_feedback", &token_feedback);
 }

@@ -223,6 +223,21 @@ __global__ void embedding_kernel(const int* __restrict__ ids, const bf16_t* __re
   }
 }
 
+// Decode token feedback: ids[i] = prev[rowmap[i]] where rowmap[i] >= 0 (the previous decode step's sampled
+// token of the same sequence, still on the device), else the host-supplied ids[i].
+__global__ void token_feedback_kernel(int* __restrict__ ids, const int* __restrict__ rowmap,
+                                      const int* __restrict__ prev, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int r = rowmap[i];
+    if (r >= 0) ids[i] = prev[r];
+  }
+}
+
+void launch_token_feedback(int* ids, const int* rowmap, const int* prev, int n, hipStream_t s) {
+  token_feedback_kernel<<<(n + 255) / 256, 256, 0, s>>>(ids, rowmap, prev, n);
+}
+
 void launch_embedding(const int* ids, const bf16_t* table, bf16_t* out, long T, int D, hipStream_t s) {
   embedding_kernel<<<grid_for(T * (D / 8)), 256, 0, s>>>(ids, table, out, T, D);
 }

@@ -76,6 +76,7 @@ void launch_sched_step(const bf16_t* model_out, bf16_t* latents, long n, int cfg
 void launch_softmax(bf16_t* x, long rows, int D, float scale, hipStream_t s);
 // Embedding gather: out[t] = table[ids[t]]
 void launch_embedding(const int* ids, const bf16_t* table, bf16_t* out, long T, int D, hipStream_t s);
+void launch_token_feedback(int* ids, const int* rowmap, const int* prev, int n, hipStream_t s);
 
 // ---------------------------------------------------------------- GEMM / conv
 struct GemmArgs {

@@ -93,8 +93,8 @@ __global__ void __launch_bounds__(SMP_T) sample_kernel(const void* __restrict__ 
   const uint32_t thr = s_prefix;
   const uint32_t ties = s_k;  // how many elements equal to thr to keep
   // ---- 2. gather exactly K candidates: every key above the threshold, and of the keys equal to it the
-  // `ties` with the lowest vocabulary indices (deterministic; when every equal key is kept -- the common
-  // case -- no ordering is needed, otherwise wave 0 walks the row in index order with ballots)
+  // `ties` with the lowest vocabulary indices (deterministic; when every equal key is kept no ordering is
+  // needed, otherwise every wave counts the equal keys of its row chunk, then ranks them in index order)
   const bool all_ties = s_eq <= ties;
   if (tid == 0) s_cnt = 0;
   __syncthreads();
@@ -110,21 +110,34 @@ __global__ void __launch_bounds__(SMP_T) sample_kernel(const void* __restrict__ 
     }
   }
   __syncthreads();
-  if (!all_ties && w == 0) {
-    uint32_t taken = 0, base_slot = s_cnt;
-    for (int i0 = 0; i0 < V && taken < ties; i0 += 64) {
+  if (!all_ties) {  // ordered selection of the `ties` lowest-index equal keys: wave w owns chunk w of the row
+    __shared__ uint32_t tie_cnt[SMP_WAVES];
+    const int C = ((V + SMP_WAVES - 1) / SMP_WAVES + 63) & ~63;
+    const int c0 = w * C, c1 = min(V, c0 + C);
+    uint32_t mine = 0;
+    for (int i0 = c0; i0 < c1; i0 += 64) {
       const int i = i0 + lane;
-      const float v = i < V ? smp_load<BF16>(base, i) : 0.f;
-      const bool eq = i < V && f2key(v) == thr;
-      const unsigned long long bal = __ballot(eq);
-      const uint32_t rank = taken + __popcll(bal & ((1ull << lane) - 1ull));
-      if (eq && rank < ties && base_slot + rank < (uint32_t)SMP_MAXK) {
-        cval[base_slot + rank] = v;
-        cidx[base_slot + rank] = i;
-      }
-      taken += __popcll(bal);
+      mine += __popcll(__ballot(i < c1 && f2key(smp_load<BF16>(base, i)) == thr));
     }
-    if (lane == 0) s_cnt = base_slot + min(taken, ties);
+    if (lane == 0) tie_cnt[w] = mine;
+    __syncthreads();
+    uint32_t rank0 = 0;
+    for (int q = 0; q < w; ++q) rank0 += tie_cnt[q];
+    const uint32_t above = s_cnt;
+    for (int i0 = c0; i0 < c1 && rank0 < ties; i0 += 64) {
+      const int i = i0 + lane;
+      const float v = i < c1 ? smp_load<BF16>(base, i) : 0.f;
+      const bool eq = i < c1 && f2key(v) == thr;
+      const unsigned long long bal = __ballot(eq);
+      const uint32_t rank = rank0 + __popcll(bal & ((1ull << lane) - 1ull));
+      if (eq && rank < ties && above + rank < (uint32_t)SMP_MAXK) {
+        cval[above + rank] = v;
+        cidx[above + rank] = i;
+      }
+      rank0 += __popcll(bal);
+    }
+    __syncthreads();
+    if (tid == 0) s_cnt = above + ties;
   }
   __syncthreads();
   const int n = min((int)s_cnt, SMP_MAXK);

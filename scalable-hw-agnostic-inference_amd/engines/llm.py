@@ -201,8 +201,7 @@ class _DecodeGraph:
 
     def _program(self):
         eng = self.engine
-        prev = eng.last_tokens.index_select(0, self.rowmap.clamp(min=0))
-        self.ids.copy_(torch.where(self.rowmap >= 0, prev, self.ids))
+        ops.token_feedback(self.ids, self.rowmap, eng.last_tokens)
         logits = eng.model(self.batch, eng.kv)
         if self.greedy:
             self.toks.copy_(logits.float().argmax(-1))

@@ -24,7 +24,7 @@ from .reference import (ACT_GELU, ACT_GELU_TANH, ACT_NONE, ACT_QUICK_GELU, ACT_R
 __all__ = [
     "rmsnorm", "layernorm", "groupnorm_stats", "groupnorm_apply", "groupnorm", "linear", "conv2d", "attention",
     "paged_attention", "decode_attention", "kv_write", "rope", "rope_pairs", "gated_act", "bias_act", "sched_step",
-    "softmax_", "embedding", "quantize_fp8_rows", "dequant_fp8", "pack_conv_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
+    "softmax_", "embedding", "token_feedback", "quantize_fp8_rows", "dequant_fp8", "pack_conv_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
     "ACT_GELU_TANH", "ACT_QUICK_GELU", "ACT_RELU", "decode_splits",
 ]
 
@@ -399,6 +399,16 @@ def softmax_(x, scale: float = 1.0):
         return x
     _K().softmax_(x, float(scale))
     return x
+
+
+def token_feedback(ids, rowmap, prev):
+    """In place: ids[i] = prev[rowmap[i]] where rowmap[i] >= 0 (decode-step token feedback; all int32)."""
+    if not _gpu(ids):
+        prev_rows = prev.index_select(0, rowmap.clamp(min=0).long())
+        ids.copy_(torch.where(rowmap >= 0, prev_rows, ids))
+        return ids
+    _K().token_feedback(ids, rowmap, prev)
+    return ids
 
 
 def embedding(ids, table):

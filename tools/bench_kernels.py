@@ -75,7 +75,7 @@ def bench_decode(rows):
             del ws
             gb = N * K * 2 / 1e9
             rows.append(dict(op="decode_gemm", shape=f"{M}x{N}x{K}", skinny_us=res[1000] * 1e6,
-                             best_tile_us=min(v for k, v in res.items() if k != 1000) * 1e6,
+                             best_tile_us=min((v for k, v in res.items() if k != 1000), default=float("nan")) * 1e6,
                              tuned_us=t_tuned * 1e6, torch_us=t_t * 1e6,
                              skinny_TBps=gb / res[1000] / 1e3, torch_TBps=gb / t_t / 1e3))
 
