@@ -59,7 +59,8 @@ __global__ void __launch_bounds__(SMP_T) sample_kernel(const void* __restrict__ 
     s_k = K;
   }
   uint32_t mask = 0;
-  for (int pass = 3; pass >= 0; --pass) {
+  // bf16 logits: the low 16 bits of a key are fixed by its sign, so the top two digits already fix the threshold
+  for (int pass = 3; pass >= (BF16 ? 2 : 0); --pass) {
     for (int i = tid; i < SMP_WAVES * 256; i += SMP_T) (&hist[0][0])[i] = 0;
     __syncthreads();
     const uint32_t prefix = s_prefix;
@@ -90,7 +91,9 @@ __global__ void __launch_bounds__(SMP_T) sample_kernel(const void* __restrict__ 
     mask |= 255u << sh;
     __syncthreads();
   }
-  const uint32_t thr = s_prefix;
+  uint32_t thr = s_prefix;
+  // (bf16: a negative value's key has its low 16 bits all ones, a positive value's all zeros)
+  if (BF16 && !(thr & 0x80000000u)) thr |= 0xFFFFu;
   const uint32_t ties = s_k;  // how many elements equal to thr to keep
   // ---- 2. gather exactly K candidates: every key above the threshold, and of the keys equal to it the
   // `ties` with the lowest vocabulary indices (deterministic; when every equal key is kept no ordering is

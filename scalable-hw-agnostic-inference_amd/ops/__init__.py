@@ -294,8 +294,11 @@ def paged_attention(q, k_cache, v_cache, block_table, kv_lens, q_lens, scale=Non
 
 
 def decode_splits(batch: int, hkv: int, max_ctx: int) -> int:
+    """Split-K factor of the paged decode attention: enough (sequence, KV head, split) workgroups to fill
+    the chip (``SHAI_DECODE_WG`` of them, default 512 = two per CU), at most one split per 64-token block."""
     nblk = max(1, (max_ctx + 63) // 64)
-    want = max(1, 512 // max(1, batch * hkv))
+    target = int(os.environ.get("SHAI_DECODE_WG", "512"))
+    want = max(1, target // max(1, batch * hkv))
     return int(min(nblk, want, 64))
 
 

@@ -203,3 +203,23 @@ def test_fused_sampler_deterministic_with_ties(cuda):
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
     assert outs[0][0].item() == 7 and outs[0][4].item() == 7
+
+
+def test_fused_sampler_negative_logits(cuda):
+    """All-negative bf16 logits (the threshold key's low half is then all ones): top-k candidates are
+    exactly the k largest, greedy rows are the argmax."""
+    torch.manual_seed(5)
+    B, V = 6, 32768
+    lb = (torch.randn(B, V, device=cuda) * 2 - 80).bfloat16()
+    temps = torch.tensor([0.0, 0.7, 1.0, 0.7, 1.5, 0.0], device=cuda)
+    tk = torch.tensor([50, 50, 5, 200, 1000, 1], device=cuda, dtype=torch.int32)
+    tp = torch.ones(B, device=cuda)
+    lf = lb.float()
+    kth = torch.stack([lf[i].topk(int(tk[i])).values[-1] for i in range(B)])
+    for it in range(50):
+        u = torch.rand(B, device=cuda)
+        o = torch.empty(B, dtype=torch.int32, device=cuda)
+        ops.sample(lb, temps, tk, tp, u, o)
+        picked = lf[torch.arange(B, device=cuda), o.long()]
+        assert bool((picked >= kth).all()), it
+        assert int(o[0]) == int(lf[0].argmax()) and int(o[5]) == int(lf[5].argmax())
