@@ -825,6 +825,59 @@ void decode_attn(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, 
   shai::launch_decode_attn(a, stream());
 }
 
+// Fused decode step on the packed QKV rows [B, (h + 2 hk) D]: RoPE on q and k, this step's k / v into the paged
+// cache at slots, attention over the cached context plus the new token (replaces rope_qkv_cache +
+// decode_attn in the decode graph).
+void decode_attn_rope(const Tensor& qkv, const Tensor& k_cache, const Tensor& v_cache, const Tensor& o,
+                      const Tensor& block_table, const Tensor& ctx_lens, const Tensor& positions, const Tensor& cos,
+                      const Tensor& sin, const Tensor& slots, const Tensor& ws, int64_t h, int64_t hk,
+                      int64_t num_splits, double scale) {
+  check_bf16(qkv, "qkv");
+  check_rows(o, "o");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_i32(block_table, "block_table");
+  check_i32(ctx_lens, "ctx_lens");
+  check_i32(positions, "positions");
+  check_i32(slots, "slots");
+  check_f32(ws, "ws");
+  SHAI_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
+                 sin.is_contiguous(), "rope tables: contiguous fp32");
+  SHAI_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 64 && k_cache.size(1) == hk, "decode_attn_rope cache shape");
+  shai::DecodeAttnArgs a{};
+  a.D = k_cache.size(3);
+  a.B = qkv.size(0);
+  a.Hq = h;
+  a.Hkv = hk;
+  SHAI_CHECK(a.D == 64 || a.D == 128, "decode_attn head dim 64/128");
+  SHAI_CHECK(a.Hq % a.Hkv == 0 && a.Hq / a.Hkv <= 8, "decode_attn GQA group must be <= 8");
+  SHAI_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) >= (h + 2 * hk) * a.D, "qkv rows");
+  SHAI_CHECK(o.dim() == 2 && o.size(0) == a.B && o.size(1) == h * a.D && o.stride(1) == 1, "o [B, h D]");
+  SHAI_CHECK(cos.size(1) == a.D / 2 && sin.sizes() == cos.sizes(), "rope tables [max_pos, D / 2]");
+  SHAI_CHECK(positions.numel() >= a.B && slots.numel() >= a.B && ctx_lens.numel() >= a.B, "per-row inputs");
+  const shai::bf16_t* base = cptr(qkv);
+  a.q = base;
+  a.knew = base + h * a.D;
+  a.vnew = base + (h + hk) * a.D;
+  a.q_bs = a.new_bs = qkv.stride(0);
+  a.o = mptr(o);
+  a.o_bs = o.stride(0);
+  a.k_cache = cptr(k_cache);
+  a.v_cache = cptr(v_cache);
+  a.block_table = block_table.data_ptr<int>();
+  a.ctx_lens = ctx_lens.data_ptr<int>();
+  a.positions = positions.data_ptr<int>();
+  a.slots = slots.data_ptr<int>();
+  a.rope_cos = cos.data_ptr<float>();
+  a.rope_sin = sin.data_ptr<float>();
+  a.max_blocks = block_table.size(1);
+  a.num_splits = num_splits;
+  a.ws = ws.data_ptr<float>();
+  SHAI_CHECK(ws.numel() * 4 >= (long)shai::decode_attn_workspace(a.B, a.Hq, a.D, num_splits), "ws too small");
+  a.scale = scale;
+  shai::launch_decode_attn(a, stream());
+}
+
 void kv_write(const Tensor& k, const Tensor& v, const Tensor& k_cache, const Tensor& v_cache, const Tensor& slots) {
   check_rows(k, "k");
   check_rows(v, "v");
@@ -1019,6 +1072,9 @@ TORCH_LIBRARY(shai, m) {
   m.def("softmax_(Tensor(a!) x, float scale) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out) -> ()");
   m.def("token_feedback(Tensor(a!) ids, Tensor rowmap, Tensor prev) -> ()");
+  m.def("decode_attn_rope(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor(c!) o, Tensor block_table, "
+        "Tensor ctx_lens, Tensor positions, Tensor cos, Tensor sin, Tensor slots, Tensor(d!) ws, int h, int hk, "
+        "int num_splits, float scale) -> ()");
   m.def("gemm_tuning() -> str[]", &gemm_tuning);
   m.def("gemm_tuning_export() -> str[]", &gemm_tuning_export);
   m.def("gemm_tuning_import(str[] entries) -> int", &gemm_tuning_import);
@@ -1047,4 +1103,5 @@ TORCH_LIBRARY_IMPL(shai, CUDA, m) {
   m.impl("softmax_", &softmax_);
   m.impl("embedding", &embedding);
   m.impl("token_feedback", &token_feedback);
+  m.impl("decode_attn_rope", &decode_attn_rope);
 }

@@ -285,6 +285,7 @@ void launch_flash_attn(const AttnArgs& a, hipStream_t s) {
 // grid (B, Hkv, splits); block = G waves (G = Hq/Hkv <= 8), wave w = head hk*G+w.
 // ----------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void da_lds_void;
+typedef __bf16 bf16x2d __attribute__((ext_vector_type(2)));
 
 // Decode attention, one workgroup per (sequence, KV head, split): G = Hq/Hkv waves, one query head
 // each.  The 64-token K/V blocks stream global -> LDS by LDS-DMA (buffer_load ... lds) into a
@@ -306,7 +307,8 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x, hk = blockIdx.y, split = blockIdx.z;
   const int hq = hk * G + w;
-  const int ctx = p.ctx_lens[b];
+  const bool fused = p.knew != nullptr;
+  const int ctx = p.ctx_lens[b] - (fused ? 1 : 0);  // tokens read from the cache
   const int nblk = (ctx + 63) / 64;
   const int per = (nblk + p.num_splits - 1) / p.num_splits;
   const int blk0 = split * per, blk1 = min(nblk, blk0 + per);
@@ -346,7 +348,23 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
     }
   };
 
-  for (int i = lane; i < D; i += 64) sQ[w * D + i] = bf2f(p.q[(long)b * p.q_bs + (long)hq * D + i]) * p.scale * kLog2e;
+  // q stays bf16 (exact: it is the QKV GEMM's bf16 output) for the packed bf16 dot products; the softmax scale
+  // is applied to the f32 score
+  bf16_t* sQb = reinterpret_cast<bf16_t*>(sQ);
+  const int rpos = fused ? p.positions[b] : 0;
+  if (fused) {  // NeoX RoPE on q (f32 math, bf16 result: what rope_qkv_cache would have stored)
+    const bf16_t* qs = p.q + (long)b * p.q_bs + (long)hq * D;
+    const float* cp = p.rope_cos + (long)rpos * (D / 2);
+    const float* sp = p.rope_sin + (long)rpos * (D / 2);
+    for (int i = lane; i < D / 2; i += 64) {
+      const float x0 = bf2f(qs[i]), x1 = bf2f(qs[i + D / 2]), c = cp[i], sn = sp[i];
+      sQb[w * D + i] = f2bf(x0 * c - x1 * sn);
+      sQb[w * D + i + D / 2] = f2bf(x1 * c + x0 * sn);
+    }
+  } else {
+    for (int i = lane; i < D; i += 64) sQb[w * D + i] = p.q[(long)b * p.q_bs + (long)hq * D + i];
+  }
+  const float sl2 = p.scale * kLog2e;
   float m_run = -INFINITY, l_run = 0.f;
   float o0 = 0.f, o1 = 0.f;  // D=128: this lane's d = 2 lane, 2 lane + 1; D=64: d = lane
   if (blk0 < blk1) stage(0, blk0);
@@ -364,42 +382,110 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
     const bf16_t* sV = sK + 64 * D;
     // lane = key
     const int key = bi * 64 + lane;
-    float sc = 0.f;
+    // QK^T: 4 packed bf16 dot products (v_dot2c_f32_bf16) per 8-element chunk, two independent chains
+    float sc0 = 0.f, sc1 = 0.f;
 #pragma unroll
     for (int ch = 0; ch < CPR; ++ch) {
-      float f[8];
-      unpack8(*reinterpret_cast<const uint4_*>(sK + lane * D + ((ch ^ (lane & (CPR - 1))) << 3)), f);
-      const float4_ qa = *reinterpret_cast<const float4_*>(sQ + w * D + ch * 8);
-      const float4_ qb = *reinterpret_cast<const float4_*>(sQ + w * D + ch * 8 + 4);
-      sc += f[0] * qa[0] + f[1] * qa[1] + f[2] * qa[2] + f[3] * qa[3] + f[4] * qb[0] + f[5] * qb[1] + f[6] * qb[2] +
-            f[7] * qb[3];
+      const uint4_ kv = *reinterpret_cast<const uint4_*>(sK + lane * D + ((ch ^ (lane & (CPR - 1))) << 3));
+      const uint4_ qv = *reinterpret_cast<const uint4_*>(sQb + w * D + ch * 8);
+      sc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2d, kv[0]), __builtin_bit_cast(bf16x2d, qv[0]), sc0, false);
+      sc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2d, kv[1]), __builtin_bit_cast(bf16x2d, qv[1]), sc1, false);
+      sc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2d, kv[2]), __builtin_bit_cast(bf16x2d, qv[2]), sc0, false);
+      sc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2d, kv[3]), __builtin_bit_cast(bf16x2d, qv[3]), sc1, false);
     }
+    float sc = (sc0 + sc1) * sl2;
     if (key >= ctx) sc = -INFINITY;
     const float mt = wave_max(sc);
     const float m_new = fmaxf(m_run, mt);
     const float alpha = exp2f(m_run - m_new);
-    const float e = key < ctx ? exp2f(sc - m_new) : 0.f;
-    l_run = l_run * alpha + wave_sum(e);
-    m_run = m_new;
-    sP[w * 64 + lane] = e;
+    float e = key < ctx ? exp2f(sc - m_new) : 0.f;
     o0 *= alpha;
     o1 *= alpha;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's sP row is written before it is read
-#pragma unroll 4
-    for (int k = 0; k < 64; k += 4) {
-      const float4_ pk = *reinterpret_cast<const float4_*>(sP + w * 64 + k);
+    if constexpr (D == 128) {
+      // P goes to LDS as bf16 and the denominator sums the same rounded values; P.V runs as packed bf16 dot
+      // products over key pairs: v_perm gathers (V[k][d], V[k+1][d]) for this lane's two dims d
+      const bf16_t eb = f2bf(e);
+      e = bf2f(eb);
+      l_run = l_run * alpha + wave_sum(e);
+      m_run = m_new;
+      bf16_t* sPb = reinterpret_cast<bf16_t*>(sP);
+      sPb[w * 64 + lane] = eb;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's P row is written before it is read
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll 2
+      for (int k = 0; k < 64; k += 8) {
+        const uint4_ pk = *reinterpret_cast<const uint4_*>(sPb + w * 64 + k);  // P[k .. k+7] as 4 bf16 pairs
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if constexpr (D == 128) {
-          const uint32_t vv = *reinterpret_cast<const uint32_t*>(sV + (k + u) * D + 2 * lane);
-          o0 += pk[u] * bf2f(vv & 0xffff);
-          o1 += pk[u] * bf2f(vv >> 16);
-        } else {
-          o0 += pk[u] * bf2f(sV[(k + u) * D + lane]);
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t va = *reinterpret_cast<const uint32_t*>(sV + (k + 2 * u) * D + 2 * lane);
+          const uint32_t vb = *reinterpret_cast<const uint32_t*>(sV + (k + 2 * u + 1) * D + 2 * lane);
+          const uint32_t lo = __builtin_amdgcn_perm(vb, va, 0x05040100u);  // (V[k][2l],   V[k+1][2l])
+          const uint32_t hi = __builtin_amdgcn_perm(vb, va, 0x07060302u);  // (V[k][2l+1], V[k+1][2l+1])
+          const bf16x2d pp = __builtin_bit_cast(bf16x2d, pk[u]);
+          if (u & 1) {
+            a0 = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2d, lo), a0, false);
+            a1 = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2d, hi), a1, false);
+          } else {
+            o0 = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2d, lo), o0, false);
+            o1 = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2d, hi), o1, false);
+          }
         }
+      }
+      o0 += a0;
+      o1 += a1;
+    } else {
+      l_run = l_run * alpha + wave_sum(e);
+      m_run = m_new;
+      sP[w * 64 + lane] = e;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's sP row is written before it is read
+#pragma unroll 4
+      for (int k = 0; k < 64; k += 4) {
+        const float4_ pk = *reinterpret_cast<const float4_*>(sP + w * 64 + k);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o0 += pk[u] * bf2f(sV[(k + u) * D + lane]);
       }
     }
     __builtin_amdgcn_s_barrier();  // every wave is done with this slot before it is refilled (block bi+2)
+  }
+  if (fused && split == p.num_splits - 1 && p.slots[b] >= 0) {
+    // this step's token: roped k (rounded to bf16, as the cache stores it) and v from the QKV rows, one more
+    // online-softmax key; wave 0 writes both into the cache (no workgroup of this launch reads that row: the
+    // block DMA range-checks it out)
+    const int slot_new = p.slots[b];
+    const bf16_t* kn = p.knew + (long)b * p.new_bs + (long)hk * D;
+    const bf16_t* vn = p.vnew + (long)b * p.new_bs + (long)hk * D;
+    float kr0 = 0.f, kr1 = 0.f, part = 0.f;
+    if (lane < D / 2) {
+      const float x0 = bf2f(kn[lane]), x1 = bf2f(kn[lane + D / 2]);
+      const float c = p.rope_cos[(long)rpos * (D / 2) + lane], sn = p.rope_sin[(long)rpos * (D / 2) + lane];
+      kr0 = bf2f(f2bf(x0 * c - x1 * sn));
+      kr1 = bf2f(f2bf(x1 * c + x0 * sn));
+      part = kr0 * bf2f(sQb[w * D + lane]) + kr1 * bf2f(sQb[w * D + lane + D / 2]);
+    }
+    const float sc = wave_sum(part) * sl2;
+    const float m_new = fmaxf(m_run, sc);
+    const float alpha = exp2f(m_run - m_new);
+    float e = exp2f(sc - m_new);
+    if constexpr (D == 128) e = bf2f(f2bf(e));  // P is bf16 on the cache path too
+    l_run = l_run * alpha + e;
+    m_run = m_new;
+    if constexpr (D == 128) {
+      const uint32_t vv = *reinterpret_cast<const uint32_t*>(vn + 2 * lane);
+      o0 = o0 * alpha + e * bf2f(vv & 0xffff);
+      o1 = o1 * alpha + e * bf2f(vv >> 16);
+    } else {
+      o0 = o0 * alpha + e * bf2f(vn[lane]);
+    }
+    if (w == 0) {
+      const long dst = (((long)(slot_new >> 6) * p.Hkv + hk) * 64 + (slot_new & 63)) * D;
+      bf16_t* kc = const_cast<bf16_t*>(p.k_cache);
+      bf16_t* vc = const_cast<bf16_t*>(p.v_cache);
+      if (lane < D / 2) {
+        kc[dst + lane] = f2bf(kr0);
+        kc[dst + lane + D / 2] = f2bf(kr1);
+      }
+      for (int i = lane; i < D; i += 64) vc[dst + i] = vn[i];
+    }
   }
   if (p.num_splits == 1) {  // no split-K: normalise and write the output here (no combine launch)
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;

@@ -178,6 +178,16 @@ struct DecodeAttnArgs {
   int B, Hq, Hkv, D, max_blocks, num_splits;
   long q_bs, o_bs;
   float scale;
+  // fused decode step (knew != nullptr): q is un-roped; this step's k / v rows ([B, Hkv, D] at row stride
+  // new_bs) are roped / taken from here, written into the cache at slots[b] (-1: padding row) and attended
+  // from registers; ctx_lens count the new token, the cache holds ctx_lens - 1 of them
+  const bf16_t* knew;
+  const bf16_t* vnew;
+  long new_bs;
+  const int* positions;
+  const float* rope_cos;    // [max_pos, D / 2] NeoX halves
+  const float* rope_sin;
+  const int* slots;
 };
 void launch_decode_attn(const DecodeAttnArgs& a, hipStream_t s);
 size_t decode_attn_workspace(int B, int Hq, int D, int num_splits);

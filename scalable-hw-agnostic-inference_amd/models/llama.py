@@ -17,6 +17,7 @@ MI355X-first:
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -28,6 +29,10 @@ from ..parallel.layers import (GLUParallelLinear, ParallelLMHead, QKVParallelLin
                                VocabParallelEmbedding)
 from ..parallel.state import tp
 from .layers import GLULinear, RMSNorm
+
+# decode steps run RoPE + the KV-cache write inside the paged decode-attention kernel (one launch per layer
+# instead of two); SHAI_FUSED_DECODE=0 keeps the separate rope_qkv_cache launch
+FUSED_DECODE = os.environ.get("SHAI_FUSED_DECODE", "1") != "0"
 
 KV_BLOCK = 64
 
@@ -153,6 +158,10 @@ class LlamaAttention(nn.Module):
         T = x.shape[0]
         qkv = self.qkv_proj(x, rms_eps=rms_eps)  # [T, (h + 2hk) * hd]
         h, hk, hd = self.h, self.hk, self.hd
+        if not batch.is_prefill and FUSED_DECODE:  # RoPE + KV-cache write inside the decode attention kernel
+            o = ops.decode_attention_rope(qkv, k_cache, v_cache, batch.block_table, batch.ctx_lens, batch.positions,
+                                          cos, sin, batch.slots, h, hk, self.scale, num_splits=batch.num_splits)
+            return self.o_proj(o, residual=residual)
         ops.rope_qkv_cache(qkv, batch.positions, cos, sin, k_cache, v_cache, batch.slots, h, hk)
         q = qkv[:, : h * hd].view(T, h, hd)
         if batch.is_prefill:

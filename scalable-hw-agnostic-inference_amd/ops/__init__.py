@@ -24,7 +24,7 @@ from .reference import (ACT_GELU, ACT_GELU_TANH, ACT_NONE, ACT_QUICK_GELU, ACT_R
 __all__ = [
     "rmsnorm", "layernorm", "groupnorm_stats", "groupnorm_apply", "groupnorm", "linear", "conv2d", "attention",
     "paged_attention", "decode_attention", "kv_write", "rope", "rope_pairs", "gated_act", "bias_act", "sched_step",
-    "softmax_", "embedding", "token_feedback", "quantize_fp8_rows", "dequant_fp8", "pack_conv_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
+    "softmax_", "embedding", "token_feedback", "decode_attention_rope", "quantize_fp8_rows", "dequant_fp8", "pack_conv_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
     "ACT_GELU_TANH", "ACT_QUICK_GELU", "ACT_RELU", "decode_splits",
 ]
 
@@ -316,6 +316,28 @@ def decode_attention(q, k_cache, v_cache, block_table, ctx_lens, scale=None, num
     ws = torch.empty(B * Hq * num_splits * (D + 2), dtype=torch.float32, device=q.device)
     o = out if out is not None else torch.empty(q.shape, dtype=q.dtype, device=q.device)
     _K().decode_attn(q, k_cache, v_cache, o, _i32(block_table), _i32(ctx_lens), ws, int(num_splits), float(scale))
+    return o
+
+
+def decode_attention_rope(qkv, k_cache, v_cache, block_table, ctx_lens, positions, cos, sin, slots, h: int, hk: int,
+                          scale=None, num_splits: Optional[int] = None, max_ctx: Optional[int] = None, out=None):
+    """One fused decode step on the packed QKV rows qkv [B, (h + 2 hk) D]: NeoX RoPE on q / k, this step's k / v
+    written into the paged caches at ``slots`` (-1: padding row), attention over the cached context plus the
+    new token (``ctx_lens`` count it).  Equivalent to rope_qkv_cache + decode_attention.  Returns [B, h D]."""
+    D = k_cache.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    B = qkv.shape[0]
+    if not _gpu(qkv):
+        rope_qkv_cache(qkv, positions, cos, sin, k_cache, v_cache, slots, h, hk)
+        q = qkv[:, : h * D].reshape(B, h, D)
+        return decode_attention(q, k_cache, v_cache, block_table, ctx_lens, scale).reshape(B, h * D)
+    if num_splits is None:
+        mc = max_ctx if max_ctx is not None else block_table.shape[1] * 64
+        num_splits = decode_splits(B, hk, mc)
+    ws = torch.empty(B * h * num_splits * (D + 2), dtype=torch.float32, device=qkv.device)
+    o = out if out is not None else torch.empty(B, h * D, dtype=qkv.dtype, device=qkv.device)
+    _K().decode_attn_rope(qkv, k_cache, v_cache, o, _i32(block_table), _i32(ctx_lens), _i32(positions), cos, sin,
+                          _i32(slots), ws, int(h), int(hk), int(num_splits), float(scale))
     return o
 
 

@@ -223,3 +223,37 @@ def test_fused_sampler_negative_logits(cuda):
         picked = lf[torch.arange(B, device=cuda), o.long()]
         assert bool((picked >= kth).all()), it
         assert int(o[0]) == int(lf[0].argmax()) and int(o[5]) == int(lf[5].argmax())
+
+
+@pytest.mark.parametrize("D,H,Hk", [(128, 32, 8), (64, 8, 2)])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_fused_decode_rope_attention(cuda, D, H, Hk, splits):
+    """decode_attention_rope (RoPE + KV-cache write + paged decode attention in one kernel) equals
+    rope_qkv_cache followed by decode_attention: same outputs, same cache contents; padding rows
+    (slot -1) write nothing."""
+    torch.manual_seed(D + splits)
+    ctx = [1, 2, 64, 65, 300, 1000, 1]       # context INCLUDING this step's token; last row is padding
+    B, nb = len(ctx), 40
+    qkv = torch.randn(B, (H + 2 * Hk) * D, device=cuda).bfloat16()
+    ang = torch.rand(1024, D // 2, device=cuda) * 3
+    cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
+    kc = torch.randn(nb, Hk, 64, D, device=cuda).bfloat16()
+    vc = torch.randn(nb, Hk, 64, D, device=cuda).bfloat16()
+    maxb = 16
+    perm = torch.randperm(nb, device=cuda).int()
+    bt = torch.zeros(B, maxb, dtype=torch.int32, device=cuda)
+    i = 0
+    for b, c in enumerate(ctx):
+        n = (c + 63) // 64
+        bt[b, :n] = perm[i:i + n]
+        i += n
+    lens = torch.tensor(ctx, dtype=torch.int32, device=cuda)
+    pos = lens - 1
+    slots = torch.stack([bt[b, (c - 1) // 64] * 64 + (c - 1) % 64 for b, c in enumerate(ctx)]).int()
+    slots[-1] = -1
+    kc2, vc2, qkv2 = kc.clone(), vc.clone(), qkv.clone()
+    o = ops.decode_attention_rope(qkv, kc, vc, bt, lens, pos, cos, sin, slots, H, Hk, num_splits=splits)
+    ops.rope_qkv_cache(qkv2, pos, cos, sin, kc2, vc2, slots, H, Hk)
+    want = ops.decode_attention(qkv2[:, :H * D].reshape(B, H, D), kc2, vc2, bt, lens, num_splits=splits)
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    assert _rel(o[:-1], want.reshape(B, H * D)[:-1]) < 1e-2
