@@ -286,6 +286,8 @@ void launch_flash_attn(const AttnArgs& a, hipStream_t s) {
 // ----------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void da_lds_void;
 typedef __bf16 bf16x2d __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8d __attribute__((ext_vector_type(8)));
+#define DA_PAIR(v, i) __builtin_shufflevector(v, v, 2 * (i), 2 * (i) + 1)
 
 // Decode attention, one workgroup per (sequence, KV head, split): G = Hq/Hkv waves, one query head
 // each.  The 64-token K/V blocks stream global -> LDS by LDS-DMA (buffer_load ... lds) into a
@@ -386,12 +388,14 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
     float sc0 = 0.f, sc1 = 0.f;
 #pragma unroll
     for (int ch = 0; ch < CPR; ++ch) {
-      const uint4_ kv = *reinterpret_cast<const uint4_*>(sK + lane * D + ((ch ^ (lane & (CPR - 1))) << 3));
-      const uint4_ qv = *reinterpret_cast<const uint4_*>(sQb + w * D + ch * 8);
-      sc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2d, kv[0]), __builtin_bit_cast(bf16x2d, qv[0]), sc0, false);
-      sc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2d, kv[1]), __builtin_bit_cast(bf16x2d, qv[1]), sc1, false);
-      sc0 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2d, kv[2]), __builtin_bit_cast(bf16x2d, qv[2]), sc0, false);
-      sc1 = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2d, kv[3]), __builtin_bit_cast(bf16x2d, qv[3]), sc1, false);
+      // (pairs taken by shufflevector: bit-casting the elements of a uint32 x4 vector to bf16 x2 miscompiles
+      // with this hipcc -- every pair reads element 0)
+      const bf16x8d kv = __builtin_bit_cast(bf16x8d, *reinterpret_cast<const uint4_*>(sK + lane * D + ((ch ^ (lane & (CPR - 1))) << 3)));
+      const bf16x8d qv = __builtin_bit_cast(bf16x8d, *reinterpret_cast<const uint4_*>(sQb + w * D + ch * 8));
+      sc0 = __builtin_amdgcn_fdot2_f32_bf16(DA_PAIR(kv, 0), DA_PAIR(qv, 0), sc0, false);
+      sc1 = __builtin_amdgcn_fdot2_f32_bf16(DA_PAIR(kv, 1), DA_PAIR(qv, 1), sc1, false);
+      sc0 = __builtin_amdgcn_fdot2_f32_bf16(DA_PAIR(kv, 2), DA_PAIR(qv, 2), sc0, false);
+      sc1 = __builtin_amdgcn_fdot2_f32_bf16(DA_PAIR(kv, 3), DA_PAIR(qv, 3), sc1, false);
     }
     float sc = (sc0 + sc1) * sl2;
     if (key >= ctx) sc = -INFINITY;
@@ -414,22 +418,20 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
       float a0 = 0.f, a1 = 0.f;
 #pragma unroll 2
       for (int k = 0; k < 64; k += 8) {
-        const uint4_ pk = *reinterpret_cast<const uint4_*>(sPb + w * 64 + k);  // P[k .. k+7] as 4 bf16 pairs
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        // P[k .. k+7] as 4 bf16 pairs
+        const bf16x8d pk = __builtin_bit_cast(bf16x8d, *reinterpret_cast<const uint4_*>(sPb + w * 64 + k));
+        auto pv = [&](int u, bf16x2d pp, float& c0, float& c1) {
           const uint32_t va = *reinterpret_cast<const uint32_t*>(sV + (k + 2 * u) * D + 2 * lane);
           const uint32_t vb = *reinterpret_cast<const uint32_t*>(sV + (k + 2 * u + 1) * D + 2 * lane);
           const uint32_t lo = __builtin_amdgcn_perm(vb, va, 0x05040100u);  // (V[k][2l],   V[k+1][2l])
           const uint32_t hi = __builtin_amdgcn_perm(vb, va, 0x07060302u);  // (V[k][2l+1], V[k+1][2l+1])
-          const bf16x2d pp = __builtin_bit_cast(bf16x2d, pk[u]);
-          if (u & 1) {
-            a0 = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2d, lo), a0, false);
-            a1 = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2d, hi), a1, false);
-          } else {
-            o0 = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2d, lo), o0, false);
-            o1 = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2d, hi), o1, false);
-          }
-        }
+          c0 = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2d, lo), c0, false);
+          c1 = __builtin_amdgcn_fdot2_f32_bf16(pp, __builtin_bit_cast(bf16x2d, hi), c1, false);
+        };
+        pv(0, DA_PAIR(pk, 0), o0, o1);
+        pv(1, DA_PAIR(pk, 1), a0, a1);
+        pv(2, DA_PAIR(pk, 2), o0, o1);
+        pv(3, DA_PAIR(pk, 3), a0, a1);
       }
       o0 += a0;
       o1 += a1;
