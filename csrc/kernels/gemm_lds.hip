@@ -297,12 +297,24 @@ __global__ void gemm_splitk_reduce(const GemmArgs p, const float* __restrict__ w
     const int m = (int)(i / n4);
     const int n = (int)(i - (long)m * n4) * 4;
     float v[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < splits; ++s) {
-      const float* src = ws + (long)s * p.M * p.N + (long)m * p.N + n;
-      if (n + 3 < p.N && (p.N & 3) == 0) {
-        const float4_ x = *reinterpret_cast<const float4_*>(src);
-        v[0] += x[0]; v[1] += x[1]; v[2] += x[2]; v[3] += x[3];
-      } else {
+    if (n + 3 < p.N && (p.N & 3) == 0) {
+      // four partial slabs per round with every load issued before the first add (a dependent
+      // load-add chain per split made the fold latency-bound: ~5 us for M = 64 decode GEMMs)
+      const float* src = ws + (long)m * p.N + n;
+      const long slab = (long)p.M * p.N;
+      for (int s0 = 0; s0 < splits; s0 += 4) {
+        float4_ x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          x[u] = s0 + u < splits ? *reinterpret_cast<const float4_*>(src + (s0 + u) * slab) : float4_{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[0] += x[u][0]; v[1] += x[u][1]; v[2] += x[u][2]; v[3] += x[u][3];
+        }
+      }
+    } else {
+      for (int s = 0; s < splits; ++s) {
+        const float* src = ws + (long)s * p.M * p.N + (long)m * p.N + n;
         for (int e = 0; e < 4 && n + e < p.N; ++e) v[e] += src[e];
       }
     }
