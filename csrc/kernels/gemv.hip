@@ -44,14 +44,14 @@ constexpr int SK_BK = 64;       // K per step
 constexpr int SK_WAVES = 4;
 constexpr uint32_t SK_OOB = 0x80000000u;
 
-template <int MB, bool F8 = false, bool XR = false>
+// (An X-in-registers variant with an 8-deep W-only ring measured 10-25 % slower at M = 64 --
+// profiles/mistral7b_b64_async_decode_round2.md -- and was dropped: the X tile in LDS is not the limiter.)
+template <int MB, bool F8 = false>
 struct SkGeom {
   static constexpr int XG = MB / 32;                    // 32-row X groups
-  // XR: X fragments go global -> registers (each is read by exactly one lane of the workgroup), so the
-  // LDS ring holds W only and runs twice as deep for the same LDS
-  static constexpr int STAGES = XR ? 8 : (MB == 32 ? 6 : 4);
+  static constexpr int STAGES = MB == 32 ? 6 : 4;
   static constexpr int W_ELEMS = F8 ? SK_BN * SK_BK / 2 : SK_BN * SK_BK;  // W tile in bf16 units
-  static constexpr int STAGE_ELEMS = XR ? W_ELEMS : W_ELEMS + MB * SK_BK;  // W tile (then X tile)
+  static constexpr int STAGE_ELEMS = W_ELEMS + MB * SK_BK;  // W tile then X tile
   static constexpr int PER = (F8 ? 1 : 2) + XG;         // DMA instructions per wave per step
   static constexpr int RP = MB + 1;                     // padded row of the reduction image
   static constexpr size_t LDS = (size_t)STAGES * STAGE_ELEMS * 2 > (size_t)SK_WAVES * SK_BN * RP * 4
@@ -144,11 +144,10 @@ __device__ __forceinline__ int sk_f8_off(int row, int c8) {
   return row * 64 + (((c8 >> 1) ^ ((row >> 2) & 3)) << 4) + ((c8 & 1) << 3);
 }
 
-template <int MB, bool GLU, int ACT, bool RMS, bool F8, bool XR = false>
+template <int MB, bool GLU, int ACT, bool RMS, bool F8>
 __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmArgs p, float* __restrict__ ws,
                                                                     int kg_steps, unsigned* __restrict__ cnt) {
-  using G = SkGeom<MB, F8, XR>;
-  static_assert(!(XR && F8), "X-in-registers variant is bf16-only");
+  using G = SkGeom<MB, F8>;
   constexpr int XG = G::XG;
   extern __shared__ __attribute__((aligned(16))) bf16_t sk_smem[];
   __shared__ float ss_red[SK_WAVES][64 * XG];
@@ -197,14 +196,12 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
                                                  0);
       }
     }
-    if constexpr (!XR) {
 #pragma unroll
-      for (int j = 0; j < XG; ++j) {
-        const int r = xr + 32 * j, k = k0 + xc * 8;
-        const uint32_t off = (r < p.M && k < p.K) ? (uint32_t)(((long)r * p.lda + k) * 2) : SK_OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (sk_lds_void*)(sx + (32 * j + w * 8) * SK_BK), 16, off, 0, 0,
-                                                 0);
-      }
+    for (int j = 0; j < XG; ++j) {
+      const int r = xr + 32 * j, k = k0 + xc * 8;
+      const uint32_t off = (r < p.M && k < p.K) ? (uint32_t)(((long)r * p.lda + k) * 2) : SK_OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (sk_lds_void*)(sx + (32 * j + w * 8) * SK_BK), 16, off, 0, 0,
+                                               0);
     }
   };
 
@@ -221,72 +218,11 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
   for (int j = 0; j < XG; ++j) ss[j] = 0.f;
   const int fr = lane & 31, fh = lane >> 5;
   const int ch = 2 * w + fh;  // this lane's 8-element chunk of the step's K range
-  if constexpr (XR) {
-    // X fragment of this lane for step `step`: row 32 j + fr, 8-element chunk ch (zero-filled rows >= M and
-    // chunks >= K by the buffer range check), issued right behind the step's W DMA so the counted vmcnt that
-    // retires the W tile retires it too.  Every step issues exactly one group (steps >= nk with out-of-range
-    // offsets: no memory traffic), so the wait before step kt is vmcnt((S - 2) * PER) and the
-    // compiler's own waits on the X registers see one fixed pattern.  The ring of S register slots is
-    // indexed statically: the loop is unrolled by S, so the ring slot (= step % S) is the unrolled index.
-    constexpr int S = G::STAGES;
-    bf16x8s xq[S][XG];
-    auto issue = [&](int buf, bf16x8s (&dst)[XG], int step) {
-      const bool live = step >= 0 && step < nk;
-      bf16_t* sw = sk_smem + buf * G::STAGE_ELEMS;
-      const int k0 = (t0 + step) * SK_BK;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = n0 + wr[j], k = k0 + wc[j] * 8;
-        const uint32_t off = (live && n < p.N && k < p.K) ? (uint32_t)(((long)n * p.ldw + k) * 2) : SK_OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (sk_lds_void*)(sw + (w * 2 + j) * 8 * SK_BK), 16, off, 0, 0,
-                                                 0);
-      }
-      const int k = k0 + ch * 8;
-#pragma unroll
-      for (int j = 0; j < XG; ++j) {
-        const int r = 32 * j + fr;
-        const uint32_t off = (live && r < p.M && k < p.K) ? (uint32_t)(((long)r * p.lda + k) * 2) : SK_OOB;
-        dst[j] = __builtin_bit_cast(bf16x8s, __builtin_amdgcn_raw_buffer_load_b128(rX, off, 0, 0));
-      }
-    };
-    auto body = [&](int u, int kt) {
-      // the X loads of steps past nk are dead and may be elided by the compiler, so the last S-2 steps drain
-      // instead of counting (their data is all in flight by then)
-      if (kt + S - 2 >= nk) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 2) * G::PER) : "memory");
-      __builtin_amdgcn_s_barrier();
-      issue((u + S - 1) % S, xq[(u + S - 1) % S], kt + S - 1);  // buffer of step kt-1: every wave is past it
-      if (kt < 0 || kt >= nk) return;
-      const bf16_t* sw = sk_smem + u * G::STAGE_ELEMS;
-      const bf16x8s w0 = *reinterpret_cast<const bf16x8s*>(sw + sk_swz(fr, ch));
-      const bf16x8s w1 = *reinterpret_cast<const bf16x8s*>(sw + sk_swz(32 + fr, ch));
-#pragma unroll
-      for (int j = 0; j < XG; ++j) {
-        const bf16x8s xf = xq[u][j];
-        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, xf, acc[0][j], 0, 0, 0);
-        acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, xf, acc[1][j], 0, 0, 0);
-        if constexpr (RMS) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float f = (float)xf[e];
-            ss[j] += f * f;
-          }
-        }
-      }
-    };
-    // one loop, one body: the first block (kt < 0) only issues steps 0 .. S-2, the last block's steps past nk
-    // only wait and issue empty groups -- every X register is defined inside the loop, so nothing is copied
-    // (and drained) at loop entry or exit
-    for (int kt0 = -S; kt0 < nk; kt0 += S) {
-#pragma unroll
-      for (int u = 0; u < S; ++u) body(u, kt0 + u);
-    }
-  }
 #pragma unroll
   for (int i = 0; i < G::STAGES - 1; ++i)
-    if (!XR && i < nk) stage(i, i);
+    if (i < nk) stage(i, i);
   int buf = 0;
-  for (int kt = 0; kt < (XR ? 0 : nk); ++kt) {
+  for (int kt = 0; kt < nk; ++kt) {
     sk_wait_upto<G::PER, G::STAGES - 2>(min(G::STAGES - 2, nk - 1 - kt));
     __builtin_amdgcn_s_barrier();
     if (kt + G::STAGES - 1 < nk) {
@@ -536,16 +472,16 @@ static unsigned* sk_tickets(hipStream_t s) {
   return tickets[dev];
 }
 
-template <int MB, bool F8, bool XR>
+template <int MB, bool F8>
 static void launch_skinny_mb(const GemmArgs& a, float* ws, int kg, unsigned* cnt, hipStream_t s) {
   const int ksteps = (a.K + SK_BK - 1) / SK_BK;
   const int kg_steps = (ksteps + kg - 1) / kg;
   dim3 grid((a.N + SK_BN - 1) / SK_BN, kg), block(SK_WAVES * 64);
-  const size_t lds = SkGeom<MB, F8, XR>::LDS;
+  const size_t lds = SkGeom<MB, F8>::LDS;
 #define SK(G, A)                                                                                          \
   do {                                                                                                    \
-    if (a.rms) skinny_gemm_kernel<MB, G, A, true, F8, XR><<<grid, block, lds, s>>>(a, ws, kg_steps, cnt);  \
-    else skinny_gemm_kernel<MB, G, A, false, F8, XR><<<grid, block, lds, s>>>(a, ws, kg_steps, cnt);       \
+    if (a.rms) skinny_gemm_kernel<MB, G, A, true, F8><<<grid, block, lds, s>>>(a, ws, kg_steps, cnt);  \
+    else skinny_gemm_kernel<MB, G, A, false, F8><<<grid, block, lds, s>>>(a, ws, kg_steps, cnt);       \
   } while (0)
 #define SK_ACT(G)                                      \
   switch (a.act) {                                     \
@@ -573,17 +509,12 @@ void launch_skinny_kg(const GemmArgs& a, float* ws, int kg, hipStream_t s, bool 
   // split-K: fixed up inside the launch when asked for and tickets are available, else a separate fold
   unsigned* cnt = nullptr;
   if (kg > 1 && fixup && (a.N + SK_BN - 1) / SK_BN <= kSkTickets) cnt = sk_tickets(s);
-  // SHAI_SKINNY_XR=1: X fragments global -> registers, 8-deep W-only LDS ring (A/B against the X-in-LDS ring)
-  static const bool xr = getenv("SHAI_SKINNY_XR") != nullptr && atoi(getenv("SHAI_SKINNY_XR")) != 0;
   if (a.w_scale) {
-    if (a.M <= 32) launch_skinny_mb<32, true, false>(a, ws, kg, cnt, s);
-    else launch_skinny_mb<64, true, false>(a, ws, kg, cnt, s);
-  } else if (xr) {
-    if (a.M <= 32) launch_skinny_mb<32, false, true>(a, ws, kg, cnt, s);
-    else launch_skinny_mb<64, false, true>(a, ws, kg, cnt, s);
+    if (a.M <= 32) launch_skinny_mb<32, true>(a, ws, kg, cnt, s);
+    else launch_skinny_mb<64, true>(a, ws, kg, cnt, s);
   } else {
-    if (a.M <= 32) launch_skinny_mb<32, false, false>(a, ws, kg, cnt, s);
-    else launch_skinny_mb<64, false, false>(a, ws, kg, cnt, s);
+    if (a.M <= 32) launch_skinny_mb<32, false>(a, ws, kg, cnt, s);
+    else launch_skinny_mb<64, false>(a, ws, kg, cnt, s);
   }
   if (kg > 1 && cnt == nullptr) launch_splitk_epilogue(a, ws, kg, s);
 }
