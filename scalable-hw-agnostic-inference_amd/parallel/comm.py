@@ -47,6 +47,57 @@ def all_reduce(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> to
     return x
 
 
+# Row-parallel compute/communication overlap: a RowParallel GEMM with at least
+# OVERLAP_MIN_ROWS rows is split into OVERLAP_CHUNKS row chunks; chunk i's all-reduce runs on a side stream
+# while chunk i+1's GEMM runs on the compute stream (a fork / join of events, so it is HIP-graph capturable).
+OVERLAP_CHUNKS = int(os.environ.get("SHAI_TP_OVERLAP_CHUNKS", "2"))
+OVERLAP_MIN_ROWS = int(os.environ.get("SHAI_TP_OVERLAP_MIN_ROWS", "1024"))
+_SIDE: dict = {}
+
+
+def _side_stream(device: torch.device) -> "torch.cuda.Stream":
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _SIDE:
+        _SIDE[idx] = torch.cuda.Stream(device=idx)
+    return _SIDE[idx]
+
+
+def overlap_chunks(rows: int) -> int:
+    """How many row chunks a row-parallel GEMM of ``rows`` rows is split into (1: no overlap)."""
+    if tp().size == 1 or OVERLAP_CHUNKS <= 1 or rows < OVERLAP_MIN_ROWS:
+        return 1
+    return max(1, min(OVERLAP_CHUNKS, rows))
+
+
+def all_reduce_overlapped(x2d: torch.Tensor, gemm_chunk, out: torch.Tensor, chunks: int,
+                          group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """out[r0:r1] = sum over the TP group of gemm_chunk(x2d[r0:r1], out[r0:r1]) for ``chunks`` row chunks.
+
+    GPU: the GEMMs run in order on the current stream; after each, an event forks the chunk's all-reduce onto a
+    side stream (RCCL or the xGMI P2P kernel, both stream-ordered), so chunk i's collective overlaps chunk
+    i+1's GEMM; the current stream joins the side stream at the end.  CPU (gloo): the same chunking, serially."""
+    M = x2d.shape[0]
+    step = (M + chunks - 1) // chunks
+    bounds = [(r, min(M, r + step)) for r in range(0, M, step)]
+    if not x2d.is_cuda:
+        for r0, r1 in bounds:
+            gemm_chunk(x2d[r0:r1], out[r0:r1])
+            all_reduce(out[r0:r1], group)
+        return out
+    cur = torch.cuda.current_stream(x2d.device)
+    side = _side_stream(x2d.device)
+    side.wait_stream(cur)   # the output buffer / inputs are ready before the side stream touches them
+    for r0, r1 in bounds:
+        gemm_chunk(x2d[r0:r1], out[r0:r1])
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            all_reduce(out[r0:r1], group)
+    cur.wait_stream(side)
+    return out
+
+
 def all_gather_last(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
     """Concatenate the TP shards along the last dim."""
     st = tp()

@@ -101,8 +101,21 @@ class RowParallelLinear(_ShardLoadMixin, nn.Module):
             x = x.narrow(-1, self.tp_rank * self.in_local, self.in_local).contiguous()
         if self.tp_size == 1:
             return ops.linear(x, self.weight, self.bias, residual=residual, w_scale=self.w_scale)
-        y = ops.linear(x, self.weight, None, w_scale=self.w_scale)
-        comm.all_reduce(y)
+        rows = x.numel() // x.shape[-1]
+        nch = comm.overlap_chunks(rows)
+        if nch > 1:  # chunk i's all-reduce overlaps chunk i+1's GEMM
+            x2 = x.reshape(rows, x.shape[-1])
+            y = torch.empty(rows, self.out_features, dtype=x.dtype, device=x.device)
+            def gemm_chunk(xs, ys):
+                if ys.is_cuda and self.w_scale is None:
+                    ops.gemm_into(xs, self.weight, ys)
+                else:
+                    ys.copy_(ops.linear(xs, self.weight, None, w_scale=self.w_scale))
+            comm.all_reduce_overlapped(x2, gemm_chunk, y, nch)
+            y = y.view(*x.shape[:-1], self.out_features)
+        else:
+            y = ops.linear(x, self.weight, None, w_scale=self.w_scale)
+            comm.all_reduce(y)
         if self.bias is not None or residual is not None:
             y = ops.bias_act(y, self.bias, residual)
         return y

@@ -13,3 +13,11 @@ def test_p2p_allreduce_two_ranks_one_gpu(cuda):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     mp.spawn(p2p_worker.run, args=(2, port), nprocs=2, join=True)
+
+
+def test_row_parallel_overlap_two_ranks_one_gpu(cuda):
+    import tp_overlap_worker
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(tp_overlap_worker.run, args=(2, port), nprocs=2, join=True)

@@ -1,0 +1,60 @@
+"""Two ranks on ONE GPU: the row-parallel compute / communication overlap path (chunk GEMMs on the compute
+stream, each chunk's all-reduce forked onto a side stream through the IPC P2P all-reduce) equals the dense
+product, eagerly and replayed from a HIP graph."""
+import os
+
+import torch
+
+
+def run(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    from shai_amd.parallel import comm
+    from shai_amd.parallel.layers import RowParallelLinear
+    from shai_amd.parallel.state import init_distributed
+    from shai_amd.weights import load_into
+    init_distributed("gloo", tp_size=world)
+    p2p = comm.P2PAllReduce(None, max_bytes=16 << 20)
+    comm.enable_p2p(p2p)
+    comm.OVERLAP_MIN_ROWS, comm.OVERLAP_CHUNKS = 256, 4
+    g = torch.Generator().manual_seed(11)
+    K, N, M = 3072, 3072, 1056                       # Flux 512^2 single-block out-projection shape
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).bfloat16()
+    x = torch.randn(M, K, generator=g).bfloat16()
+    res = torch.randn(M, N, generator=g).bfloat16()
+    lin = RowParallelLinear(K, N, bias=False, input_is_parallel=False).cuda()
+    load_into(lin, {"weight": w}, strict=True)
+    xc, rc = x.cuda(), res.cuda()
+    want = (x.float() @ w.float().t() + res.float()).cuda()
+    assert comm.overlap_chunks(M) == 4
+
+    def rel(a):
+        return ((a.float() - want).norm() / want.norm()).item()
+
+    for _ in range(3):
+        y = lin(xc, residual=rc)
+        torch.cuda.synchronize()
+        assert rel(y) < 2e-2, rel(y)
+        dist.barrier()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        lin(xc, residual=rc)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    dist.barrier()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        yg = lin(xc, residual=rc)
+    for _ in range(3):
+        dist.barrier()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert rel(yg) < 2e-2, rel(yg)
+    assert not p2p.error()
+    dist.barrier()
+    comm.enable_p2p(None)
+    p2p.close()
+    dist.destroy_process_group()

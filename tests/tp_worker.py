@@ -65,8 +65,12 @@ def run(rank, world, port, which):
         m2 = T5EncoderModel(c)
         load_into(m2, dict(sd), strict=True)
         _close(m2(ids, mask), ref, 1e-2)
-    elif which in ("flux", "flux_sp"):
+    elif which in ("flux", "flux_sp", "flux_ovl"):
         # flux_sp: sequence-parallel single blocks (S/n-row residual shards, all-gather + reduce-scatter)
+        # flux_ovl: every row-parallel GEMM chunked with its all-reduce overlapped
+        if which == "flux_ovl":
+            from shai_amd.parallel import comm
+            comm.OVERLAP_MIN_ROWS, comm.OVERLAP_CHUNKS = 1, 2
         from shai_amd.models.flux import FluxConfig, FluxTransformer2DModel
         c = FluxConfig.tiny()
         c.sequence_parallel = which == "flux_sp"
@@ -86,6 +90,19 @@ def run(rank, world, port, which):
         load_into(m2, dict(sd), strict=True)
         with torch.no_grad():
             _close(m2(lat, t5, pooled, t, g, img_hw=(4, 6)), ref, 3e-2)
+    elif which == "row_overlap":
+        # chunked row-parallel GEMM + all-reduce (compute / communication overlap path) vs the dense product
+        from shai_amd.parallel import comm
+        from shai_amd.parallel.layers import RowParallelLinear
+        init_distributed("gloo", tp_size=world)
+        comm.OVERLAP_MIN_ROWS, comm.OVERLAP_CHUNKS = 1, 3
+        g = torch.Generator().manual_seed(5)
+        w, b = torch.randn(48, 64, generator=g), torch.randn(48, generator=g)
+        x, res = torch.randn(2, 300, 64, generator=g), torch.randn(2, 300, 48, generator=g)
+        lin = RowParallelLinear(64, 48, bias=True, input_is_parallel=False, dtype=torch.float32)
+        load_into(lin, {"weight": w, "bias": b}, strict=True)
+        assert comm.overlap_chunks(600) == 3 and comm.overlap_chunks(2) == 2
+        _close(lin(x, residual=res), x @ w.t() + b + res, 1e-5)
     elif which == "seq_comm":
         from shai_amd.parallel import comm
         init_distributed("gloo", tp_size=world)
