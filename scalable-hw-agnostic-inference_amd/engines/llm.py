@@ -13,8 +13,15 @@ Per engine step (one call to :meth:`LLMEngine.step`):
      ``prefill_chunk`` are prefilled chunk by chunk, the chunks alternating with
      decode steps so running sequences keep streaming (chunked prefill);
   3. otherwise every running sequence decodes one token -- the decode forward
-     for each batch-size bucket is captured once into a HIP graph and replayed;
-  4. sampling (temperature / top-k / top-p; greedy at temperature 0) on device.
+     for each batch-size bucket is captured once into a HIP graph and replayed,
+     with the fused RoPE / KV-write / attention kernel and the sampler inside;
+  4. sampling (temperature / top-k / top-p; greedy at temperature 0) on device,
+     from host-drawn uniforms (deterministic for a seed, identical on TP ranks).
+With ``async_decode`` (default) steady-state decode runs one step ahead of the
+host: step t+1 is enqueued (its input tokens fed from step t's output on the
+device) before step t's tokens are read back, so a sequence's ``output`` grows
+one ``step()`` call after its token was computed; a step past a stop token is
+dropped, and steps that would pass ``max_tokens`` are never enqueued.
 With TP > 1 every rank runs the same deterministic loop (SPMD); logits are
 all-gathered so all ranks sample identically.
 """
