@@ -361,6 +361,23 @@ class LLMEngine:
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "steps": 0, "prefix_hit_tokens": 0}
         self.eos = {cfg.eos_token_id}
 
+    def warmup_graphs(self, greedy_too: bool = False) -> int:
+        """Capture the decode-step HIP graph of every batch bucket (1, 2, 4, ... >= max_num_seqs) now, so no
+        request pays a capture when the running batch first reaches a new bucket.  Returns how many were
+        captured.  (The warm-up forwards use padding rows only: no KV-cache row is written.)"""
+        if not self.use_graphs:
+            return 0
+        n, Bc = 0, 1
+        while True:
+            for greedy in ((False, True) if greedy_too else (False,)):
+                key = (Bc, False, greedy)
+                if key not in self._graphs:
+                    self._graphs[key] = _DecodeGraph(self, Bc, cross=False, greedy=greedy)
+                    n += 1
+            if Bc >= self.max_num_seqs:
+                return n
+            Bc *= 2
+
     # ------------------------------------------------------------------ requests
     def add_request(self, prompt: Sequence[int], params: Optional[SamplingParams] = None, image=None) -> Sequence_:
         """image: PIL image / HWC uint8 array / preprocess_image() dict (multimodal models only); the prompt

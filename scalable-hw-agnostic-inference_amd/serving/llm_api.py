@@ -48,6 +48,9 @@ def build_service(env: ServerEnv):
                     max_num_seqs=int(vc.get("max_num_seqs", 64)),
                     max_model_len=int(vc.get("max_model_len", min(8192, text.max_position_embeddings))),
                     enable_prefix_caching=True, quantization=vc.get("quantization"))
+    import torch
+    with torch.inference_mode():
+        eng.warmup_graphs()   # every decode batch bucket captured before the first request
     specials = {"<|begin_of_text|>": text.bos_token_id}
     if text is not cfg:
         specials["<|image|>"] = cfg.image_token_index

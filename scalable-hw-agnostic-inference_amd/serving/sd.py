@@ -13,6 +13,7 @@ one pipeline call per request on a shared, unsynchronised pipeline.
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Optional
 
@@ -45,8 +46,15 @@ def create_app(engine=None, env: Optional[ServerEnv] = None, max_batch: int = 8,
         img = worker.submit_batched(int(steps or env.num_inference_steps), prompt).result()
         return img, str(time.time() - t0)
 
-    # import-time warm-up, as the reference does (run-sd.py:144-146)
-    worker.call(lambda: engine.generate([WARMUP_PROMPT], min(env.num_inference_steps, 2)))
+    # import-time warm-up, as the reference does (run-sd.py:144-146); it also captures the UNet-step HIP graph
+    # of every batch size the dynamic batcher can form, so no request pays a capture later
+    # (SHAI_WARMUP_ALL_BATCHES=0: batch size 1 only)
+    def warm():
+        engine.generate([WARMUP_PROMPT], min(env.num_inference_steps, 2))
+        if os.environ.get("SHAI_WARMUP_ALL_BATCHES", "1") != "0":
+            for b in range(2, max_batch + 1):
+                engine.generate([WARMUP_PROMPT] * b, 1)
+    worker.call(warm)
 
     app = base_app(env, f"{env.model_id} SD2.1{title_suffix}", spaced=False)
     app.state.engine, app.state.worker = engine, worker

@@ -71,6 +71,8 @@ def test_llm_engine_async_decode_gpu(cuda):
     gs = SamplingParams(max_tokens=12, temperature=0.0, ignore_eos=True, stop_token_ids=[t])
     want = [s.output for s in mk(False).generate(prompts, gs)]
     e = mk(True)
+    with torch.inference_mode():
+        assert e.warmup_graphs(greedy_too=True) == 6   # buckets 1, 2, 4 x {sampled, greedy}
     got = [s.output for s in e.generate(prompts, gs)]
     assert got == want and len(want[j]) == i + 1
     assert e._inflight is None and e.bm.num_free == e.num_kv_blocks

@@ -28,7 +28,7 @@ import shai_amd  # noqa: F401
 from shai_amd.bench.client import run_clients
 from shai_amd.bench.breaking_point import find_breaking_point
 url = "http://127.0.0.1:8000/load/1/infer/50"
-warm = run_clients(8, url, 25.0).summary()           # every batch bucket captured before the ramp
+warm = run_clients(8, url, 15.0).summary()           # (the server captured every batch bucket at start-up)
 res = find_breaking_point(url, step_s=25.0, clients_seq=[1, 2, 3, 4, 6, 8, 12, 16])
 res["warmup"] = warm
 res["request"] = "GET /load/1/infer/50 (1 image, 512x512, 50 DDIM steps, CFG 7.5)"
