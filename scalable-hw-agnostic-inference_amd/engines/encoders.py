@@ -119,6 +119,16 @@ class ImageClassifierEngine:
         return out
 
     @torch.inference_mode()
+    def warmup(self, max_batch: int) -> int:
+        """Capture the HIP graph of every batch size 1 .. max_batch now (a serving replica's dynamic batcher
+        forms any of them); returns how many graphs exist."""
+        if self.use_graphs:
+            H, W = self.cfg.image_size
+            for b in range(1, max_batch + 1):
+                self.logits_u8(torch.zeros(b, H, W, 3, dtype=torch.uint8, device=self.device))
+        return len(self._graphs)
+
+    @torch.inference_mode()
     def classify(self, images) -> List[str]:
         H, W = self.cfg.image_size
         x = torch.stack([_resize_u8(_to_u8(im) if not isinstance(im, torch.Tensor) else im, H, W)

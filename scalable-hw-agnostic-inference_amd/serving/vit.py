@@ -6,6 +6,7 @@ network).  The model stays resident on the GPU (the reference reloads it per
 request, run-vit.py:40-41) and concurrent requests are batched.
 """
 
+import os
 import time
 from typing import Optional
 
@@ -35,6 +36,8 @@ def create_app(engine=None, env: Optional[ServerEnv] = None):
         return label, time.time() - t0
 
     classify_image(synthetic_image())  # warm-up (reference uses a COCO URL; no network here)
+    if os.environ.get("SHAI_WARMUP_ALL_BATCHES", "1") != "0" and hasattr(engine, "warmup"):
+        worker.call(lambda: engine.warmup(32))  # every batch size's graph, before the first request
     app = base_app(env, f"{env.compiled_model_id} image classification", spaced=False)
 
     class Item(BaseModel):

@@ -192,3 +192,15 @@ def test_vit_graph_replay_matches_eager(cuda):
         got = eng.logits_u8(x).float().clone()
         want = eng._forward_u8(x).float()
         assert torch.allclose(got, want, atol=1e-2, rtol=1e-2), i
+
+
+def test_vit_warmup_captures_every_batch(cuda):
+    """A serving replica captures every batch size's graph up front; a later batch replays it."""
+    from shai_amd.engines.encoders import ImageClassifierEngine
+    from shai_amd.models.vit import ViTConfig
+    eng = ImageClassifierEngine(ViTConfig.vit_base(), device=cuda, seed=0)
+    assert eng.warmup(5) == 5
+    x = torch.randint(0, 256, (3, 224, 224, 3), device=cuda, dtype=torch.uint8)
+    got = eng.logits_u8(x).float().clone()
+    assert len(eng._graphs) == 5
+    assert torch.allclose(got, eng._forward_u8(x).float(), atol=1e-2, rtol=1e-2)
