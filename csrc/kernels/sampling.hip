@@ -39,7 +39,9 @@ __global__ void __launch_bounds__(SMP_T) sample_kernel(const void* __restrict__ 
                                                        const float* __restrict__ temps, const int* __restrict__ topk,
                                                        const float* __restrict__ topp,
                                                        const float* __restrict__ uniforms, int* __restrict__ out) {
-  __shared__ uint32_t hist[SMP_WAVES][256];
+  // 4 histogram copies per wave (by lane & 3): logits crowd into a few exponent bins, and same-address LDS
+  // atomics of one wave instruction serialise -- the copies cut the worst case from 64-way to 16-way
+  __shared__ uint32_t hist[SMP_WAVES][4][256];
   __shared__ uint32_t tot[256];
   __shared__ float cval[SMP_MAXK];
   __shared__ int cidx[SMP_MAXK];
@@ -61,19 +63,19 @@ __global__ void __launch_bounds__(SMP_T) sample_kernel(const void* __restrict__ 
   uint32_t mask = 0;
   // bf16 logits: the low 16 bits of a key are fixed by its sign, so the top two digits already fix the threshold
   for (int pass = 3; pass >= (BF16 ? 2 : 0); --pass) {
-    for (int i = tid; i < SMP_WAVES * 256; i += SMP_T) (&hist[0][0])[i] = 0;
+    for (int i = tid; i < SMP_WAVES * 4 * 256; i += SMP_T) (&hist[0][0][0])[i] = 0;
     __syncthreads();
     const uint32_t prefix = s_prefix;
     const int sh = 8 * pass;
     for (int i = tid; i < V; i += SMP_T) {
       const uint32_t key = f2key(smp_load<BF16>(base, i));
-      if ((key & mask) == prefix) atomicAdd(&hist[w][(key >> sh) & 255], 1u);
+      if ((key & mask) == prefix) atomicAdd(&hist[w][lane & 3][(key >> sh) & 255], 1u);
     }
     __syncthreads();
     if (tid < 256) {
       uint32_t s = 0;
 #pragma unroll
-      for (int q = 0; q < SMP_WAVES; ++q) s += hist[q][tid];
+      for (int q = 0; q < SMP_WAVES; ++q) s += (hist[q][0][tid] + hist[q][1][tid]) + (hist[q][2][tid] + hist[q][3][tid]);
       tot[tid] = s;
     }
     __syncthreads();
