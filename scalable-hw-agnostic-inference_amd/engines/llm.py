@@ -69,6 +69,7 @@ class Sequence_:
     img_pos: int = -1                                            # index of <|image|> in the prompt
     cross_blocks: List[int] = field(default_factory=list)        # paged blocks holding the image K/V
     prefill_started: bool = False                                # first prefill chunk done (blocks held)
+    rng_key: int = 0                                             # sampling-noise stream (seq_uniforms)
     arrival: float = field(default_factory=time.perf_counter)
     first_token_time: Optional[float] = None
     finish_time: Optional[float] = None
@@ -86,6 +87,26 @@ class Sequence_:
     @property
     def last_token(self) -> int:
         return self.output[-1] if self.output else self.prompt[-1]
+
+
+def _mix64(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser on uint64 arrays (wrap-around arithmetic)."""
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def seq_uniforms(keys: Sequence[int], positions: Sequence[int]) -> np.ndarray:
+    """One U[0,1) float32 per (sequence key, absolute token position): a counter-based draw, so a sequence's
+    sampling noise depends only on its key (``SamplingParams.seed`` or engine seed + sequence id) and on the
+    position of the token being sampled -- not on which other sequences share the batch, on look-ahead
+    steps whose tokens are dropped, or on preemption (a recomputed sequence redraws the same values)."""
+    k = np.asarray(keys, dtype=np.uint64)
+    p = np.asarray(positions, dtype=np.uint64)
+    h = _mix64(_mix64(k) ^ p)
+    return (h >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / (1 << 24))
 
 
 def _chain_hash(prev: int, toks: Sequence[int]) -> int:
@@ -347,7 +368,7 @@ class LLMEngine:
         self._graphs: Dict[tuple, _DecodeGraph] = {}
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
-        self.rng = np.random.default_rng(seed)  # sampling uniforms (host-drawn: identical on every TP rank)
+        self.seed = int(seed)   # sampling uniforms: seq_uniforms(key, position), host-drawn (identical on TP ranks)
         # decode steps run one ahead of the host (step t+1 enqueued before step t's tokens are read back)
         if async_decode is None:
             async_decode = os.environ.get("SHAI_ASYNC_DECODE", "1") != "0"
@@ -396,12 +417,31 @@ class LLMEngine:
                 at = 1 if prompt and prompt[0] == self.cfg.bos_token_id else 0
                 prompt = prompt[:at] + [itok] + prompt[at:]
             pos = prompt.index(itok)
-        s = Sequence_(next(self._ids), prompt, params, image=img, img_pos=pos)
+        sid = next(self._ids)
+        key = (int(params.seed) & ((1 << 63) - 1)) | (1 << 63) if params.seed is not None else (self.seed << 32) + sid
+        s = Sequence_(sid, prompt, params, image=img, img_pos=pos, rng_key=key)
         self.waiting.append(s)
         return s
 
     def has_work(self) -> bool:
         return bool(self.waiting or self.running or self._inflight is not None)
+
+    def abort_all(self) -> List[Sequence_]:
+        """Drop every request (after a failed step): KV blocks go back to the pool, nothing stays in flight.
+        Returns the aborted sequences."""
+        if self._inflight is not None and self._inflight.event is not None:
+            try:
+                self._inflight.event.synchronize()
+            except Exception:  # the failed step's event may itself be broken
+                pass
+        self._inflight = None
+        gone = self.waiting + self.running
+        for s in gone:
+            if s.blocks or s.cross_blocks:
+                self._free(s)
+            s.finished, s.finish_reason = True, "abort"
+        self.waiting, self.running = [], []
+        return gone
 
     # ------------------------------------------------------------------ kv blocks
     def _ensure_blocks(self, s: Sequence_, n_tokens: int) -> bool:
@@ -575,7 +615,9 @@ class LLMEngine:
         g = self._graphs.get(key)
         if g is None:
             g = self._graphs[key] = _DecodeGraph(self, Bc, cross=cross is not None, greedy=greedy)
-        u = self.rng.random(B, dtype=np.float32) if not greedy else np.zeros(B, np.float32)
+        # noise for the token each row samples, at absolute position ctx_before + 1
+        u = (seq_uniforms([s.rng_key for s in seqs], [c + 1 for c in ctx_before]) if not greedy
+             else np.zeros(B, np.float32))
         toks, ev = g.launch(seqs, pos, slots, lens, bt, ids, rowmap, u, cross)
         self.stats["decode_tokens"] += B
         return _Inflight(seqs, toks, ev, cross is not None)
@@ -625,7 +667,8 @@ class LLMEngine:
         tk = torch.tensor([s.params.top_k for s in seqs], dtype=torch.int64, device=d)
         tpp = torch.tensor([s.params.top_p for s in seqs], dtype=torch.float32, device=d)
         greedy = all(s.params.temperature <= 0 for s in seqs)
-        u = None if greedy else torch.from_numpy(self.rng.random(len(seqs), dtype=np.float32)).to(d)
+        u = None if greedy else torch.from_numpy(seq_uniforms([s.rng_key for s in seqs],
+                                                              [s.length for s in seqs])).to(d)
         toks = sample(logits, temps, tk, tpp, self.gen, all_greedy=greedy, uniforms=u).tolist()
         self._append(seqs, toks)
 
@@ -748,18 +791,48 @@ def bench_decode_throughput(args, rank, world):
 
 
 # ---------------------------------------------------------------------- online service
+def engine_step(engine: LLMEngine, adds) -> tuple:
+    """Add ``adds`` = [(token ids, SamplingParams, image or None), ...] to ``engine`` and run one step.
+
+    The unit of work of :class:`LLMService` -- and, at TP > 1, exactly what every follower rank executes
+    for each STEP message the leader broadcasts (serving/tp.py), so all ranks make identical scheduling
+    and sampling decisions and their collectives line up.  Returns (per-add Sequence_ or exception,
+    finished sequences, step exception or None); a failed step aborts every request (KV blocks freed)."""
+    added = []
+    for ids, params, image in adds:
+        try:
+            added.append(engine.add_request(ids, params, image=image))
+        except Exception as e:  # bad request (e.g. an image for a text-only model)
+            added.append(e)
+    if not engine.has_work():
+        return added, [], None
+    try:
+        with torch.inference_mode():
+            return added, engine.step(), None
+    except Exception as e:  # noqa: BLE001
+        engine.abort_all()
+        return added, [], e
+
+
 class LLMService:
     """Thread-safe front end: a dedicated engine thread runs continuous batching;
     callers submit prompts (text or ids) and wait on futures.
 
     Replaces the reference's offline ``LLM.generate`` per HTTP request
-    (app/vllm_model_api.py:38-43), so concurrent requests share decode steps."""
+    (app/vllm_model_api.py:38-43), so concurrent requests share decode steps.
 
-    def __init__(self, engine: LLMEngine, tokenizer=None):
+    ``channel`` (TP > 1, rank 0): before every engine step the requests admitted since the previous step are
+    broadcast to the follower ranks (serving/tp.py), which run the same :func:`engine_step`.
+    ``live``: engine liveness for ``/health`` (a step that never returns turns the replica unhealthy)."""
+
+    def __init__(self, engine: LLMEngine, tokenizer=None, channel=None):
         import queue
         import threading
+        from ..utils.liveness import Liveness, register
         self.engine = engine
         self.tokenizer = tokenizer
+        self.channel = channel
+        self.live = register(Liveness())
         self._q: "queue.Queue" = queue.Queue()
         self._futs = {}
         self._t = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
@@ -767,40 +840,42 @@ class LLMService:
 
     def _loop(self):
         import queue
+        from ..serving.tp import STEP
         while True:
+            items = []
             try:
                 block = not self.engine.has_work()
                 while True:
-                    item = self._q.get(block=block, timeout=None if block else 0)
+                    items.append(self._q.get(block=block, timeout=None if block else 0))
                     block = False
-                    ids, params, fut, image = item
-                    try:
-                        s = self.engine.add_request(ids, params, image=image)
-                    except Exception as e:  # bad request (e.g. image for a text-only model)
-                        fut.set_exception(e)
-                        continue
-                    self._futs[s.seq_id] = (s, fut)
             except queue.Empty:
                 pass
-            try:
-                with torch.inference_mode():
-                    done = self.engine.step()
-            except BaseException as e:  # fail every in-flight request
+            adds = [(ids, params, image) for ids, params, _, image in items]
+            if self.channel is not None:
+                self.channel.send(STEP, adds)
+            added, done, err = engine_step(self.engine, adds)
+            for (_, _, fut, _), s in zip(items, added):
+                if isinstance(s, Exception):
+                    fut.set_exception(s)
+                else:
+                    self._futs[s.seq_id] = (s, fut)
+            if err is not None:  # fail every in-flight request
                 for sid, (s, fut) in list(self._futs.items()):
                     if not fut.done():
-                        fut.set_exception(e)
+                        fut.set_exception(err)
                 self._futs.clear()
-                self.engine.waiting.clear()
-                self.engine.running.clear()
-                continue
             for s in done:
                 ent = self._futs.pop(s.seq_id, None)
                 if ent is not None:
                     ent[1].set_result(s)
+            self.live.progress(still_pending=self.engine.has_work() or not self._q.empty())
 
     def submit_ids(self, ids, params: SamplingParams, image=None):
         from concurrent.futures import Future
         f = Future()
+        if image is not None and self.channel is not None:
+            image = np.asarray(image.convert("RGB") if hasattr(image, "convert") else image, dtype=np.uint8)
+        self.live.work_pending()
         self._q.put((list(ids), params, f, image))
         return f
 

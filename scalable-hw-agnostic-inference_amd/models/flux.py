@@ -197,6 +197,9 @@ class _SingleProjOut(_ShardLoadMixin, nn.Module):
         m = full[:, self.d + self.rank * self.m_loc:self.d + (self.rank + 1) * self.m_loc]
         return torch.cat([a, m], 1).contiguous()
 
+    def full_shape(self, name):
+        return (self.d, self.d + self.mlp) if name == "weight" else (self.d,)
+
 
 class FluxAttention(nn.Module):
     """Holds the fused projections and q/k RMSNorm weights of one block."""

@@ -182,6 +182,21 @@ def init_random_(module: nn.Module, seed: int = 0, std_scale: float = 1.0) -> nn
             continue
         g = torch.Generator(device=own[0].device)
         g.manual_seed(seed * 1000003 + i)
+        if hasattr(m, "full_shape") and hasattr(m, "_shard"):
+            # tensor-parallel layer: draw the FULL (unsharded) tensor from the shared seed and keep this rank's
+            # shard, so a TP=n replica holds exactly the TP=1 model's weights (random-init serving at any TP)
+            for pname, p in m._parameters.items():
+                if p is None:
+                    continue
+                full = m.full_shape(pname)
+                if pname == "weight" and len(full) == 2 and not hasattr(m, "vocab"):
+                    std = std_scale / math.sqrt(full[1])
+                else:
+                    std = 0.02
+                t = torch.randn(full, generator=g, device=p.device) * std
+                p.copy_(m._shard(pname, t) if tuple(full) != tuple(p.shape) else t)
+                covered.add(id(p))
+            continue
         if isinstance(m, (Linear, GLULinear, Conv2d, Embedding, GroupNorm, LayerNorm, RMSNorm)):
             covered.update(id(p) for p in own)
         else:

@@ -74,6 +74,9 @@ class ColumnParallelLinear(_ShardLoadMixin, nn.Module):
     def _shard(self, name, full):
         return full.narrow(0, self.tp_rank * self.out_local, self.out_local).contiguous()
 
+    def full_shape(self, name):
+        return (self.out_features, self.in_features) if name == "weight" else (self.out_features,)
+
     def forward(self, x, act=None, rms_eps=None):
         y = ops.linear(x, self.weight, self.bias, act=act, rms_eps=rms_eps, w_scale=self.w_scale)
         return comm.all_gather_last(y) if self.gather_output else y
@@ -95,6 +98,9 @@ class RowParallelLinear(_ShardLoadMixin, nn.Module):
         if name == "bias":
             return full
         return full.narrow(1, self.tp_rank * self.in_local, self.in_local).contiguous()
+
+    def full_shape(self, name):
+        return (self.out_features, self.in_features) if name == "weight" else (self.out_features,)
 
     def forward(self, x, residual=None):
         if not self.input_is_parallel and self.tp_size > 1:
@@ -148,6 +154,10 @@ class QKVParallelLinear(_ShardLoadMixin, nn.Module):
         vs = v.narrow(0, kv_idx * self.kv_local * hd, self.kv_local * hd)
         return torch.cat([qs, ks, vs], 0).contiguous()
 
+    def full_shape(self, name):
+        n = (self.heads + 2 * self.kv_heads) * self.head_dim
+        return (n, self.weight.shape[1]) if name == "weight" else (n,)
+
     def forward(self, x, rms_eps=None):
         return ops.linear(x, self.weight, self.bias, rms_eps=rms_eps, w_scale=self.w_scale)
 
@@ -168,6 +178,10 @@ class GLUParallelLinear(_ShardLoadMixin, nn.Module):
     def _shard(self, name, full):
         return full.narrow(0, self.tp_rank * 2 * self.i_local, 2 * self.i_local).contiguous()
 
+    def full_shape(self, name):
+        n = 2 * self.i_local * self.tp_size
+        return (n, self.weight.shape[1]) if name == "weight" else (n,)
+
     def forward(self, x, rms_eps=None):
         return ops.linear(x, self.weight, self.bias, act=self.act, glu=True, rms_eps=rms_eps, w_scale=self.w_scale)
 
@@ -183,10 +197,13 @@ class VocabParallelEmbedding(_ShardLoadMixin, nn.Module):
         self.weight = nn.Parameter(torch.empty(self.v_local, dim, dtype=dtype), requires_grad=False)
 
     def _shard(self, name, full):
-        out = torch.zeros(self.v_local, full.shape[1], dtype=full.dtype)
+        out = torch.zeros(self.v_local, full.shape[1], dtype=full.dtype, device=full.device)
         n = max(0, min(self.v_local, self.vocab - self.start))
         out[:n] = full[self.start:self.start + n]
         return out
+
+    def full_shape(self, name):
+        return (self.vocab, self.weight.shape[1])
 
     def forward(self, ids):
         if self.tp_size == 1:
@@ -207,6 +224,7 @@ class ParallelLMHead(VocabParallelEmbedding):
 
 
 FP8_LAYER_TYPES = (ColumnParallelLinear, RowParallelLinear, QKVParallelLinear, GLUParallelLinear)
+
 
 
 @torch.no_grad()

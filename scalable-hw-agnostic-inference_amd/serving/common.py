@@ -30,6 +30,8 @@ from concurrent.futures import Future
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
+from ..utils import liveness as _liveness
+
 VALID_DEVICES = {"xla", "cuda", "triton", "cpu", "rocm", "hip", "gpu", ""}
 
 
@@ -209,16 +211,19 @@ class EngineWorker:
         self.q: "queue.Queue[_Job]" = queue.Queue()
         self.batch_fn, self.max_batch, self.max_wait = batch_fn, max_batch, max_wait_ms / 1000.0
         self.busy = 0
+        self.live = _liveness.register(_liveness.Liveness())
         self.t = threading.Thread(target=self._loop, name=name, daemon=True)
         self.t.start()
 
     def submit(self, fn: Callable, *args) -> Future:
         f: Future = Future()
+        self.live.work_pending()
         self.q.put(_Job(fn, args, f))
         return f
 
     def submit_batched(self, key, *args) -> Future:
         f: Future = Future()
+        self.live.work_pending()
         self.q.put(_Job(None, args, f, key))
         return f
 
@@ -264,6 +269,7 @@ class EngineWorker:
                     job.fut.set_exception(e)
             finally:
                 self.busy = 0
+                self.live.progress(still_pending=bool(pending) or not self.q.empty())
 
 
 # ----------------------------------------------------------------------------- app factory
@@ -299,6 +305,13 @@ def base_app(env: ServerEnv, title: str, spaced: bool, cors: bool = False):
 
     @app.get("/health")
     def healthy():
+        # liveness, not just "the HTTP server answers": 503 once an engine has had work pending without
+        # progress for longer than its hang timeout (utils/liveness.py), so the router drains this replica
+        # and the supervisor's watchdog restarts it
+        live = _liveness.worst()
+        if live is not None and not live.healthy:
+            from fastapi import HTTPException
+            raise HTTPException(status_code=503, detail=f"engine stalled: {live.snapshot()}")
         return {"message": f"{env.pod_name}{sep}is healthy"}
 
     @app.get("/readiness")

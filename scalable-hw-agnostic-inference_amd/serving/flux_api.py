@@ -16,14 +16,20 @@ flux_model_api.py:322-328; here 1 run by default, FLUX_WARMUP_RUNS overrides).
 
 Concurrent requests with the same step count are batched into one transformer
 pass per step (EngineWorker dynamic batching).
+
+Tensor parallelism (the reference's transformer TP8, flux_model_api.py:128-140, and T5
+TP8, :312-314): ``TENSOR_PARALLEL_SIZE=N`` runs the worker as N ranks (one GPU each,
+torch.distributed.run); every rank holds its shard of the MMDiT / T5 and rank 0 broadcasts
+each batched ``generate`` call (prompts, steps, seed) to the others (serving/tp.py).
 """
 import os
+import secrets
 import time
 from typing import Optional
 
 from pydantic import BaseModel
 
-from .common import METRICS, EngineWorker, ServerEnv, base_app, benchmark, mount_ui, png_b64, run
+from .common import METRICS, EngineWorker, ServerEnv, base_app, benchmark, mount_ui, png_b64
 
 WARMUP_PROMPT = "A cat holding a sign that says hello world"
 
@@ -52,7 +58,9 @@ def build_engine(env: ServerEnv):
 
 def _worker(engine, env: ServerEnv, max_batch: int):
     def batch_fn(steps, arg_lists):
-        imgs = engine.generate([a[0] for a in arg_lists], steps)
+        # explicit seed: at TP > 1 every rank must draw the same initial noise (SHAI_SEED pins it)
+        seed = int(os.environ["SHAI_SEED"]) if os.environ.get("SHAI_SEED") else secrets.randbits(31)
+        imgs = engine.generate([a[0] for a in arg_lists], steps, seed=seed)
         return [imgs[i] for i in range(len(arg_lists))]
 
     w = EngineWorker("flux-engine", batch_fn=batch_fn, max_batch=max_batch, max_wait_ms=10.0)
@@ -60,14 +68,24 @@ def _worker(engine, env: ServerEnv, max_batch: int):
     test_name = (f"flux1-dev-{runs}runs with dim {env.height}x{env.width} on {env.nodepool};"
                  f"num_inference_steps:{min(env.num_inference_steps, 10)}")
     w.call(lambda: print(benchmark(runs, test_name, lambda: engine.generate([WARMUP_PROMPT],
-                                                                           min(env.num_inference_steps, 10)),
+                                                                           min(env.num_inference_steps, 10),
+                                                                           seed=0),
                                    env.pod_name, warmup=True)))
     return w
 
 
-def create_app(engine=None, env: Optional[ServerEnv] = None, max_batch: int = 4):
-    env = env or ServerEnv.from_env(app="flux", model_id="black-forest-labs/FLUX.1-dev", num_inference_steps=28)
+def _env():
+    return ServerEnv.from_env(app="flux", model_id="black-forest-labs/FLUX.1-dev", num_inference_steps=28)
+
+
+def _engine(engine, env, tpc):
     engine = engine or build_engine(env)
+    return tpc.wrap(engine, ("generate",)) if tpc is not None else engine
+
+
+def create_app(engine=None, env: Optional[ServerEnv] = None, max_batch: int = 4, tpc=None):
+    env = env or _env()
+    engine = _engine(engine, env, tpc)
     worker = _worker(engine, env, max_batch)
     app = base_app(env, f"{env.model_id} Flux API", spaced=True)
     app.state.engine, app.state.worker = engine, worker
@@ -90,10 +108,10 @@ def create_app(engine=None, env: Optional[ServerEnv] = None, max_batch: int = 4)
     return app
 
 
-def create_gradio_app(engine=None, env: Optional[ServerEnv] = None, max_batch: int = 4):
+def create_gradio_app(engine=None, env: Optional[ServerEnv] = None, max_batch: int = 4, tpc=None):
     """run-flux.py equivalent: UI at /serve driving text2img(prompt, steps) -> (image, execution time)."""
-    env = env or ServerEnv.from_env(app="flux", model_id="black-forest-labs/FLUX.1-dev", num_inference_steps=28)
-    engine = engine or build_engine(env)
+    env = env or _env()
+    engine = _engine(engine, env, tpc)
     worker = _worker(engine, env, max_batch)
     app = base_app(env, f"{env.model_id} in MI355X {env.device} instance; pod name {env.pod_name}", spaced=False)
     app.state.engine, app.state.worker = engine, worker
@@ -113,7 +131,11 @@ def create_gradio_app(engine=None, env: Optional[ServerEnv] = None, max_batch: i
 
 
 def main():
-    run(create_gradio_app() if os.environ.get("FLUX_UI", "") == "gradio" else create_app())
+    from . import tp as tp_serving
+    env = _env()
+    make = create_gradio_app if os.environ.get("FLUX_UI", "") == "gradio" else create_app
+    tp_serving.serve("shai_amd.serving.flux_api", tp_serving.env_tp_degree(), lambda: build_engine(env),
+                     lambda tpc: make(env=env, tpc=tpc))
 
 
 if __name__ == "__main__":

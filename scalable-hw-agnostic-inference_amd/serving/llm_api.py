@@ -8,11 +8,19 @@
   GET  /health, /readiness ("<pod> is healthy"/"... is ready"), /metrics
 
 Sampling defaults follow the reference (temperature 0.7, top-k 50, top-p 0.9,
-app/vllm_model_api.py:24).  Unlike vllm_model_api.py:38-43, ``max_new_tokens``
-is honoured (the _m variant's behaviour).  Engine kwargs can come from a
-/vllm_config.yaml-style file (``VLLM_CONFIG``): tensor_parallel_size,
-max_num_seqs, max_model_len, block_size (rounded to 64-token KV blocks),
-quantization (``fp8``: e4m3 weights + per-row scales, bf16 activations).
+app/vllm_model_api.py:24; ``SHAI_TEMPERATURE`` overrides the temperature, 0 =
+greedy).  Unlike vllm_model_api.py:38-43, ``max_new_tokens`` is honoured (the _m
+variant's behaviour).  Engine kwargs come from a /vllm_config.yaml-style file
+(``VLLM_CONFIG``): tensor_parallel_size, max_num_seqs, max_model_len, block_size
+(rounded to 64-token KV blocks), quantization (``fp8``: e4m3 weights + per-row
+scales, bf16 activations).
+
+Tensor parallelism (``tensor_parallel_size: N``, app/vllm_model_api.py:127-129 with
+cova/mllama-32-11b-vllm-trn1-config.yaml:9): the worker runs as N processes, one
+per GPU (the supervisor launches ``torch.distributed.run --nproc-per-node N``; a
+bare ``python -m ...llm_api`` relaunches itself that way).  Rank 0 serves HTTP and
+broadcasts each engine step's new requests to the other ranks, which run the same
+step (serving/tp.py).
 
 ``image``: with a Llama-3.2-Vision model (``MODEL_ID`` containing "vision", or a
 local checkpoint with a ``vision_config``) the image goes through the native
@@ -27,7 +35,7 @@ import time
 import traceback
 from typing import Optional
 
-from .common import METRICS, LatencyCollector, ServerEnv, b64text, base_app, latency_report, mount_ui, run
+from .common import METRICS, LatencyCollector, ServerEnv, b64text, base_app, latency_report, mount_ui
 
 
 def load_vllm_config(path: Optional[str]) -> dict:
@@ -38,10 +46,19 @@ def load_vllm_config(path: Optional[str]) -> dict:
         return yaml.safe_load(f) or {}
 
 
-def build_service(env: ServerEnv):
-    from ..engines.llm import LLMEngine, LLMService, llama_config_for
-    from ..tokenizers import load_tokenizer
-    vc = load_vllm_config(os.environ.get("VLLM_CONFIG", "/vllm_config.yaml"))
+def _vllm_config() -> dict:
+    return load_vllm_config(os.environ.get("VLLM_CONFIG", "/vllm_config.yaml"))
+
+
+def tp_degree(vc: dict) -> int:
+    from .tp import env_tp_degree
+    return int(vc.get("tensor_parallel_size") or env_tp_degree())
+
+
+def build_engine(env: ServerEnv, vc: Optional[dict] = None):
+    """The (TP-sharded, when the process group is up) engine; identical on every rank."""
+    from ..engines.llm import LLMEngine, llama_config_for
+    vc = _vllm_config() if vc is None else vc
     cfg = llama_config_for(env.model_id, env.model_path, env.config)
     text = getattr(cfg, "text", cfg)   # MllamaConfig (vision) or LlamaConfig
     eng = LLMEngine(cfg, device=env.torch_device, model_path=env.model_path,
@@ -50,13 +67,27 @@ def build_service(env: ServerEnv):
                     enable_prefix_caching=True, quantization=vc.get("quantization"))
     import torch
     with torch.inference_mode():
-        eng.warmup_graphs()   # every decode batch bucket captured before the first request
+        # every decode batch bucket (sampled and all-greedy) captured before the first request
+        eng.warmup_graphs(greedy_too=True)
+    return eng
+
+
+def build_service(env: ServerEnv, tpc=None):
+    from ..engines.llm import LLMService
+    from ..tokenizers import load_tokenizer
+    eng = build_engine(env)
+    cfg = eng.mcfg if eng.mcfg is not None else eng.cfg
+    text = eng.cfg
     specials = {"<|begin_of_text|>": text.bos_token_id}
     if text is not cfg:
         specials["<|image|>"] = cfg.image_token_index
     tok = load_tokenizer(env.model_path, vocab_size=text.vocab_size, bos_id=text.bos_token_id,
                          eos_id=text.eos_token_id, pad_id=0, model_max_length=eng.max_model_len, specials=specials)
-    return LLMService(eng, tok)
+    channel = None
+    if tpc is not None and tpc.enabled:
+        tpc.start_heartbeat()
+        channel = tpc.channel
+    return LLMService(eng, tok, channel=channel)
 
 
 def _decode_image(b64: str):
@@ -73,13 +104,14 @@ def add_instruct(prompt: str, has_image: bool) -> str:
             f"<|start_header_id|>assistant<|end_header_id|>\n\n")
 
 
-def create_app(service=None, env: Optional[ServerEnv] = None):
+def create_app(service=None, env: Optional[ServerEnv] = None, tpc=None):
     from fastapi import HTTPException
     from pydantic import BaseModel, Field
 
     from ..engines.llm import SamplingParams
     env = env or ServerEnv.from_env(app="llm")
-    service = service or build_service(env)
+    service = service or build_service(env, tpc)
+    temperature = float(os.environ.get("SHAI_TEMPERATURE", "0.7"))
 
     class GenerateRequest(BaseModel):
         max_new_tokens: int = 128
@@ -99,7 +131,7 @@ def create_app(service=None, env: Optional[ServerEnv] = None):
         report: str = Field(..., description="Benchmark report")
 
     def params(n):
-        return SamplingParams(temperature=0.7, top_k=50, top_p=0.9, max_tokens=max(1, int(n)))
+        return SamplingParams(temperature=temperature, top_k=50, top_p=0.9, max_tokens=max(1, int(n)))
 
     multimodal = bool(getattr(service, "multimodal", False))
 
@@ -153,7 +185,14 @@ def create_app(service=None, env: Optional[ServerEnv] = None):
 
 
 def main():
-    run(create_app())
+    from . import tp as tp_serving
+    from ..engines.llm import engine_step
+    vc = _vllm_config()
+    env = ServerEnv.from_env(app="llm")
+    # follower ranks mirror rank 0's engine steps (each STEP message = the requests admitted since the last)
+    tp_serving.serve("shai_amd.serving.llm_api", tp_degree(vc), lambda: build_engine(env, vc),
+                     lambda tpc: create_app(env=env, tpc=tpc),
+                     step_fn=lambda eng: (lambda adds: engine_step(eng, adds)))
 
 
 if __name__ == "__main__":

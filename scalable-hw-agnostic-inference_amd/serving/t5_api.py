@@ -5,7 +5,9 @@
   POST /benchmark {"n_runs", "max_new_tokens", "prompt"} -> {"report": base64(...)}
        (the reference passes 5 args to a 4-arg benchmark(), t5_model_api.py:64,139;
         the intended behaviour is implemented)
-TP-sharded artifacts (tp_*.pt) are replaced by shard-on-load of the HF checkpoint.
+TP-sharded artifacts (tp_*.pt) are replaced by shard-on-load of the HF checkpoint:
+``TENSOR_PARALLEL_SIZE=N`` runs the worker as N ranks (one GPU each); rank 0 broadcasts
+each batched ``embed`` call to the others (serving/tp.py).
 """
 
 import time
@@ -14,7 +16,7 @@ from typing import Optional
 
 import numpy as np
 
-from .common import METRICS, EngineWorker, LatencyCollector, ServerEnv, b64text, base_app, latency_report, run
+from .common import METRICS, EngineWorker, LatencyCollector, ServerEnv, b64text, base_app, latency_report
 
 
 def build_engine(env: ServerEnv):
@@ -25,11 +27,17 @@ def build_engine(env: ServerEnv):
     return TextEmbeddingEngine(cfg, device=env.torch_device, model_path=env.model_path)
 
 
-def create_app(engine=None, env: Optional[ServerEnv] = None):
+def _env():
+    return ServerEnv.from_env(app="t5", model_id="google/t5-v1_1-large", max_seq_len=1024)
+
+
+def create_app(engine=None, env: Optional[ServerEnv] = None, tpc=None):
     from fastapi import HTTPException
     from pydantic import BaseModel, Field
-    env = env or ServerEnv.from_env(app="t5", model_id="google/t5-v1_1-large", max_seq_len=1024)
+    env = env or _env()
     engine = engine or build_engine(env)
+    if tpc is not None:
+        engine = tpc.wrap(engine, ("embed",))
     worker = EngineWorker("t5", batch_fn=lambda L, args: list(engine.embed([a[0] for a in args], L)), max_batch=32,
                           max_wait_ms=2.0)
 
@@ -89,7 +97,10 @@ def create_app(engine=None, env: Optional[ServerEnv] = None):
 
 
 def main():
-    run(create_app())
+    from . import tp as tp_serving
+    env = _env()
+    tp_serving.serve("shai_amd.serving.t5_api", tp_serving.env_tp_degree(), lambda: build_engine(env),
+                     lambda tpc: create_app(env=env, tpc=tpc))
 
 
 if __name__ == "__main__":

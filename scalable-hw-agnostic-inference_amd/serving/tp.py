@@ -1,0 +1,233 @@
+"""Tensor-parallel serving: one process per GPU of a TP group behind ONE HTTP front end.
+
+The reference serves its large models sharded inside a single process that drives many
+NeuronCores: vLLM ``LLM(**vllm_config)`` with ``tensor_parallel_size: 32``
+(app/vllm_model_api.py:33-34,127-129; cova/mllama-32-11b-vllm-trn1-config.yaml:9), the Flux
+transformer as TP8 NEFFs (app/flux_model_api.py:128-140) and T5 from ``tp_*.pt`` shards
+(app/flux_model_api.py:312-314, app/t5_model_api.py:27,33).  On MI355X a TP group is N processes
+(``torch.distributed.run --nproc-per-node N``, launched by the supervisor for ``WorkerSpec.tp = N``),
+one per GPU, with the model's collectives on RCCL over xGMI (or the P2P all-reduce kernel).
+
+SPMD protocol:
+
+* every rank builds the same sharded engine (``set_device(LOCAL_RANK)`` + ``init_distributed``);
+* rank 0 (the *leader*) binds the HTTP port and owns the request queue;
+* before each engine call the leader broadcasts a small control message -- the method name and its
+  arguments (diffusion / encoder engines: :class:`SPMDProxy`), or an LLM step with the requests
+  admitted since the last step (:meth:`LLMService` with a channel) -- and the *followers*
+  (:func:`follow`) execute exactly the same call, so every collective inside it lines up.
+
+Control messages travel on a separate **gloo** group (host sockets), never on the RCCL
+communicator: an idle follower blocks in a CPU receive, not in a GPU collective, and the leader sends
+a heartbeat every ``HEARTBEAT_S`` seconds so the gloo timeout only fires when the leader is gone.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import pickle
+import threading
+from dataclasses import dataclass
+from typing import Any, Iterable, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..utils.logging import get_logger
+
+_log = get_logger("tp-serving")
+
+CALL, STEP, NOOP, STOP = 1, 2, 3, 4
+HEARTBEAT_S = float(os.environ.get("SHAI_TP_HEARTBEAT_S", "20"))
+
+
+class TPChannel:
+    """Leader -> followers control messages: an int64 header [kind, nbytes] + an optional pickled payload,
+    both broadcast from rank 0 over a dedicated gloo group.  Thread-safe on the sending side."""
+
+    def __init__(self, timeout_s: float = 3600.0):
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+        self.group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s))
+        self._lock = threading.Lock()
+        self.sent = 0
+
+    @property
+    def is_leader(self) -> bool:
+        return self.rank == 0
+
+    def send(self, kind: int, payload: Any = None) -> None:
+        assert self.is_leader, "only rank 0 sends control messages"
+        data = pickle.dumps(payload, protocol=pickle.HIGHEST_PROTOCOL) if payload is not None else b""
+        with self._lock:
+            dist.broadcast(torch.tensor([kind, len(data)], dtype=torch.int64), 0, group=self.group)
+            if data:
+                dist.broadcast(torch.frombuffer(bytearray(data), dtype=torch.uint8), 0, group=self.group)
+            self.sent += 1
+
+    def recv(self):
+        hdr = torch.zeros(2, dtype=torch.int64)
+        dist.broadcast(hdr, 0, group=self.group)
+        kind, n = (int(v) for v in hdr.tolist())
+        payload = None
+        if n:
+            buf = torch.empty(n, dtype=torch.uint8)
+            dist.broadcast(buf, 0, group=self.group)
+            payload = pickle.loads(buf.numpy().tobytes())   # sent by our own rank 0
+        return kind, payload
+
+
+class SPMDProxy:
+    """Wraps an engine on the leader: calling one of ``methods`` first broadcasts (name, args, kwargs) so
+    every follower runs the same call, then runs it locally.  Other attributes pass through untouched."""
+
+    def __init__(self, target, channel: TPChannel, methods: Iterable[str]):
+        self._target, self._channel, self._methods = target, channel, set(methods)
+
+    def __getattr__(self, name):
+        attr = getattr(self._target, name)
+        if name not in self._methods:
+            return attr
+
+        def call(*args, **kwargs):
+            self._channel.send(CALL, (name, args, kwargs))
+            return attr(*args, **kwargs)
+        return call
+
+
+def follow(target, channel: TPChannel, step_fn=None) -> int:
+    """Follower main loop: execute the leader's calls until STOP.  ``step_fn(payload)`` handles STEP
+    messages (the LLM engine loop).  A call that raises is logged and skipped -- the leader hits the same
+    exception (same inputs, same code) and reports it to its client.  Returns the number of calls run."""
+    n = 0
+    while True:
+        kind, payload = channel.recv()
+        if kind == STOP:
+            return n
+        if kind == NOOP:
+            continue
+        try:
+            with torch.inference_mode():
+                if kind == CALL:
+                    name, args, kwargs = payload
+                    getattr(target, name)(*args, **kwargs)
+                elif kind == STEP and step_fn is not None:
+                    step_fn(payload)
+        except Exception as e:  # noqa: BLE001 -- mirrored on the leader
+            _log.warning("follower call failed", extra={"event": "follower_error", "detail": repr(e)[:300]})
+        n += 1
+
+
+def heartbeat(channel: TPChannel, stop: threading.Event) -> threading.Thread:
+    """Leader thread: a NOOP every HEARTBEAT_S seconds so an idle follower never hits the gloo timeout
+    (sends are serialised by the channel lock, so a NOOP only ever lands between two messages)."""
+    def loop():
+        while not stop.wait(HEARTBEAT_S):
+            try:
+                channel.send(NOOP)
+            except Exception:  # group torn down at shutdown
+                return
+    t = threading.Thread(target=loop, daemon=True, name="tp-heartbeat")
+    t.start()
+    return t
+
+
+@dataclass
+class TPContext:
+    rank: int = 0
+    world: int = 1
+    channel: Optional[TPChannel] = None
+    _hb: Optional[threading.Event] = None
+
+    @property
+    def enabled(self) -> bool:
+        return self.world > 1
+
+    @property
+    def is_leader(self) -> bool:
+        return self.rank == 0
+
+    def start_heartbeat(self) -> None:
+        if self.enabled and self.is_leader and self._hb is None:
+            self._hb = threading.Event()
+            heartbeat(self.channel, self._hb)
+
+    def wrap(self, engine, methods: Iterable[str]):
+        """Leader: an :class:`SPMDProxy` over ``engine`` (and the idle heartbeat); TP1: ``engine`` itself."""
+        if not self.enabled:
+            return engine
+        self.start_heartbeat()
+        return SPMDProxy(engine, self.channel, methods)
+
+
+def env_tp_degree() -> int:
+    """TP degree from the environment: ``TENSOR_PARALLEL_SIZE`` (SURVEY 2.12's vLLM compile variable), else the
+    launcher's WORLD_SIZE, else 1."""
+    return int(os.environ.get("TENSOR_PARALLEL_SIZE") or os.environ.get("WORLD_SIZE") or 1)
+
+
+def serve(module: str, tp: int, build_engine, create_app, methods=(), step_fn=None) -> None:
+    """Common ``main()`` of a TP-capable server: relaunch as ``tp`` ranks if needed, join the group, then
+    rank 0 runs ``create_app(tpc)`` under uvicorn while every other rank builds the same engine
+    (``build_engine()``) and follows rank 0's calls (``step_fn(engine)`` -> STEP handler, for the LLM)."""
+    if relaunch_under_torchrun(tp, module):
+        return
+    tpc = setup(tp)
+    if tpc.enabled and not tpc.is_leader:
+        eng = build_engine()
+        follow(eng, tpc.channel, step_fn=step_fn(eng) if step_fn is not None else None)
+        return
+    from .common import run
+    try:
+        run(create_app(tpc))
+    finally:
+        shutdown(tpc)
+
+
+def relaunch_under_torchrun(tp: int, module: str) -> bool:
+    """A TP > 1 server started as a single process (``python -m <server>``) re-runs itself as ``tp`` ranks
+    under ``torch.distributed.run`` (a child process, started before this process touches the GPU) and
+    exits with its status.  Returns False (nothing done) when already launched as a group or at TP1."""
+    if tp <= 1 or "WORLD_SIZE" in os.environ:
+        return False
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    if module == "__main__":
+        module = sys.modules["__main__"].__spec__.name
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={tp}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", "-m", module]
+    _log.info("relaunching as a TP group", extra={"event": "tp_relaunch", "detail": " ".join(cmd)})
+    sys.exit(subprocess.call(cmd))
+
+
+def setup(tensor_parallel_size: Optional[int] = None) -> TPContext:
+    """Join the TP group this process was launched into (``torch.distributed.run`` env vars).  The TP degree
+    is ``tensor_parallel_size`` (e.g. from /vllm_config.yaml) and must equal WORLD_SIZE -- one replica per
+    launch; data parallelism is the supervisor's job (more replicas), not the launcher's."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    tp = int(tensor_parallel_size or world)
+    if tp != world:
+        raise ValueError(f"tensor_parallel_size={tp} but the worker was launched with WORLD_SIZE={world}: "
+                         f"launch it with --nproc-per-node={tp} (supervisor WorkerSpec.tp)")
+    if world == 1:
+        return TPContext()
+    from ..parallel.state import init_distributed
+    backend = "gloo" if os.environ.get("DEVICE", "").lower() == "cpu" else None
+    init_distributed(backend=backend, tp_size=tp)
+    ctx = TPContext(dist.get_rank(), world, TPChannel())
+    _log.info("tp worker up", extra={"event": "tp_up", "detail": f"rank {ctx.rank}/{world}"})
+    return ctx
+
+
+def shutdown(ctx: TPContext) -> None:
+    if ctx.enabled and ctx.is_leader and ctx.channel is not None:
+        if ctx._hb is not None:
+            ctx._hb.set()
+        try:
+            ctx.channel.send(STOP)
+        except Exception:
+            pass

@@ -147,6 +147,8 @@ class Supervisor:
             env["HOST"] = "127.0.0.1"
             env.setdefault("POD_NAME", spec.name)
             env.setdefault("SHAI_LOG_FORMAT", "json")   # one JSON object per line in <log_dir>/<name>.log
+            if spec.tp > 1:   # every rank of the group agrees on the TP degree (serving/tp.py)
+                env["TENSOR_PARALLEL_SIZE"] = str(spec.tp)
             env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
             if spec.gpus:
                 env["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in spec.gpus)

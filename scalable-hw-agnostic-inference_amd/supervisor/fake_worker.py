@@ -1,23 +1,37 @@
 """Model-free worker speaking the SD/LLM API (for router / supervisor /
 autoscaler tests and load-generator dry runs): configurable latency
-(FAKE_LATENCY_S) and failure injection (FAKE_FAIL_RATE)."""
+(FAKE_LATENCY_S), failure injection (FAKE_FAIL_RATE) and a hung engine
+(FAKE_HANG_AFTER=n: the engine thread blocks forever on request n + 1, the way a
+hung kernel blocks a real engine; ``/health`` then turns 503 after
+SHAI_HANG_TIMEOUT_S)."""
 import os
 import random
 import time
 
-from ..serving.common import METRICS, ServerEnv, base_app, benchmark, run
+import threading
+
+from ..serving.common import METRICS, EngineWorker, ServerEnv, base_app, benchmark, run
 
 
 def create_app():
     env = ServerEnv.from_env(app=os.environ.get("APP", "fake"))
     lat = float(os.environ.get("FAKE_LATENCY_S", "0.01"))
     fail = float(os.environ.get("FAKE_FAIL_RATE", "0"))
+    hang_after = int(os.environ.get("FAKE_HANG_AFTER", "-1"))
     app = base_app(env, "fake worker", spaced=False)
+    engine = EngineWorker("fake-engine")
+    served = [0]
 
-    def work():
+    def _engine_work():
+        served[0] += 1
+        if 0 <= hang_after < served[0]:
+            threading.Event().wait()   # never returns: a stuck kernel
         time.sleep(lat)
         if random.random() < fail:
             raise RuntimeError("injected failure")
+
+    def work():
+        return engine.call(_engine_work)
 
     @app.post("/genimage")
     def genimage(request: dict):

@@ -1,0 +1,69 @@
+"""Engine liveness: "is the engine making progress on the work it has?"
+
+The reference's replicas are judged by the ALB health check (``/health`` every 10 s, unhealthy after
+10 failures, sd21-weighted-routing-ing.yaml:9-14) and the K8s probes, which only prove that the HTTP
+server answers -- a replica stuck in a hung kernel stays "healthy".  Here every engine loop reports
+progress (a finished job / engine step) and whether work is pending; ``/health`` turns 503 once work has
+been pending for longer than ``SHAI_HANG_TIMEOUT_S`` without progress, so the router drains the replica and
+the supervisor's watchdog (``supervisor.health.GPUHealthMonitor.check_workers``) kills and restarts it.
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+
+DEFAULT_HANG_TIMEOUT_S = float(os.environ.get("SHAI_HANG_TIMEOUT_S", "180"))
+
+
+class Liveness:
+    def __init__(self, hang_timeout_s: float = DEFAULT_HANG_TIMEOUT_S, clock=time.monotonic):
+        self.hang_timeout_s = hang_timeout_s
+        self.clock = clock
+        self._lock = threading.Lock()
+        self.last_progress = clock()
+        self.pending_since = None
+        self.progress_count = 0
+
+    def work_pending(self) -> None:
+        """Work was queued (or is in flight)."""
+        with self._lock:
+            if self.pending_since is None:
+                self.pending_since = self.clock()
+
+    def progress(self, still_pending: bool) -> None:
+        """One unit of work completed (a job, an engine step)."""
+        with self._lock:
+            now = self.clock()
+            self.last_progress = now
+            self.progress_count += 1
+            self.pending_since = now if still_pending else None
+
+    def stalled_for(self) -> float:
+        """Seconds that pending work has waited without any progress (0 when idle)."""
+        with self._lock:
+            if self.pending_since is None:
+                return 0.0
+            return max(0.0, self.clock() - max(self.pending_since, self.last_progress))
+
+    @property
+    def healthy(self) -> bool:
+        return self.stalled_for() <= self.hang_timeout_s
+
+    def snapshot(self) -> dict:
+        return {"stalled_s": round(self.stalled_for(), 3), "hang_timeout_s": self.hang_timeout_s,
+                "progress_count": self.progress_count, "pending": self.pending_since is not None}
+
+
+_REGISTRY: list = []
+
+
+def register(live: "Liveness") -> "Liveness":
+    """Make ``live`` part of this process's ``/health`` verdict (every engine loop registers one)."""
+    _REGISTRY.append(live)
+    return live
+
+
+def worst() -> "Liveness | None":
+    """The registered engine that has been stalled longest (None when none is registered)."""
+    return max(_REGISTRY, key=lambda l: l.stalled_for() - l.hang_timeout_s, default=None)

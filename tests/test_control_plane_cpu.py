@@ -241,3 +241,69 @@ def test_gpu_health_monitor_faults_and_recovery():
     assert mon.check_workers(now=110.0) == []
     assert mon.check_workers(now=140.5) == ["w1"] and killed == ["w1"]
     assert GPUHealthMonitor(sup, probe=lambda: None).check_devices() == {}   # no library: no verdicts
+
+
+def test_liveness_unit():
+    from shai_amd.utils.liveness import Liveness
+    t = [0.0]
+    lv = Liveness(hang_timeout_s=5.0, clock=lambda: t[0])
+    assert lv.healthy and lv.stalled_for() == 0.0           # idle: never stalled
+    lv.work_pending()
+    t[0] = 4.0
+    assert lv.healthy
+    lv.progress(still_pending=True)                         # progress resets the clock
+    t[0] = 8.5
+    assert lv.healthy and abs(lv.stalled_for() - 4.5) < 1e-9
+    t[0] = 9.5
+    assert not lv.healthy                                   # pending 5.5 s without progress
+    lv.progress(still_pending=False)
+    t[0] = 100.0
+    assert lv.healthy                                       # idle again
+
+
+def test_hung_engine_is_unhealthy_and_restarted(tmp_path):
+    """A replica whose engine thread hangs (FAKE_HANG_AFTER: the 2nd request blocks forever, like a stuck
+    kernel) keeps answering HTTP, but /health turns 503 once work has been pending without progress for
+    SHAI_HANG_TIMEOUT_S; the router marks it unhealthy after the ALB threshold
+    (sd21-weighted-routing-ing.yaml:9-14) and the supervisor's watchdog kills and restarts it."""
+    import httpx
+    from shai_amd.supervisor import GPUInventory, Supervisor, WorkerSpec
+    from shai_amd.supervisor.health import GPUHealthMonitor
+    router = Router(policy="round_robin", health_interval_s=0.2, unhealthy_threshold=2, healthy_threshold=1)
+    sup = Supervisor(router, GPUInventory([0]), log_dir=str(tmp_path))
+    spec = WorkerSpec("h0", "shai_amd.supervisor.fake_worker",
+                      env={"DEVICE": "cpu", "FAKE_LATENCY_S": "0.01", "FAKE_HANG_AFTER": "1",
+                           "SHAI_HANG_TIMEOUT_S": "1.0"}, model_key="fake")
+    try:
+        assert sup.start(spec) and sup.wait_ready("h0", timeout=120)
+        url = f"http://127.0.0.1:{spec.port}"
+        assert httpx.post(url + "/genimage", json={"prompt": "x"}, timeout=10).status_code == 200
+        assert httpx.get(url + "/health", timeout=5).status_code == 200
+        with pytest.raises(httpx.ReadTimeout):     # this request hangs the engine thread
+            httpx.post(url + "/genimage", json={"prompt": "y"}, timeout=1.5)
+        time.sleep(0.5)
+        r = httpx.get(url + "/health", timeout=5)
+        assert r.status_code == 503 and "stalled" in r.text
+        import asyncio
+        b = router.get("h0")
+
+        async def probe_twice():
+            async with httpx.AsyncClient() as client:
+                for _ in range(2):
+                    await router.check_once(client)
+        asyncio.run(probe_twice())                 # the router's own /health probes, ALB-style threshold
+        assert not b.healthy
+        mon = GPUHealthMonitor(sup, probe=lambda: None, hang_timeout_s=0.5)
+        assert mon.check_workers(now=0.0) == []
+        assert mon.check_workers(now=1.0) == ["h0"]
+        deadline = time.time() + 60
+        while time.time() < deadline and "crash" not in [e[1] for e in sup.events]:
+            sup.poll()
+            time.sleep(0.2)
+        while time.time() < deadline and not (sup.procs.get("h0") and sup.procs["h0"].poll() is None):
+            sup.poll()
+            time.sleep(0.2)
+        assert sup.wait_ready("h0", timeout=120)   # restarted replica serves again
+        assert httpx.get(f"http://127.0.0.1:{spec.port}/health", timeout=5).status_code == 200
+    finally:
+        sup.shutdown()

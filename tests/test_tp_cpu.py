@@ -19,6 +19,17 @@ def test_tp2_matches_tp1(which):
     mp.spawn(tp_worker.run, args=(2, _port(), which), nprocs=2, join=True)
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [4, 8])
+@pytest.mark.parametrize("which", ["llama", "t5", "flux", "flux_sp"])
+def test_tp_degrees_4_8_match_tp1(which, world):
+    """The TP degrees the reference runs (TP8: app/src/transformer/compile.py:25,
+    app/src/text_encoder_2/compile.py:24): Llama with kv_heads < tp (replicated KV heads) checked on prefill
+    AND 10 teacher-forced decode steps, T5 with 1 head per rank at TP8, Flux with 24 heads (3 per rank at
+    TP8) with and without sequence parallelism."""
+    mp.spawn(tp_worker.run, args=(world, _port(), which), nprocs=world, join=True)
+
+
 def test_seq_major_layout_is_rank_chunks():
     """The RCCL reduce-scatter input layout: chunk r of the rank-major view is sequence rows [r*s, (r+1)*s)."""
     import torch

@@ -27,32 +27,62 @@ def run(rank, world, port, which):
     if which == "llama":
         from shai_amd.engines.llm import LLMEngine, SamplingParams
         from shai_amd.models.llama import LlamaConfig, LlamaForCausalLM
-        c = LlamaConfig.tiny()
+        # 8 query heads / 2 KV heads: at TP 4 and 8 each rank holds a REPLICATED KV head (kv_heads < tp)
+        c = LlamaConfig(vocab_size=512, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                        num_attention_heads=8, num_key_value_heads=2, head_dim=32, max_position_embeddings=1024)
         _tp1()
         full = LlamaForCausalLM(c)
         init_random_(full, 3)
         sd = {k: v.clone() for k, v in full.state_dict().items()}
-        e1 = LLMEngine(c, device="cpu", max_num_seqs=2, max_model_len=256, enable_prefix_caching=False)
-        load_into(e1.model, dict(sd), strict=True)
-        p = SamplingParams(max_tokens=1, temperature=0.0, ignore_eos=True)
+        n_dec = 10
         prompts = [[5, 9, 200, 31, 7], list(range(3, 80))]
 
-        def prefill_logits(eng):
+        def run_engine(eng, forced=None):
+            """Greedy generation recording the logits of every step (prefill, then n_dec - 1 decode steps).
+            ``forced``: teacher forcing -- each step's appended tokens are replaced by the TP1 run's, so both
+            runs see the same sequences even if an argmax flips under bf16 rounding."""
             rec = []
-            orig = eng._sample_and_append
-            eng._sample_and_append = lambda seqs, logits: (rec.append(logits.float().clone()), orig(seqs, logits))
-            eng.generate(prompts, p)
-            return rec[0]
-        ref = prefill_logits(e1)
+            fwd = eng.model.forward
+            eng.model.forward = lambda *a, **k: (lambda y: (rec.append(y.float().clone()), y)[1])(fwd(*a, **k))
+            p = SamplingParams(max_tokens=n_dec, temperature=0.0, ignore_eos=True)
+            seqs = [eng.add_request(pr, p) for pr in prompts]
+            row = {id(s): i for i, s in enumerate(seqs)}
+            if forced is not None:
+                app = eng._append
+                eng._append = lambda ss, toks: app(ss, [forced[row[id(q)]][len(q.output)] for q in ss])
+            while not all(q.finished for q in seqs):
+                eng.step()
+            return rec, [q.output for q in seqs]
+        e1 = LLMEngine(c, device="cpu", max_num_seqs=2, max_model_len=256, enable_prefix_caching=False,
+                       async_decode=False)
+        load_into(e1.model, dict(sd), strict=True)
+        ref_logits, ref_toks = run_engine(e1)
+        assert len(ref_logits) == n_dec and all(len(t) == n_dec for t in ref_toks)
         init_distributed("gloo", tp_size=world)
-        e2 = LLMEngine(c, device="cpu", max_num_seqs=2, max_model_len=256, enable_prefix_caching=False)
+        e2 = LLMEngine(c, device="cpu", max_num_seqs=2, max_model_len=256, enable_prefix_caching=False,
+                       async_decode=False)
+        assert e2.model.kv_heads_local == 1
         load_into(e2.model, dict(sd), strict=True)
-        got = prefill_logits(e2)
-        assert got.shape == ref.shape
-        _close(got, ref, 3e-2)   # bf16 partial sums are rounded before the all-reduce at TP>1
+        got_logits, got_toks = run_engine(e2, forced=ref_toks)
+        assert got_toks == ref_toks
+        assert len(got_logits) == len(ref_logits)
+        for g, r in zip(got_logits, ref_logits):   # prefill logits, then every decode step's
+            assert g.shape == r.shape
+            _close(g, r, 3e-2)   # bf16 partial sums are rounded before the all-reduce at TP>1
+        # random init is TP-consistent: a TP=world engine built from the seed alone equals the TP1 one
+        st = init_distributed("gloo", tp_size=world)
+        e3 = LLMEngine(c, device="cpu", max_num_seqs=2, max_model_len=256, enable_prefix_caching=False,
+                       async_decode=False, seed=0)
+        l3, _ = run_engine(e3)
+        _tp1()
+        e4 = LLMEngine(c, device="cpu", max_num_seqs=2, max_model_len=256, enable_prefix_caching=False,
+                       async_decode=False, seed=0)
+        l4, _ = run_engine(e4)
+        set_tp(st)
+        _close(l3[0], l4[0], 3e-2)
     elif which == "t5":
         from shai_amd.models.t5 import T5Config, T5EncoderModel
-        c = T5Config.tiny()
+        c = T5Config(vocab_size=500, d_model=128, d_kv=16, d_ff=256, num_layers=2, num_heads=8)
         _tp1()
         m1 = T5EncoderModel(c)
         init_random_(m1, 4)
@@ -64,7 +94,7 @@ def run(rank, world, port, which):
         init_distributed("gloo", tp_size=world)
         m2 = T5EncoderModel(c)
         load_into(m2, dict(sd), strict=True)
-        _close(m2(ids, mask), ref, 1e-2)
+        _close(m2(ids, mask), ref, 3e-2)   # bf16 partial sums rounded before the all-reduce
     elif which in ("flux", "flux_sp", "flux_ovl"):
         # flux_sp: sequence-parallel single blocks (S/n-row residual shards, all-gather + reduce-scatter)
         # flux_ovl: every row-parallel GEMM chunked with its all-reduce overlapped
@@ -72,7 +102,9 @@ def run(rank, world, port, which):
             from shai_amd.parallel import comm
             comm.OVERLAP_MIN_ROWS, comm.OVERLAP_CHUNKS = 1, 2
         from shai_amd.models.flux import FluxConfig, FluxTransformer2DModel
-        c = FluxConfig.tiny()
+        # 24 heads like Flux.1-dev: 3 heads per rank at TP 8 (app/src/transformer/model.py:163)
+        c = FluxConfig(hidden=384, heads=24, head_dim=16, num_layers=2, num_single_layers=2,
+                       joint_attention_dim=64, pooled_projection_dim=32, axes_dims_rope=(4, 6, 6))
         c.sequence_parallel = which == "flux_sp"
         B = 2 if c.sequence_parallel else 1
         _tp1()
