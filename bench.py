@@ -16,9 +16,15 @@ native LLM engine at TP = N (see shai_amd.engines.llm).
 
 ``--workload vit``: ViT-base/16 224x224 classification images/s at batch 32 per GPU.
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+``--tp T`` (mistral / flux): tensor-parallel degree of one replica; the N GPUs run N / T replicas
+(data parallel x tensor parallel).  Defaults: mistral T = N (one engine over all GPUs, strong scaling),
+flux T = 1 (one replica per GPU).  ``--workload flux --tp 8`` is the reference's Flux TP8 latency setup
+(cova/README.md:98).
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--tp T]
         python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
-Prints ONE JSON line on rank 0.
+``python bench.py --gpus N`` with N > 1 outside a launcher re-runs itself under torch.distributed.run with N
+ranks (a child process, started before this process touches the GPU).  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -38,27 +44,66 @@ sys.path.insert(0, ROOT)
 REF_SD21_IMG_PER_S = 130.0 / 60.0
 
 
+def _relaunch(n):
+    """``--gpus N`` without a launcher: run N ranks under torch.distributed.run (127.0.0.1 rendezvous) as a
+    child process and exit with its status.  Nothing here has touched the GPU yet."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
+# --cpu-dry-run: the multi-process plumbing (launcher, rendezvous, barriers, max over ranks, JSON line) on a
+# tiny config over gloo on the CPU -- for tests; NOT a measurement.
+DEVICE = "cuda"
+
+
+def _sync():
+    import torch
+    if DEVICE == "cuda":
+        torch.cuda.synchronize()
+
+
 def _dist_init(n):
     import torch
     import torch.distributed as dist
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n:
+        raise SystemExit(f"bench.py --gpus {n} but WORLD_SIZE={world}: launch {n} ranks (or run without a launcher)")
+    if DEVICE == "cpu":
+        if world > 1 and not dist.is_initialized():
+            dist.init_process_group("gloo")
+        return rank, world, local
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if not dist.is_initialized():
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     return rank, world, local
 
 
+def _groups(args, world):
+    """(tp, replicas, replica index of this rank): consecutive ranks form one TP group."""
+    tp = args.tp or 1
+    if world % tp:
+        raise SystemExit(f"--tp {tp} does not divide --gpus {world}")
+    rank = int(os.environ.get("RANK", "0"))
+    return tp, world // tp, rank // tp
+
+
 def _barrier(world):
-    import torch
     import torch.distributed as dist
-    torch.cuda.synchronize()
+    _sync()
     if world > 1:
         dist.barrier()
-        torch.cuda.synchronize()
+        _sync()
 
 
 def _max_over_ranks(x, world):
@@ -66,7 +111,7 @@ def _max_over_ranks(x, world):
     import torch.distributed as dist
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=DEVICE)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -75,18 +120,18 @@ def bench_sd21(args, rank, world):
     import torch
     from shai_amd.engines.diffusion import SDConfig, StableDiffusionEngine
 
-    eng = StableDiffusionEngine(SDConfig.sd21(height=args.height, width=args.width), device="cuda", seed=rank,
-                                use_graphs=not args.no_graphs)
+    cfg = SDConfig.tiny() if DEVICE == "cpu" else SDConfig.sd21(height=args.height, width=args.width)
+    eng = StableDiffusionEngine(cfg, device=DEVICE, seed=rank, use_graphs=not args.no_graphs)
     prompts = [f"a photo of an astronaut riding a horse on mars, variant {rank}-{i}" for i in range(args.batch)]
     for i in range(args.warmup):
         eng.generate(prompts, args.inference_steps, seed=1000 + i, output="tensor")
     # p50 single-image latency (reference's request latency semantics), outside the timed region
     lat = []
     for i in range(args.latency_runs):
-        torch.cuda.synchronize()
+        _sync()
         t0 = time.perf_counter()
         eng.generate(prompts[:1], args.inference_steps, seed=2000 + i)
-        torch.cuda.synchronize()
+        _sync()
         lat.append(time.perf_counter() - t0)
     _barrier(world)
     t0 = time.perf_counter()
@@ -94,7 +139,7 @@ def bench_sd21(args, rank, world):
     for i in range(args.steps):
         s0 = time.perf_counter()
         img = eng.generate(prompts, args.inference_steps, seed=3000 + i, output="tensor")
-        torch.cuda.synchronize()
+        _sync()
         per.append(time.perf_counter() - s0)
     _barrier(world)
     elapsed = _max_over_ranks(time.perf_counter() - t0, world)
@@ -133,13 +178,18 @@ REF_FLUX_512_10STEP_S = 5.61   # cova/README.md:98 (Neuron TP8 Flux service, 512
 
 
 def bench_flux(args, rank, world):
-    """Flux.1-dev txt2img (CLIP-L + T5-XXL 512 tokens + 12B MMDiT + 16-ch VAE), one replica per GPU."""
+    """Flux.1-dev txt2img (CLIP-L + T5-XXL 512 tokens + 12B MMDiT + 16-ch VAE).  ``--tp T``: each replica is
+    a TP group of T GPUs (MMDiT + T5 sharded, collectives over RCCL / the xGMI P2P kernel); default one
+    replica per GPU."""
     import torch
     from shai_amd.engines.flux import FluxEngine, FluxPipelineConfig
+    from shai_amd.parallel.state import init_distributed
+    tp, replicas, rep = _groups(args, world)
+    init_distributed(tp_size=tp)
     steps_inf = args.inference_steps if args.inference_steps != 50 else 10
-    eng = FluxEngine(FluxPipelineConfig.dev(args.height, args.width, 512), device="cuda", seed=rank,
+    eng = FluxEngine(FluxPipelineConfig.dev(args.height, args.width, 512), device="cuda", seed=0,
                      use_graphs=not args.no_graphs)
-    prompts = [f"A cat holding a sign that says hello world, variant {rank}-{i}" for i in range(args.batch)]
+    prompts = [f"A cat holding a sign that says hello world, variant {rep}-{i}" for i in range(args.batch)]
     for i in range(args.warmup):
         eng.generate(prompts, steps_inf, seed=10 + i, output="tensor")
     lat = []
@@ -156,20 +206,21 @@ def bench_flux(args, rank, world):
     torch.cuda.synchronize()
     _barrier(world)
     elapsed = _max_over_ranks(time.perf_counter() - t0, world)
-    value = args.batch * args.steps * world / elapsed
+    value = args.batch * args.steps * replicas / elapsed
     p50 = statistics.median(lat) if lat else None
     return {
         "metric": f"Flux.1-dev {args.height}x{args.width} images/sec ({steps_inf} steps)",
         "value": round(value, 4), "unit": "images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2), "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if tp == 1 else "strong",
         "vs_baseline": round(REF_FLUX_512_10STEP_S / p50, 3) if (p50 and steps_inf == 10 and args.height == 512)
         else None,
         "dtype": "bf16", "data": "synthetic prompts, random-init weights (full Flux.1-dev architecture)",
         "config": {"model": "black-forest-labs/FLUX.1-dev (MMDiT 11.9B + T5-XXL + CLIP-L + VAE)",
-                   "global_batch": args.batch * world, "per_gpu_batch": args.batch, "seq_len": 512,
+                   "global_batch": args.batch * replicas, "per_replica_batch": args.batch, "seq_len": 512,
                    "resolution": f"{args.height}x{args.width}", "inference_steps": steps_inf,
-                   "guidance_scale": 3.5, "parallelism": f"dp{world}", "hip_graphs": not args.no_graphs},
+                   "guidance_scale": 3.5, "parallelism": f"dp{replicas}" + (f"xtp{tp}" if tp > 1 else ""),
+                   "hip_graphs": not args.no_graphs},
         "p50_latency_ms_bs1": round(1000 * p50, 1) if p50 else None,
         "baseline_note": "vs_baseline = 5.61 s (reference Flux 512^2 10-step end-to-end on Neuron TP8, "
                          "cova/README.md:98) / our p50 single-image latency",
@@ -305,7 +356,19 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--gen-len", type=int, default=128)
+    ap.add_argument("--cpu-dry-run", action="store_true",
+                    help="tests only: tiny SD2.1 config on the CPU over gloo (launcher / rendezvous / JSON plumbing)")
+    ap.add_argument("--tp", type=int, default=None,
+                    help="tensor-parallel degree per replica (mistral default: --gpus; flux default: 1)")
     args = ap.parse_args()
+    global DEVICE
+    if args.cpu_dry_run:
+        DEVICE = "cpu"
+        args.no_graphs = True
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        _relaunch(args.gpus)
+    if args.tp is None:
+        args.tp = args.gpus if args.workload in ("mistral", "mllama") else 1
     if args.batch is None:  # dynamic-batching caps a serving replica would use for each workload
         args.batch = {"sd21": 32, "mistral": 64, "flux": 1, "mllama": 8, "vit": 32}[args.workload]
     import torch
@@ -314,6 +377,8 @@ def main():
         fn = {"sd21": bench_sd21, "mistral": bench_mistral, "flux": bench_flux,
               "mllama": bench_mllama, "vit": bench_vit}[args.workload]
         res = fn(args, rank, world)
+    if DEVICE == "cpu":
+        res["data"] = "CPU DRY RUN (tiny config, gloo): plumbing check, not a measurement"
     if rank == 0:
         print(json.dumps(res), flush=True)
         save = os.environ.get("SHAI_GEMM_TUNE_SAVE")

@@ -744,9 +744,14 @@ def smoke_llm(device="cuda:0"):
 
 
 def bench_decode_throughput(args, rank, world):
-    """Mistral-7B bf16 at TP=world: batch of prompts, generate gen_len tokens each."""
+    """Mistral-7B bf16, ``args.tp``-way tensor parallel (default: all ``world`` GPUs), world / tp data-parallel
+    replicas: each replica generates gen_len tokens for a batch of prompt_len-token prompts; tokens/s is the
+    sum over replicas."""
     from ..parallel.state import init_distributed
-    init_distributed(tp_size=world)
+    tpd = int(getattr(args, "tp", None) or world)
+    assert world % tpd == 0, (world, tpd)
+    replicas = world // tpd
+    init_distributed(tp_size=tpd)
     cfg = LlamaConfig.mistral_7b()
     B, P, G = args.batch, args.prompt_len, args.gen_len
     quant = getattr(args, "quantization", None)
@@ -776,16 +781,17 @@ def bench_decode_throughput(args, rank, world):
         t = torch.tensor([el], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    toks = B * G * args.steps
+    toks = B * G * args.steps * replicas
     return {
         "metric": ("Mistral-7B output tokens/sec (fp8 e4m3 weights, bf16 activations, continuous batching)"
                    if quant == "fp8" else "Mistral-7B output tokens/sec (bf16, continuous batching)"),
         "value": round(toks / el, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 2), "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "fp8w-bf16a" if quant == "fp8" else "bf16",
+        "scaling": "strong" if replicas == 1 else "weak", "vs_baseline": None, "dtype": "fp8w-bf16a" if quant == "fp8" else "bf16",
         "data": "synthetic prompts, random-init weights",
-        "config": {"model": "mistralai/Mistral-7B-Instruct-v0.3 (architecture)", "global_batch": B,
-                   "seq_len": P + G, "prompt_len": P, "gen_len": G, "parallelism": f"tp{world}"},
+        "config": {"model": "mistralai/Mistral-7B-Instruct-v0.3 (architecture)", "global_batch": B * replicas,
+                   "seq_len": P + G, "prompt_len": P, "gen_len": G,
+                   "parallelism": (f"dp{replicas}x" if replicas > 1 else "") + f"tp{tpd}"},
         "p50_ttft_ms": round(1000 * float(np.median(ttft)), 2), "p50_tpot_ms": round(1000 * float(np.median(tpot)), 3),
     }
 
