@@ -12,18 +12,24 @@
 //      flags never need resetting and the kernel is HIP-graph replay safe),
 //   3. it sums the same slice from all `world` buffers (fp32 accumulate) into the
 //      output, 4. an end barrier so nobody overwrites a slice a peer still reads.
-// The buffer is allocated uncached (hipDeviceMallocUncached), so peer data and
-// flags are never served stale from an L2.  Spins are bounded: a missing peer
-// ends the call with a flagged error instead of hanging the GPU.
+// The buffer is allocated uncached (hipDeviceMallocUncached) and every read of a
+// PEER's buffer is a system-coherent buffer load (sc0 sc1), so peer data is never
+// served stale from a cache whatever the importer's IPC mapping type.  Spins are
+// bounded: a missing peer ends the call with the error flag set -- in the device
+// signal area AND in a host-mapped word the engine polls after every step without a
+// device sync (shai_p2p_error) -- instead of hanging the GPU.
+//
+// p2p_all_gather (below) reuses the same buffers and barriers: rank-major
+// concatenation of every rank's shard (vocab-parallel logits).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 namespace {
 
 constexpr int kMaxRanks = 8;
 constexpr int kMaxBlocks = 256;
-constexpr long kSpinLimit = 1L << 27;
 
 struct Layout {  // signal area at the start of each rank's buffer
   // flags[phase][block][src_rank] = epoch written by src_rank
@@ -36,7 +42,25 @@ constexpr size_t kDataOff = (sizeof(Layout) + 4095) & ~size_t(4095);
 
 struct Peers {
   char* base[kMaxRanks];
+  uint32_t* host_err;        // host-mapped (pinned) error word
+  unsigned long long spin_ticks;  // barrier timeout in wall-clock ticks (constant-rate counter)
 };
+
+// cache-policy bits of a vector memory instruction (gfx94x/gfx950): sc0 = 1, nt = 2, sc1 = 16; sc0|sc1 = system
+// scope -- a peer's bytes come over xGMI from its HBM, never from a (possibly stale) local cache line
+constexpr int kSysCoherent = 1 | 16;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t peer_rsrc(const char* base, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0,
+                                           (int)(bytes > 0x7fffffffu ? 0x7fffffffu : bytes), 0x00020000);
+}
+
+// 16 bytes at uint4 index i of the buffer behind rsrc (i * 16 < 2 GiB)
+__device__ __forceinline__ uint4 peer_load16(__amdgpu_buffer_rsrc_t r, long i) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16), 0, kSysCoherent));
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
 
 __device__ __forceinline__ void barrier_phase(const Peers& P, Layout* me, int phase, int rank, int world,
                                               uint32_t epoch) {
@@ -44,10 +68,11 @@ __device__ __forceinline__ void barrier_phase(const Peers& P, Layout* me, int ph
   if (t < world) {
     Layout* peer = reinterpret_cast<Layout*>(P.base[t]);
     __hip_atomic_store(&peer->flags[phase][b][rank], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    long spins = 0;
+    const unsigned long long t0 = wall_clock64();
     while (__hip_atomic_load(&me->flags[phase][b][t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
-      if (++spins > kSpinLimit) {
+      if (wall_clock64() - t0 > P.spin_ticks) {
         __hip_atomic_store(&me->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (P.host_err) __hip_atomic_store(P.host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -76,7 +101,7 @@ __global__ void __launch_bounds__(512) p2p_one_shot(Peers P, int rank, int world
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int r = 0; r < world; ++r) {
-      const uint4 v = reinterpret_cast<const uint4*>(P.base[r] + kDataOff)[i];
+      const uint4 v = r == rank ? mine[i] : peer_load16(peer_rsrc(P.base[r] + kDataOff, n16 * 16), i);
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -149,7 +174,7 @@ __global__ void __launch_bounds__(512) p2p_two_shot(Peers P, int rank, int world
       float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int r = 0; r < world; ++r) {
         const int src = (rank + r) % world;  // stagger the peers so the links are loaded evenly
-        const uint4 v = reinterpret_cast<const uint4*>(P.base[src] + kDataOff)[i];
+        const uint4 v = src == rank ? slotA[i] : peer_load16(peer_rsrc(P.base[src] + kDataOff, n16 * 16), i);
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -165,16 +190,56 @@ __global__ void __launch_bounds__(512) p2p_two_shot(Peers P, int rank, int world
   barrier_phase(P, me, 1, rank, world, epoch);
   for (int r = 0; r < world; ++r) {
     const int s = (rank + r) % world;
-    const uint4* src = reinterpret_cast<const uint4*>(P.base[s] + kDataOff + slot_bytes);
     const long beg = s * seg, end = min(n16, beg + seg);
-    for (long i = beg + t0; i < end; i += stride) out[i] = src[i];
+    if (s == rank) {
+      for (long i = beg + t0; i < end; i += stride) out[i] = slotB[i];
+    } else {
+      const __amdgpu_buffer_rsrc_t rb = peer_rsrc(P.base[s] + kDataOff + slot_bytes, n16 * 16);
+      for (long i = beg + t0; i < end; i += stride) out[i] = peer_load16(rb, i);
+    }
   }
+}
+
+// All-gather: out[r * n16 + i] = rank r's in[i] (rank-major concatenation), one shot.  Each rank stages its
+// shard in slot A, start barrier, every rank reads every peer's shard over its xGMI link, end barrier (a
+// peer may still be reading our slot A until then).
+__global__ void __launch_bounds__(512) p2p_all_gather(Peers P, int rank, int world, const uint4* in, uint4* out,
+                                                      long n16) {
+  __shared__ uint32_t s_epoch;
+  Layout* me = reinterpret_cast<Layout*>(P.base[rank]);
+  if (threadIdx.x == 0) {
+    const uint32_t e = me->epoch[blockIdx.x] + 1;
+    me->epoch[blockIdx.x] = e;
+    s_epoch = e;
+  }
+  __syncthreads();
+  const uint32_t epoch = s_epoch;
+  uint4* mine = reinterpret_cast<uint4*>(P.base[rank] + kDataOff);
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (long i = t0; i < n16; i += stride) {
+    const uint4 v = in[i];
+    mine[i] = v;
+    out[(long)rank * n16 + i] = v;
+  }
+  __threadfence_system();
+  __syncthreads();
+  barrier_phase(P, me, 0, rank, world, epoch);
+  for (int r = 1; r < world; ++r) {
+    const int s = (rank + r) % world;
+    const __amdgpu_buffer_rsrc_t rb = peer_rsrc(P.base[s] + kDataOff, n16 * 16);
+    for (long i = t0; i < n16; i += stride) out[(long)s * n16 + i] = peer_load16(rb, i);
+  }
+  __syncthreads();
+  barrier_phase(P, me, 1, rank, world, epoch);
 }
 
 struct Ctx {
   int rank, world, device;
+  int max_blocks;  // grid cap (identical on every rank): ranks sharing one GPU must all fit on it at once
   size_t max_bytes;
   char* local;
+  uint32_t* host_err;  // pinned, mapped into the device address space (Peers::host_err)
   Peers peers;
   bool opened[kMaxRanks];
 };
@@ -190,7 +255,8 @@ void* shai_p2p_create(int rank, int world, size_t max_bytes, char* handle_out) {
   c->rank = rank;
   c->world = world;
   c->max_bytes = max_bytes;
-  hipGetDevice(&c->device);
+  c->max_blocks = kMaxBlocks;
+  (void)hipGetDevice(&c->device);
   // signal area | slot A (staging, both algorithms) | slot B (two-shot reduced segments)
   if (hipExtMallocWithFlags(reinterpret_cast<void**>(&c->local), kDataOff + 2 * max_bytes,
                             hipDeviceMallocUncached) != hipSuccess) {
@@ -208,10 +274,30 @@ void* shai_p2p_create(int rank, int world, size_t max_bytes, char* handle_out) {
   memcpy(handle_out, &h, sizeof(h));
   memset(&c->peers, 0, sizeof(c->peers));
   c->peers.base[rank] = c->local;
+  {  // barrier timeout: SHAI_P2P_TIMEOUT_S seconds (default 20) of the constant-rate wall clock
+    int khz = 100000;
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device);
+    const char* e = getenv("SHAI_P2P_TIMEOUT_S");
+    const double secs = e ? atof(e) : 20.0;
+    c->peers.spin_ticks = (unsigned long long)(secs * 1000.0 * (khz > 0 ? khz : 100000));
+  }
+  c->host_err = nullptr;
+  if (hipHostMalloc(reinterpret_cast<void**>(&c->host_err), sizeof(uint32_t),
+                    hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+    *c->host_err = 0;
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, c->host_err, 0) == hipSuccess) c->peers.host_err = static_cast<uint32_t*>(dp);
+  }
   return c;
 }
 
 int shai_p2p_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+// Cap every kernel's grid at n workgroups (1..256); must be called identically on every rank.
+void shai_p2p_set_max_blocks(void* ctx, int n) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  c->max_blocks = n < 1 ? 1 : (n > kMaxBlocks ? kMaxBlocks : n);
+}
 
 // handles: world consecutive 64-byte handles (own entry ignored).  0 on success.
 int shai_p2p_open(void* ctx, const char* handles) {
@@ -234,7 +320,7 @@ int shai_p2p_allreduce_bf16(void* ctx, const void* in, void* out, size_t bytes, 
   if (bytes % 16 != 0 || bytes > c->max_bytes) return -1;
   const long n16 = (long)(bytes / 16);
   int blocks = (int)((n16 + 511) / 512);
-  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  if (blocks > c->max_blocks) blocks = c->max_blocks;
   if (blocks < 1) blocks = 1;
   // every rank must use the same grid: it is a function of bytes only
   hipLaunchKernelGGL(p2p_one_shot, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world,
@@ -249,16 +335,31 @@ int shai_p2p_allreduce2_bf16(void* ctx, const void* in, void* out, size_t bytes,
   const long n16 = (long)(bytes / 16);
   const long per_rank = (n16 + c->world - 1) / c->world;
   int blocks = (int)((per_rank + 511) / 512);
-  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  if (blocks > c->max_blocks) blocks = c->max_blocks;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(p2p_two_shot, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world,
                      static_cast<const uint4*>(in), static_cast<uint4*>(out), n16, c->max_bytes);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-// 1 if any spin timed out since creation (a peer did not arrive).
+// Rank-major all-gather of `bytes` (multiple of 16, <= max_bytes) per rank: out holds world * bytes.
+int shai_p2p_allgather(void* ctx, const void* in, void* out, size_t bytes, hipStream_t stream) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (bytes % 16 != 0 || bytes > c->max_bytes) return -1;
+  const long n16 = (long)(bytes / 16);
+  int blocks = (int)((n16 + 511) / 512);
+  if (blocks > c->max_blocks) blocks = c->max_blocks;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(p2p_all_gather, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world,
+                     static_cast<const uint4*>(in), static_cast<uint4*>(out), n16);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// 1 if any spin timed out since creation (a peer did not arrive).  Reads the host-mapped word: no device
+// synchronisation, cheap enough to poll after every engine step (falls back to a device read without it).
 int shai_p2p_error(void* ctx) {
   Ctx* c = static_cast<Ctx*>(ctx);
+  if (c->host_err) return (int)__atomic_load_n(c->host_err, __ATOMIC_ACQUIRE);
   uint32_t e = 0;
   (void)hipMemcpy(&e, c->local + offsetof(Layout, error), 4, hipMemcpyDeviceToHost);
   return (int)e;
@@ -270,6 +371,7 @@ void shai_p2p_destroy(void* ctx) {
   for (int r = 0; r < c->world; ++r)
     if (c->opened[r]) (void)hipIpcCloseMemHandle(c->peers.base[r]);
   (void)hipFree(c->local);
+  if (c->host_err) (void)hipHostFree(c->host_err);
   delete c;
 }
 

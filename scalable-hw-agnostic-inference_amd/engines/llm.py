@@ -722,6 +722,9 @@ class LLMEngine:
                 else:
                     self._finish_decode(h)
             self._last_step = "decode"
+        if tp().size > 1:  # a timed-out xGMI peer collective leaves partial sums: fail the step loudly
+            from ..parallel.comm import raise_if_p2p_error
+            raise_if_p2p_error()
         return self._reap()
 
     @torch.inference_mode()

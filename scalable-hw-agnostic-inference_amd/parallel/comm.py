@@ -8,8 +8,12 @@ and capturable in HIP graphs.  Two transports:
   :func:`reduce_scatter_seq`) used by the Flux single-stream blocks at SP > 1.
 * ``P2PAllReduce`` (``csrc/comm/p2p_allreduce.hip``) -- one-shot all-reduce for
   small, latency-bound messages (LLM decode: B x 4096 bf16 per layer), reading
-  every peer's IPC-mapped buffer directly over xGMI in one kernel.  Enabled
-  with ``SHAI_P2P_ALLREDUCE=1`` once registered via :func:`enable_p2p`.
+  every peer's IPC-mapped buffer directly over xGMI in one kernel, and a one-shot
+  all-gather (vocab-parallel logits).  ON by default for every TP > 1 group on
+  GPUs (``SHAI_P2P_ALLREDUCE=0`` disables it): all-reduces up to
+  ``SHAI_P2P_MAX_BYTES`` (default 512 KiB) and all-gather shards up to the buffer
+  capacity go through it; everything else goes to RCCL.  A peer that never arrives
+  sets an error word the engines poll after every step (:func:`raise_if_p2p_error`).
 
 On a fully connected 8x MI355X node each GPU has 7 xGMI links; RCCL's
 multi-channel rings / direct algorithms use them for the large Flux/prefill
@@ -27,12 +31,24 @@ from .state import tp
 
 _P2P = None
 P2P_ONE_SHOT_MAX = int(os.environ.get("SHAI_P2P_ONE_SHOT_MAX", str(512 * 1024)))
-P2P_MAX_BYTES = int(os.environ.get("SHAI_P2P_MAX_BYTES", str(64 << 20)))
+P2P_MAX_BYTES = int(os.environ.get("SHAI_P2P_MAX_BYTES", str(512 * 1024)))
+P2P_CAPACITY = int(os.environ.get("SHAI_P2P_CAPACITY", str(16 << 20)))
 
 
 def enable_p2p(p2p) -> None:
     global _P2P
     _P2P = p2p
+
+
+def p2p():
+    return _P2P
+
+
+def raise_if_p2p_error() -> None:
+    """Raise if an xGMI peer collective timed out (a peer never arrived): its output is a partial sum.
+    Reads a host-mapped word -- no device synchronisation -- so the engines call it after every step."""
+    if _P2P is not None and _P2P.error():
+        raise RuntimeError("xGMI P2P collective timed out waiting for a peer rank: TP group broken")
 
 
 def all_reduce(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
@@ -107,7 +123,11 @@ def all_gather_last(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) 
     n = st.size if group is None else dist.get_world_size(g)
     x = x.contiguous()
     flat = torch.empty((n * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(flat, x, group=g)   # rank-major concat along dim 0
+    if (group is None and _P2P is not None and x.is_cuda and x.dtype == torch.bfloat16
+            and _P2P.can_gather(x.numel() * x.element_size())):
+        _P2P.all_gather_into(flat, x)                  # one-shot over xGMI (vocab-parallel logits)
+    else:
+        dist.all_gather_into_tensor(flat, x, group=g)   # rank-major concat along dim 0
     out = flat.view((n,) + tuple(x.shape))
     return out.movedim(0, -2).reshape(*x.shape[:-1], n * x.shape[-1])
 
@@ -178,25 +198,27 @@ class P2PAllReduce:
     (``SHAI_P2P_ALLREDUCE=1`` in the engine).  Everything larger, or any other dtype, goes to RCCL."""
 
     def __init__(self, group: Optional[dist.ProcessGroup] = None, max_bytes: int = P2P_MAX_BYTES,
-                 one_shot_max: int = P2P_ONE_SHOT_MAX):
+                 one_shot_max: int = P2P_ONE_SHOT_MAX, capacity: Optional[int] = None):
         import ctypes
         from .. import native
         self.lib = native.comm()
         self.lib.shai_p2p_create.restype = ctypes.c_void_p
         self.lib.shai_p2p_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_char_p]
         self.lib.shai_p2p_open.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
-        for fn in (self.lib.shai_p2p_allreduce_bf16, self.lib.shai_p2p_allreduce2_bf16):
+        for fn in (self.lib.shai_p2p_allreduce_bf16, self.lib.shai_p2p_allreduce2_bf16, self.lib.shai_p2p_allgather):
             fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         self.one_shot_max = one_shot_max
         self.lib.shai_p2p_error.argtypes = [ctypes.c_void_p]
+        self.lib.shai_p2p_set_max_blocks.argtypes = [ctypes.c_void_p, ctypes.c_int]
         self.lib.shai_p2p_destroy.argtypes = [ctypes.c_void_p]
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        self.max_bytes = max_bytes
+        self.max_bytes = max_bytes                       # all-reduce routing threshold
+        self.capacity = max(max_bytes, capacity if capacity is not None else P2P_CAPACITY)   # staging slot size
         hs = self.lib.shai_p2p_handle_size()
         buf = ctypes.create_string_buffer(hs)
-        self.ctx = self.lib.shai_p2p_create(self.rank, self.world, max_bytes, buf)
+        self.ctx = self.lib.shai_p2p_create(self.rank, self.world, self.capacity, buf)
         if not self.ctx:
             raise RuntimeError("P2P all-reduce buffer allocation / IPC export failed")
         handles = [None] * self.world
@@ -204,6 +226,9 @@ class P2PAllReduce:
         rc = self.lib.shai_p2p_open(self.ctx, b"".join(handles))
         if rc != 0:
             raise RuntimeError(f"hipIpcOpenMemHandle failed for peer {-rc - 1}")
+        # ranks sharing one GPU (tests) must all be resident at once: SHAI_P2P_MAX_BLOCKS caps every grid
+        if os.environ.get("SHAI_P2P_MAX_BLOCKS"):
+            self.lib.shai_p2p_set_max_blocks(self.ctx, int(os.environ["SHAI_P2P_MAX_BLOCKS"]))
         dist.barrier(group=group)
 
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
@@ -217,6 +242,17 @@ class P2PAllReduce:
         if rc != 0:
             raise RuntimeError(f"p2p all-reduce launch failed ({rc})")
         return x
+
+    def can_gather(self, shard_bytes: int) -> bool:
+        return shard_bytes % 16 == 0 and shard_bytes <= self.capacity
+
+    def all_gather_into(self, out: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+        """Rank-major concatenation of every rank's contiguous bf16 ``x`` into ``out`` ([world * rows, ...])."""
+        st = torch.cuda.current_stream(x.device).cuda_stream
+        rc = self.lib.shai_p2p_allgather(self.ctx, x.data_ptr(), out.data_ptr(), x.numel() * x.element_size(), st)
+        if rc != 0:
+            raise RuntimeError(f"p2p all-gather launch failed ({rc})")
+        return out
 
     def error(self) -> bool:
         return bool(self.lib.shai_p2p_error(self.ctx))

@@ -27,15 +27,22 @@ class TPState:
 _TP = TPState()
 
 
-def init_distributed(backend: Optional[str] = None, tp_size: Optional[int] = None) -> TPState:
+def init_distributed(backend: Optional[str] = None, tp_size: Optional[int] = None,
+                     device: Optional[str] = None) -> TPState:
     """Initialise the default process group from torchrun env vars and make the
-    (single) tensor-parallel group span ``tp_size`` consecutive ranks."""
+    (single) tensor-parallel group span ``tp_size`` consecutive ranks.
+
+    GPUs: backend "nccl" (RCCL) with one GPU per rank; every TP group of size > 1 also gets the xGMI P2P
+    all-reduce / all-gather (``SHAI_P2P_ALLREDUCE=0`` disables it).  ``device="cuda"`` with backend "gloo" puts
+    every rank on GPU ``LOCAL_RANK % device_count`` with gloo only for host-side coordination -- several ranks
+    sharing ONE GPU (tests): then the model's collectives must fit the P2P kernels."""
     global _TP
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    use_gpu = torch.cuda.is_available() and (backend != "gloo" or device == "cuda")
     if use_gpu:
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:
@@ -56,10 +63,12 @@ def init_distributed(backend: Optional[str] = None, tp_size: Optional[int] = Non
             if rank in ranks:
                 group = g
     _TP = TPState(rank % tp if tp > 1 else 0, tp, group, device)
-    if tp > 1 and use_gpu and os.environ.get("SHAI_P2P_ALLREDUCE", "0") == "1":
-        # custom xGMI peer all-reduce (one-shot / two-shot) for the TP group; RCCL stays the fallback
-        from .comm import P2PAllReduce, enable_p2p
-        enable_p2p(P2PAllReduce(group))
+    if tp > 1 and use_gpu and os.environ.get("SHAI_P2P_ALLREDUCE", "1") != "0":
+        # custom xGMI peer all-reduce / all-gather for the TP group (small, latency-bound messages); RCCL for
+        # the rest
+        from .comm import P2PAllReduce, enable_p2p, p2p
+        if p2p() is None or p2p().world != tp:
+            enable_p2p(P2PAllReduce(group))
     return _TP
 
 

@@ -90,8 +90,11 @@ class SPMDProxy:
             return attr
 
         def call(*args, **kwargs):
+            from ..parallel.comm import raise_if_p2p_error
             self._channel.send(CALL, (name, args, kwargs))
-            return attr(*args, **kwargs)
+            out = attr(*args, **kwargs)
+            raise_if_p2p_error()
+            return out
         return call
 
 
@@ -109,8 +112,10 @@ def follow(target, channel: TPChannel, step_fn=None) -> int:
         try:
             with torch.inference_mode():
                 if kind == CALL:
+                    from ..parallel.comm import raise_if_p2p_error
                     name, args, kwargs = payload
                     getattr(target, name)(*args, **kwargs)
+                    raise_if_p2p_error()
                 elif kind == STEP and step_fn is not None:
                     step_fn(payload)
         except Exception as e:  # noqa: BLE001 -- mirrored on the leader
@@ -216,8 +221,11 @@ def setup(tensor_parallel_size: Optional[int] = None) -> TPContext:
     if world == 1:
         return TPContext()
     from ..parallel.state import init_distributed
-    backend = "gloo" if os.environ.get("DEVICE", "").lower() == "cpu" else None
-    init_distributed(backend=backend, tp_size=tp)
+    on_cpu = os.environ.get("DEVICE", "").lower() == "cpu"
+    # SHAI_TP_BACKEND=gloo on GPUs: ranks may share a GPU (tests); the model's collectives then run on the
+    # xGMI/IPC P2P kernels and gloo only coordinates
+    backend = "gloo" if on_cpu else (os.environ.get("SHAI_TP_BACKEND") or None)
+    init_distributed(backend=backend, tp_size=tp, device=None if on_cpu else "cuda")
     ctx = TPContext(dist.get_rank(), world, TPChannel())
     _log.info("tp worker up", extra={"event": "tp_up", "detail": f"rank {ctx.rank}/{world}"})
     return ctx

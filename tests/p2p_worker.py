@@ -1,5 +1,6 @@
-"""Two ranks on ONE GPU (gloo for the handle exchange): the IPC-mapped one-shot and two-shot all-reduces
-must equal the sum of both ranks' tensors, repeatedly, at mixed sizes and inside a HIP graph."""
+"""world ranks (2, 4 or 8) on ONE GPU (gloo for the handle exchange): the IPC-mapped one-shot and two-shot
+all-reduces must equal the sum of every rank's tensor, and the one-shot all-gather the rank-major
+concatenation, repeatedly, at mixed sizes and inside a HIP graph."""
 import os
 
 import torch
@@ -7,6 +8,10 @@ import torch
 
 def run(rank, world, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    # every rank's spinning workgroups must fit on the ONE shared GPU together (8 x 32 x 512 threads), and a
+    # barrier that still never completes errors out in seconds instead of hanging the test
+    os.environ.setdefault("SHAI_P2P_MAX_BLOCKS", str(256 // world))
+    os.environ.setdefault("SHAI_P2P_TIMEOUT_S", "10")
     import torch.distributed as dist
     dist.init_process_group("gloo")
     torch.cuda.set_device(0)
@@ -24,6 +29,17 @@ def run(rank, world, port):
             err = ((x.float() - want).abs().max() / want.abs().max()).item()
             assert err < 2e-2, (n, it, err)
             dist.barrier()
+    # all-gather (vocab-parallel logits: [B, V / world] shards -> [world * B, V / world] rank-major)
+    for rows, cols in ((1, 8), (64, 4096), (3, 1000), (64, 16032)):
+        torch.manual_seed(rows * 7 + cols)
+        full = [torch.randn(rows, cols, device="cuda").bfloat16() for _ in range(world)]
+        out = torch.empty(world * rows, cols, device="cuda", dtype=torch.bfloat16)
+        assert ar.can_gather(rows * cols * 2) == ((rows * cols * 2) % 16 == 0)
+        if ar.can_gather(rows * cols * 2):
+            ar.all_gather_into(out, full[rank])
+            torch.cuda.synchronize()
+            assert torch.equal(out, torch.cat(full, 0)), (rows, cols)
+        dist.barrier()
     # graph replay
     x = torch.ones(4096, device="cuda").bfloat16() * (rank + 1)
     s = torch.cuda.Stream()
@@ -42,7 +58,8 @@ def run(rank, world, port):
         dist.barrier()
         g.replay()
         torch.cuda.synchronize()
-        assert torch.allclose(y.float(), torch.full_like(y.float(), 3.0)), y[:4]
+        want = world * (world + 1) / 2
+        assert torch.allclose(y.float(), torch.full_like(y.float(), want)), y[:4]
         dist.barrier()
     assert not ar.error()
     dist.barrier()
