@@ -790,6 +790,54 @@ void flash_attn(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor&
   shai::launch_flash_attn(a, stream());
 }
 
+// Packed varlen prefill attention over the paged KV cache: q / o are flat [T, Hq, D] (no padding rows);
+// sequence b's queries are rows q_start[b] .. + q_lens[b] - 1, its keys the first kv_lens[b] cache entries
+// of its block table; causal with offset kv_len - q_len.  max_q = max(q_lens) sizes the grid.
+void paged_attn_varlen(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& o,
+                       const Tensor& block_table, const Tensor& kv_lens, const Tensor& q_lens, const Tensor& q_start,
+                       int64_t max_q, double scale, bool causal) {
+  check_rows(q, "q");
+  check_rows(o, "o");
+  SHAI_CHECK(q.dim() == 3 && o.dim() == 3 && q.sizes() == o.sizes(), "q/o must be [T, H, D]");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_i32(block_table, "block_table");
+  check_i32(kv_lens, "kv_lens");
+  check_i32(q_lens, "q_lens");
+  check_i32(q_start, "q_start");
+  shai::AttnArgs a{};
+  a.B = block_table.size(0);
+  SHAI_CHECK(kv_lens.numel() == a.B && q_lens.numel() == a.B && q_start.numel() == a.B, "per-sequence [B] metadata");
+  SHAI_CHECK(max_q >= 1, "max_q >= 1");
+  a.Sq = (int)max_q;
+  a.Hq = q.size(1);
+  a.D = q.size(2);
+  SHAI_CHECK(a.D == 64 || a.D == 128, "paged_attn_varlen supports head dim 64 / 128, got ", a.D);
+  SHAI_CHECK(q.stride(1) == a.D && o.stride(1) == a.D, "heads must be packed (head stride == D)");
+  SHAI_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 64 && k_cache.size(3) == a.D && k_cache.is_contiguous() &&
+                 v_cache.is_contiguous() && v_cache.sizes() == k_cache.sizes(),
+             "paged k/v must be [blocks, Hkv, 64, D]");
+  a.Hkv = k_cache.size(1);
+  SHAI_CHECK(a.Hq % a.Hkv == 0, "Hq must be a multiple of Hkv");
+  a.block_table = block_table.data_ptr<int>();
+  a.max_blocks = block_table.size(1);
+  a.kc_bs = k_cache.stride(0);
+  a.kc_hs = k_cache.stride(1);
+  a.Skv = a.max_blocks * 64;
+  a.q = cptr(q);
+  a.k = cptr(k_cache);
+  a.v = cptr(v_cache);
+  a.o = mptr(o);
+  a.q_ts = q.stride(0);
+  a.o_ts = o.stride(0);
+  a.scale = scale;
+  a.causal = causal;
+  a.kv_lens = kv_lens.data_ptr<int>();
+  a.q_lens = q_lens.data_ptr<int>();
+  a.q_start = q_start.data_ptr<int>();
+  shai::launch_flash_attn(a, stream());
+}
+
 void decode_attn(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& o,
                  const Tensor& block_table, const Tensor& ctx_lens, const Tensor& ws, int64_t num_splits,
                  double scale) {
@@ -1060,6 +1108,7 @@ TORCH_LIBRARY(shai, m) {
   m.def("qk_norm_rope(Tensor(a!) x, Tensor? q_w, Tensor? k_w, Tensor? cos, Tensor? sin, int H, int D, int S, float eps) -> ()");
   m.def("conv2d(Tensor x, Tensor? x2, Tensor w, Tensor(a!) out, Tensor? bias, Tensor? bias2d, Tensor? residual, Tensor? in_scale, Tensor? in_shift, int in_act, int kh, int kw, int stride, int pad, bool upsample, int act, float res_alpha) -> ()");
   m.def("flash_attn(Tensor q, Tensor k, Tensor v, Tensor(a!) o, float scale, bool causal, int causal_offset, Tensor? kv_lens, Tensor? q_lens, Tensor? bias, Tensor? block_table) -> ()");
+  m.def("paged_attn_varlen(Tensor q, Tensor k_cache, Tensor v_cache, Tensor(a!) o, Tensor block_table, Tensor kv_lens, Tensor q_lens, Tensor q_start, int max_q, float scale, bool causal) -> ()");
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor(a!) o, Tensor block_table, Tensor ctx_lens, Tensor(b!) ws, int num_splits, float scale) -> ()");
   m.def("kv_write(Tensor k, Tensor v, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slots) -> ()");
   m.def("gated_act(Tensor x, Tensor(a!) out, int act, bool gate_first) -> ()");
@@ -1091,6 +1140,7 @@ TORCH_LIBRARY_IMPL(shai, CUDA, m) {
   m.impl("qk_norm_rope", &qk_norm_rope);
   m.impl("conv2d", &conv2d);
   m.impl("flash_attn", &flash_attn);
+  m.impl("paged_attn_varlen", &paged_attn_varlen);
   m.impl("decode_attn", &decode_attn);
   m.impl("kv_write", &kv_write);
   m.impl("gated_act", &gated_act);

@@ -118,7 +118,8 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
   // ---- Q fragments (B operand of S^T = K Q^T): Q[qi][16 s + 8 fh .. +7]
   bf16x8a qf[NS];
   {
-    const bf16_t* qp = p.q + (long)b * p.q_bs + (long)min(qi, q_len - 1) * p.q_ts + (long)hq * D;
+    const bf16_t* qp = p.q + (p.q_start ? (long)p.q_start[b] * p.q_ts : (long)b * p.q_bs) +
+                        (long)min(qi, q_len - 1) * p.q_ts + (long)hq * D;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       uint4_ v = *reinterpret_cast<const uint4_*>(qp + 16 * s + 8 * fh);
@@ -385,7 +386,8 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   if (qi < q_len) {
-    bf16_t* op = p.o + (long)b * p.o_bs + (long)qi * p.o_ts + (long)hq * D;
+    bf16_t* op = p.o + (p.q_start ? (long)p.q_start[b] * p.o_ts : (long)b * p.o_bs) + (long)qi * p.o_ts +
+                 (long)hq * D;
 #pragma unroll
     for (int d = 0; d < ND; ++d) {
 #pragma unroll

@@ -33,6 +33,8 @@
 #include "launchers.h"
 
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 namespace shai {
 
@@ -146,7 +148,8 @@ __device__ __forceinline__ int sk_f8_off(int row, int c8) {
 
 template <int MB, bool GLU, int ACT, bool RMS, bool F8>
 __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmArgs p, float* __restrict__ ws,
-                                                                    int kg_steps, unsigned* __restrict__ cnt) {
+                                                                    int kg_steps, unsigned* __restrict__ cnt,
+                                                                    int relaxed_ticket) {
   using G = SkGeom<MB, F8>;
   constexpr int XG = G::XG;
   extern __shared__ __attribute__((aligned(16))) bf16_t sk_smem[];
@@ -301,10 +304,11 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
     return;
   }
   if (cnt != nullptr) {
-    // ---- split-K fixed up in this launch (no reduce kernel, no fences): every K group writes its 64 x MB
-    // partial slab (+ MB row sums of squares) write-through (sc1), drains (vmcnt 0 in every wave), joins
-    // the workgroup barrier, then one lane takes a ticket (relaxed agent atomic); the workgroup that draws
-    // KG-1 re-arms the ticket and reduces the KG slabs with sc1 loads before the fused epilogue.
+    // ---- split-K fixed up in this launch (no reduce kernel): every K group writes its 64 x MB partial slab
+    // (+ MB row sums of squares) write-through (sc1), drains (vmcnt 0 in every wave), joins the workgroup
+    // barrier, then one lane takes a ticket (acq_rel agent-scope atomic on this launch's own ticket slice,
+    // sk_tickets); the workgroup that draws KG-1 re-arms the ticket and reduces the KG slabs with sc1 loads
+    // before the fused epilogue.
     // (MI355X_MICROARCH / hip guide "Projection GEMM at M = 256" item 2, write-through form.)
     constexpr int SLAB = 64 * MB + MB, PT = 64 * MB / 256;
     const __amdgpu_buffer_rsrc_t rws = sk_rsrc(ws, 0x7fffffffu);
@@ -328,7 +332,12 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
     __syncthreads();
     __shared__ unsigned sk_last;
     if (tid == 0) {
-      const unsigned old = __hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // acq_rel at agent scope: this group's slab stores (already write-through) are released before its
+      // arrival counts, and the last arriver's slab reads below are ordered after every arrival it observed
+      // (SHAI_SK_RELAXED_TICKET=1: the relaxed form the write-through slab protocol was first measured with)
+      const unsigned old = relaxed_ticket
+                               ? __hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : __hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       sk_last = old == (unsigned)(KG - 1);
     }
     __syncthreads();
@@ -455,21 +464,52 @@ int skinny_max_kgroups(const GemmArgs& a) {
   return kg;
 }
 
-// Per-device arrival tickets of the in-kernel split-K fixup: zeroed once, re-armed by every last arriver.
-constexpr int kSkTickets = 4096;
-static unsigned* sk_tickets(hipStream_t s) {
-  static unsigned* tickets[64] = {};
+// Arrival tickets of the in-kernel split-K fixup.  One pool per device (kSkPool tickets, zeroed once, outside
+// any capture); every launch counts arrivals in a slice of it that no launch able to run at the same time
+// shares: a launch being captured into a HIP graph takes a fresh slice from a bump allocator (the graph keeps
+// it for its lifetime: replays of one graph are serialised by its own buffers), an eager launch uses the
+// slice owned by its stream.  The last arriver re-arms its ticket, so a slice serves every later launch on
+// the same stream / replay of the same graph.  No slice (pool not yet allocated while capturing, or
+// exhausted) -> the separate fold kernel, which needs no tickets.
+constexpr int kSkTickets = 4096;            // max tiles of one launch (and the per-stream slice)
+constexpr size_t kSkPool = size_t(1) << 24;  // 16 M tickets = 64 MB per device
+
+struct SkTicketPool {
+  unsigned* base = nullptr;
+  size_t next = 0;
+  std::map<hipStream_t, unsigned*> per_stream;
+};
+
+static unsigned* sk_tickets(hipStream_t s, int ntiles) {
+  static std::mutex mu;
+  static SkTicketPool pools[64];
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (tickets[dev] == nullptr) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;  // never allocate inside a graph capture
+  if (ntiles > kSkTickets || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess) return nullptr;
+  const bool capturing = cs != hipStreamCaptureStatusNone;
+  std::lock_guard<std::mutex> lock(mu);
+  SkTicketPool& P = pools[dev];
+  if (P.base == nullptr) {
+    if (capturing) return nullptr;  // never allocate inside a graph capture
     unsigned* p = nullptr;
-    if (hipMalloc(&p, kSkTickets * sizeof(unsigned)) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, kSkTickets * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return nullptr;
-    tickets[dev] = p;
+    if (hipMalloc(&p, kSkPool * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, kSkPool * sizeof(unsigned)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+      (void)hipFree(p);
+      return nullptr;
+    }
+    P.base = p;
   }
-  return tickets[dev];
+  if (!capturing) {
+    auto it = P.per_stream.find(s);
+    if (it != P.per_stream.end()) return it->second;
+  }
+  const size_t want = capturing ? (size_t)ntiles : (size_t)kSkTickets;
+  if (P.next + want > kSkPool) return nullptr;
+  unsigned* slice = P.base + P.next;
+  P.next += (want + 63) & ~size_t(63);
+  if (!capturing) P.per_stream[s] = slice;
+  return slice;
 }
 
 template <int MB, bool F8>
@@ -478,10 +518,11 @@ static void launch_skinny_mb(const GemmArgs& a, float* ws, int kg, unsigned* cnt
   const int kg_steps = (ksteps + kg - 1) / kg;
   dim3 grid((a.N + SK_BN - 1) / SK_BN, kg), block(SK_WAVES * 64);
   const size_t lds = SkGeom<MB, F8>::LDS;
+  static const int rlx = getenv("SHAI_SK_RELAXED_TICKET") != nullptr && getenv("SHAI_SK_RELAXED_TICKET")[0] == '1';
 #define SK(G, A)                                                                                          \
   do {                                                                                                    \
-    if (a.rms) skinny_gemm_kernel<MB, G, A, true, F8><<<grid, block, lds, s>>>(a, ws, kg_steps, cnt);  \
-    else skinny_gemm_kernel<MB, G, A, false, F8><<<grid, block, lds, s>>>(a, ws, kg_steps, cnt);       \
+    if (a.rms) skinny_gemm_kernel<MB, G, A, true, F8><<<grid, block, lds, s>>>(a, ws, kg_steps, cnt, rlx);  \
+    else skinny_gemm_kernel<MB, G, A, false, F8><<<grid, block, lds, s>>>(a, ws, kg_steps, cnt, rlx);       \
   } while (0)
 #define SK_ACT(G)                                      \
   switch (a.act) {                                     \
@@ -508,7 +549,7 @@ void launch_skinny_kg(const GemmArgs& a, float* ws, int kg, hipStream_t s, bool 
   if (kg > ksteps) kg = ksteps;
   // split-K: fixed up inside the launch when asked for and tickets are available, else a separate fold
   unsigned* cnt = nullptr;
-  if (kg > 1 && fixup && (a.N + SK_BN - 1) / SK_BN <= kSkTickets) cnt = sk_tickets(s);
+  if (kg > 1 && fixup) cnt = sk_tickets(s, (a.N + SK_BN - 1) / SK_BN);
   if (a.w_scale) {
     if (a.M <= 32) launch_skinny_mb<32, true>(a, ws, kg, cnt, s);
     else launch_skinny_mb<64, true>(a, ws, kg, cnt, s);

@@ -156,6 +156,8 @@ struct AttnArgs {
   int causal_offset;        // query i sees keys <= i + causal_offset
   const int* kv_lens;       // optional [B] valid key count per batch
   const int* q_lens;        // optional [B] valid query count; causal offset becomes kv_len - q_len
+  const int* q_start;       // optional [B] packed varlen: sequence b's queries / outputs are rows
+                            // q_start[b] .. q_start[b] + q_lens[b] - 1 of a flat [T, Hq, D] q / o (q_bs unused)
   const bf16_t* bias;       // optional additive bias [Hq, Sq, Skv] (bf16), broadcast over batch
   // paged K/V (LLM prefill over cached context): block tables of 64-token blocks
   const int* block_table;   // optional [B, max_blocks]

@@ -77,4 +77,30 @@ void shai_build_prefill(int B, int S, const int* n_cached, const int* n_new, con
   }
 }
 
+// Packed (varlen) prefill: the step's T = sum(n_new) tokens are laid out back to back, no padding rows.
+// Sequence b owns rows q_start[b] .. q_start[b] + n_new[b] - 1; a decode row is simply a sequence with
+// n_new = 1 (its last token, n_cached = length - 1), so prefill chunks and decode rows share one step.
+void shai_build_prefill_packed(int B, const int* n_cached, const int* n_new, const int* tables_flat,
+                               const int* table_offs, int max_blocks, int* positions, int* slots, int* ctx_lens,
+                               int* q_lens, int* q_start, int* bt_out, int* last_index) {
+  int t = 0;
+  for (int b = 0; b < B; ++b) {
+    const int* tb = tables_flat + table_offs[b];
+    const int nb = table_offs[b + 1] - table_offs[b];
+    q_start[b] = t;
+    for (int s = 0; s < n_new[b]; ++s, ++t) {
+      const int pos = n_cached[b] + s;
+      positions[t] = pos;
+      slots[t] = pos / kBlock < nb ? tb[pos / kBlock] * kBlock + pos % kBlock : -1;
+    }
+    ctx_lens[b] = n_cached[b] + n_new[b];
+    q_lens[b] = n_new[b];
+    last_index[b] = t - 1;
+    int* row = bt_out + (int64_t)b * max_blocks;
+    const int n = std::min(nb, max_blocks);
+    std::copy(tb, tb + n, row);
+    std::fill(row + n, row + max_blocks, 0);
+  }
+}
+
 }  // extern "C"

@@ -64,7 +64,7 @@ class FluxPipelineConfig:
             transformer=t,
             clip=CLIPTextConfig(vocab_size=1000, hidden_size=t.pooled_projection_dim, intermediate_size=64,
                                 num_hidden_layers=1, num_attention_heads=1, bos_token_id=998, eos_token_id=999),
-            t5=T5Config(vocab_size=500, d_model=t.joint_attention_dim, d_kv=32, d_ff=128, num_layers=1, num_heads=2),
+            t5=T5Config(vocab_size=500, d_model=t.joint_attention_dim, d_kv=64, d_ff=128, num_layers=1, num_heads=2),
             vae=VAEConfig.tiny(latent_channels=16), height=64, width=64, max_sequence_length=16)
 
 

@@ -8,10 +8,13 @@ HF ``generate`` (app/run-llama.py:34-46, app/deepseek_model_api.py:45-57).
 Per engine step (one call to :meth:`LLMEngine.step`):
   1. the native scheduler (csrc/runtime/scheduler.cpp) admits waiting prompts
      FCFS under KV-block / sequence / token budgets;
-  2. admitted prompts run as one padded prefill batch (prefix-cached blocks are
-     reused via the native block manager's content hashes); prompts longer than
-     ``prefill_chunk`` are prefilled chunk by chunk, the chunks alternating with
-     decode steps so running sequences keep streaming (chunked prefill);
+  2. admitted prompts run as one PACKED varlen prefill batch -- the step's
+     sum(new tokens) rows back to back, no [B, S_max] padding, attention over
+     per-sequence row offsets (prefix-cached blocks are reused via the native
+     block manager's content hashes); prompts longer than ``prefill_chunk`` are
+     prefilled chunk by chunk (chunked prefill), and the running batch's decode
+     rows join every prefill step as one-token rows (mixed steps), so running
+     sequences keep streaming while long prompts are encoded;
   3. otherwise every running sequence decodes one token -- the decode forward
      for each batch-size bucket is captured once into a HIP graph and replayed,
      with the fused RoPE / KV-write / attention kernel and the sampler inside;
@@ -316,7 +319,8 @@ class LLMEngine:
                  max_num_seqs: int = 64, max_model_len: int = 4096, num_kv_blocks: Optional[int] = None,
                  gpu_memory_utilization: float = 0.85, prefill_token_budget: int = 8192, use_graphs: bool = True,
                  enable_prefix_caching: bool = True, prefill_chunk: Optional[int] = None,
-                 quantization: Optional[str] = None, async_decode: Optional[bool] = None):
+                 quantization: Optional[str] = None, async_decode: Optional[bool] = None,
+                 packed_prefill: bool = True, mixed_steps: bool = True):
         from ..models.mllama import MllamaConfig, MllamaForConditionalGeneration
         from ..runtime import BlockManager
         self.mcfg = cfg if isinstance(cfg, MllamaConfig) else None
@@ -360,6 +364,9 @@ class LLMEngine:
         # longest prompt slice one prefill step processes (chunked prefill; SURVEY 5.7: <= 8k tokens)
         self.prefill_chunk = max(KV_BLOCK, prefill_chunk or prefill_token_budget)
         self._last_step = "decode"
+        # packed varlen prefill (no [B, S_max] padding) with decode rows mixed into prefill steps (text models)
+        self.packed_prefill = packed_prefill and os.environ.get("SHAI_PADDED_PREFILL", "0") != "1"
+        self.mixed_steps = mixed_steps
         self.prefix_caching = enable_prefix_caching
         self.use_graphs = use_graphs and self.device.type == "cuda"
         self.waiting: List[Sequence_] = []
@@ -488,11 +495,17 @@ class LLMEngine:
         del self.waiting[:n]
         return adm
 
-    def _prefill(self, seqs: List[Sequence_]):
+    def _prefill(self, seqs: List[Sequence_], decode_rows: Sequence[Sequence_] = ()):
         """One prefill chunk for each of ``seqs``: at most ``prefill_chunk`` new prompt tokens per sequence
-        (chunked prefill -- a long prompt spans several engine steps that alternate with decode steps of
-        the running batch).  The first chunk looks up cached prefix blocks and allocates the sequence's KV
-        (and image) blocks; only sequences whose prompt is complete sample their first token."""
+        (chunked prefill -- a long prompt spans several engine steps).  The first chunk looks up cached prefix
+        blocks and allocates the sequence's KV (and image) blocks; only sequences whose prompt is complete
+        sample their first token.
+
+        Text models run the step PACKED: the T = sum(new tokens) rows go back to back through every GEMM (no
+        [B, S_max] padding) and attention takes per-sequence row offsets (``ops.paged_attention_varlen``).
+        ``decode_rows`` -- running sequences that would otherwise wait for this prefill step -- join it as
+        one-token rows (their last token against their cached context), so prefill chunks and decode share
+        the step instead of alternating with it."""
         for s in seqs:
             if s.prefill_started:
                 continue
@@ -511,17 +524,31 @@ class LLMEngine:
             if s.image is not None and not s.cross_blocks:
                 s.cross_blocks = self.bm.allocate(self.max_cross_blocks)
                 s._img_encoded = False
-        news = [min(len(s.prompt) - s.n_cached, self.prefill_chunk) for s in seqs]
+        packed = self.mcfg is None and self.packed_prefill
+        decode_rows = [s for s in decode_rows if self._ensure_blocks(s, s.length)] if packed else []
+        rows = list(seqs) + decode_rows
+        n_pre = len(seqs)
+        news = [min(len(s.prompt) - s.n_cached, self.prefill_chunk) for s in seqs] + [1] * len(decode_rows)
         S = max(news)
-        from ..runtime import build_prefill
-        pos, slots, lens, qlens, bt, last = build_prefill([s.n_cached for s in seqs], news,
-                                                          [s.blocks for s in seqs], S, self.max_blocks)
-        ids = np.zeros(len(seqs) * S, dtype=np.int32)
-        for i, (s, n) in enumerate(zip(seqs, news)):
-            ids[i * S:i * S + n] = s.prompt[s.n_cached:s.n_cached + n]
         d = self.device
         t = lambda a: torch.from_numpy(a).to(d, non_blocking=True)
-        batch = Batch(t(ids), t(pos), t(slots), t(bt), t(lens), t(qlens), len(seqs), S, True, 1, t(last).long())
+        if packed:
+            from ..runtime import build_prefill_packed
+            pos, slots, lens, qlens, qstart, bt, last = build_prefill_packed([s.n_cached for s in rows], news,
+                                                                             [s.blocks for s in rows],
+                                                                             self.max_blocks)
+            ids = np.concatenate([np.asarray((s.prompt if not s.output else s.tokens)[s.n_cached:s.n_cached + n],
+                                             dtype=np.int32) for s, n in zip(rows, news)])
+            batch = Batch(t(ids), t(pos), t(slots), t(bt), t(lens), t(qlens), len(rows), S, True, 1,
+                          t(last).long(), q_start=t(qstart))
+        else:
+            from ..runtime import build_prefill
+            pos, slots, lens, qlens, bt, last = build_prefill([s.n_cached for s in seqs], news,
+                                                              [s.blocks for s in seqs], S, self.max_blocks)
+            ids = np.zeros(len(seqs) * S, dtype=np.int32)
+            for i, (s, n) in enumerate(zip(seqs, news)):
+                ids[i * S:i * S + n] = s.prompt[s.n_cached:s.n_cached + n]
+            batch = Batch(t(ids), t(pos), t(slots), t(bt), t(lens), t(qlens), len(seqs), S, True, 1, t(last).long())
         if any(s.cross_blocks for s in seqs):
             fresh = [s for s in seqs if s.cross_blocks and not s._img_encoded]
             if fresh:
@@ -530,10 +557,14 @@ class LLMEngine:
                     s._img_encoded = True
             self._attach_cross_prefill(batch, seqs, S, news)
         logits = self.model(batch, self.kv)
-        self.stats["prefill_tokens"] += int(sum(news))
+        self.stats["prefill_tokens"] += int(sum(news[:n_pre]))
+        self.stats["decode_tokens"] += len(decode_rows)
         done = []
-        for i, (s, n) in enumerate(zip(seqs, news)):
+        for i, (s, n) in enumerate(zip(rows, news)):
             s.n_cached += n
+            if i >= n_pre:       # decode row: always samples its next token
+                done.append(i)
+                continue
             if s.n_cached < len(s.prompt):
                 continue
             done.append(i)
@@ -541,8 +572,8 @@ class LLMEngine:
                 for j, h in enumerate(s._hashes):
                     self.bm.register(s.blocks[j], h)
         if done:
-            sel = logits if len(done) == len(seqs) else logits.index_select(0, torch.tensor(done, device=d))
-            self._sample_and_append([seqs[i] for i in done], sel)
+            sel = logits if len(done) == len(rows) else logits.index_select(0, torch.tensor(done, device=d))
+            self._sample_and_append([rows[i] for i in done], sel)
 
     # ------------------------------------------------------------------ images (multimodal models)
     def _encode_images(self, seqs: List[Sequence_]):
@@ -707,11 +738,13 @@ class LLMEngine:
         adm = self._admit()
         pending = [s for s in self.running if s.n_cached < len(s.prompt)]     # mid chunked prefill
         decodable = [s for s in self.running if s.n_cached >= len(s.prompt) and not s.finished]
-        # new prompts and remaining prefill chunks alternate with decode steps of the running batch
-        if adm or (pending and (not decodable or self._last_step != "prefill")):
+        mix = self.mcfg is None and self.packed_prefill and self.mixed_steps
+        # new prompts and remaining prefill chunks run as packed prefill steps that the running batch's decode
+        # rows join (mixed steps); without mixing (multimodal models) they alternate with decode steps
+        if adm or (pending and (mix or not decodable or self._last_step != "prefill")):
             self.running += adm
             with prof.range_("llm_prefill"):
-                self._prefill(pending + adm)
+                self._prefill(pending + adm, decodable if mix else ())
             self._last_step = "prefill"
         elif decodable:
             with prof.range_("llm_decode"):

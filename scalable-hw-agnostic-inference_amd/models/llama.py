@@ -118,7 +118,7 @@ def rope_tables(cfg: LlamaConfig, max_pos: int, device) -> tuple:
 
 @dataclass
 class Batch:
-    """Flattened token batch for one engine step (prefill is padded to [B, S])."""
+    """Flattened token batch for one engine step (prefill: packed varlen rows, or padded to [B, S])."""
     input_ids: torch.Tensor         # [T] int32 (T = B*S for prefill, B for decode)
     positions: torch.Tensor         # [T] int32
     slots: torch.Tensor             # [T] int32 cache slot (-1 = padding)
@@ -139,6 +139,9 @@ class Batch:
     cross_attn_rows: Optional[torch.Tensor] = None  # [T] bool row's sequence has an image
     cross_mlp_rows: Optional[torch.Tensor] = None   # [T] bool cross MLP applies (image, at/after <|image|>)
     cross_splits: int = 1
+    # packed varlen prefill: T = sum(q_lens) rows, sequence b's rows start at q_start[b] (no padding rows);
+    # S is then max(q_lens).  None = the padded [B, S] layout.
+    q_start: Optional[torch.Tensor] = None
 
 
 class LlamaAttention(nn.Module):
@@ -164,7 +167,10 @@ class LlamaAttention(nn.Module):
             return self.o_proj(o, residual=residual)
         ops.rope_qkv_cache(qkv, batch.positions, cos, sin, k_cache, v_cache, batch.slots, h, hk)
         q = qkv[:, : h * hd].view(T, h, hd)
-        if batch.is_prefill:
+        if batch.is_prefill and batch.q_start is not None:
+            o = ops.paged_attention_varlen(q, k_cache, v_cache, batch.block_table, batch.ctx_lens, batch.q_lens,
+                                           batch.q_start, batch.S, self.scale).view(T, h * hd)
+        elif batch.is_prefill:
             o = ops.paged_attention(q.view(batch.B, batch.S, h, hd), k_cache, v_cache, batch.block_table,
                                     batch.ctx_lens, batch.q_lens, self.scale, causal=True).view(T, h * hd)
         else:

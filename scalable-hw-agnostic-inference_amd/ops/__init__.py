@@ -293,6 +293,20 @@ def paged_attention(q, k_cache, v_cache, block_table, kv_lens, q_lens, scale=Non
     return o
 
 
+def paged_attention_varlen(q, k_cache, v_cache, block_table, kv_lens, q_lens, q_start, max_q: int, scale=None,
+                           causal=True):
+    """Packed (varlen) prefill attention over a paged KV cache: q [T, Hq, D] holds every sequence's new tokens
+    back to back (sequence b = rows q_start[b] .. + q_lens[b] - 1), so no padding rows are computed."""
+    D = q.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if not _gpu(q):
+        return ref.paged_attention_varlen(q, k_cache, v_cache, block_table, kv_lens, q_lens, q_start, scale, causal)
+    o = torch.empty(q.shape, dtype=q.dtype, device=q.device)
+    _K().paged_attn_varlen(q, k_cache, v_cache, o, _i32(block_table), _i32(kv_lens), _i32(q_lens), _i32(q_start),
+                           int(max_q), float(scale), bool(causal))
+    return o
+
+
 def decode_splits(batch: int, hkv: int, max_ctx: int) -> int:
     """Split-K factor of the paged decode attention: enough (sequence, KV head, split) workgroups to fill
     the chip (``SHAI_DECODE_WG`` of them, default 512 = two per CU), at most one split per 64-token block."""

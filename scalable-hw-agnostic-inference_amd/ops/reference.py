@@ -238,6 +238,17 @@ def paged_attention(q, k_cache, v_cache, block_table, kv_lens, q_lens, scale=Non
     return out
 
 
+def paged_attention_varlen(q, k_cache, v_cache, block_table, kv_lens, q_lens, q_start, scale=None, causal=True):
+    """q [T, Hq, D] packed (sequence b = rows q_start[b] .. + q_lens[b] - 1)."""
+    out = torch.zeros_like(q)
+    for b in range(block_table.shape[0]):
+        L, ql, q0 = int(kv_lens[b]), int(q_lens[b]), int(q_start[b])
+        k = gather_paged(k_cache, block_table[b], L)[None]
+        v = gather_paged(v_cache, block_table[b], L)[None]
+        out[q0:q0 + ql] = attention(q[None, q0:q0 + ql], k, v, scale=scale, causal=causal, causal_offset=L - ql)[0]
+    return out
+
+
 def decode_attention(q, k_cache, v_cache, block_table, ctx_lens, scale=None):
     B, Hq, D = q.shape
     out = torch.empty_like(q)

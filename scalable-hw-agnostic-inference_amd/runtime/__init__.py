@@ -41,6 +41,7 @@ def lib():
         L.shai_sched_admit.restype = _I
         L.shai_build_decode.argtypes = [_I, _IP, _IP, _IP, _I, _IP, _IP, _IP, _IP]
         L.shai_build_prefill.argtypes = [_I, _I, _IP, _IP, _IP, _IP, _I, _IP, _IP, _IP, _IP, _IP, _IP]
+        L.shai_build_prefill_packed.argtypes = [_I, _IP, _IP, _IP, _IP, _I, _IP, _IP, _IP, _IP, _IP, _IP, _IP]
         _lib = L
     return _lib
 
@@ -144,3 +145,19 @@ def build_prefill(n_cached: Sequence[int], n_new: Sequence[int], tables: Sequenc
     lib().shai_build_prefill(B, S, _ip(nc), _ip(nn), _ip(flat), _ip(offs), max_blocks, _ip(pos), _ip(slots), _ip(lens),
                              _ip(qlens), _ip(bt), _ip(last))
     return pos, slots, lens, qlens, bt, last
+
+
+def build_prefill_packed(n_cached: Sequence[int], n_new: Sequence[int], tables: Sequence[Sequence[int]],
+                         max_blocks: int):
+    """Varlen prefill metadata (no padding rows): positions / slots [T = sum(n_new)], per sequence ctx_lens,
+    q_lens, q_start (first row), last-row index, and the padded block table [B, max_blocks]."""
+    B = len(n_new)
+    nc, nn = np.asarray(n_cached, dtype=np.int32), np.asarray(n_new, dtype=np.int32)
+    T = int(nn.sum())
+    flat, offs = _flatten_tables(tables)
+    pos, slots = np.empty(max(T, 1), dtype=np.int32), np.empty(max(T, 1), dtype=np.int32)
+    lens, qlens, qstart, last = (np.empty(B, dtype=np.int32) for _ in range(4))
+    bt = np.empty((B, max_blocks), dtype=np.int32)
+    lib().shai_build_prefill_packed(B, _ip(nc), _ip(nn), _ip(flat), _ip(offs), max_blocks, _ip(pos), _ip(slots),
+                                    _ip(lens), _ip(qlens), _ip(qstart), _ip(bt), _ip(last))
+    return pos[:T], slots[:T], lens, qlens, qstart, bt, last

@@ -169,3 +169,77 @@ def test_async_lookahead_decode_matches_sync():
         e.step()
         ahead += e._inflight is not None
     assert ahead >= 8
+
+
+def test_packed_prefill_matches_padded_mixed_lengths():
+    """Packed varlen prefill (no [B, S_max] padding rows) gives the padded path's logits and greedy tokens for
+    prompts of very different lengths (3 .. 700 tokens) admitted together."""
+    c = LlamaConfig.tiny()
+    prompts = [[5, 6, 7], [(11 * i) % 500 + 3 for i in range(700)], [(3 * i) % 400 + 9 for i in range(64)],
+               [(5 * i) % 300 + 1 for i in range(129)]]
+    p = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+
+    def run(packed):
+        e = LLMEngine(c, device="cpu", max_num_seqs=4, max_model_len=1024, enable_prefix_caching=False,
+                      packed_prefill=packed, mixed_steps=False)
+        rec = []
+        fwd = e.model.forward
+        e.model.forward = lambda *a, **k: (lambda y: (rec.append(y.float().clone()), y)[1])(fwd(*a, **k))
+        out = [s.output for s in e.generate(prompts, p)]
+        return out, rec[0], e
+    want, l_pad, _ = run(False)
+    got, l_packed, e = run(True)
+    assert got == want
+    torch.testing.assert_close(l_packed, l_pad, rtol=2e-2, atol=2e-2)
+    assert e.stats["prefill_tokens"] == sum(len(q) for q in prompts)   # real tokens, not B x S_max
+
+
+def test_mixed_prefill_decode_steps():
+    """Decode rows join packed prefill steps: a running sequence produces a token in EVERY step while a long
+    prompt is prefilled in chunks (no alternation), and both sequences' greedy tokens equal the unmixed run."""
+    c = LlamaConfig.tiny()
+    long = [(7 * i) % 500 + 3 for i in range(300)]
+    p_long = SamplingParams(max_tokens=5, temperature=0.0, ignore_eos=True)
+    p_short = SamplingParams(max_tokens=30, temperature=0.0, ignore_eos=True)
+
+    def run(mixed):
+        e = LLMEngine(c, device="cpu", max_num_seqs=4, max_model_len=512, enable_prefix_caching=False,
+                      prefill_chunk=64, mixed_steps=mixed, async_decode=False)
+        short = e.add_request([5, 6, 7], p_short)
+        e.step()
+        s = e.add_request(long, p_long)
+        per_step = []
+        while not s.finished:
+            n0 = len(short.output)
+            e.step()
+            per_step.append(len(short.output) - n0)
+        while e.has_work():
+            e.step()
+        return short.output, s.output, per_step
+    s_ref, l_ref, steps_ref = run(False)
+    s_mix, l_mix, steps_mix = run(True)
+    assert l_mix == l_ref and s_mix == s_ref
+    assert all(d == 1 for d in steps_mix), steps_mix          # decoded in every step of the long prefill
+    assert 0 in steps_ref                                      # the alternating engine stalls it
+
+
+def test_sampled_async_matches_sync_with_stops_and_seeds():
+    """temperature > 0 with stop tokens: the async engine's dropped look-ahead rows must not shift any other
+    sequence's sampling noise (counter-based per-sequence uniforms), and SamplingParams.seed makes a request's
+    tokens independent of its batch-mates."""
+    c = LlamaConfig.tiny()
+    prompts = [[3, 17, 99, 250, 7], [5, 6, 7], [400, 12, 13, 14, 15, 16], [9, 9]]
+    mk = lambda a: LLMEngine(c, device="cpu", max_num_seqs=4, max_model_len=256, enable_prefix_caching=False,
+                             seed=5, async_decode=a)
+    sp = SamplingParams(max_tokens=12, temperature=0.9, top_k=30, top_p=0.95, ignore_eos=True)
+    ref = [s.output for s in mk(False).generate(prompts, sp)]
+    stops = [ref[0][3], ref[2][6]]
+    sps = SamplingParams(max_tokens=12, temperature=0.9, top_k=30, top_p=0.95, ignore_eos=True, stop_token_ids=stops)
+    want = [s.output for s in mk(False).generate(prompts, sps)]
+    got = [s.output for s in mk(True).generate(prompts, sps)]
+    assert got == want and any(len(o) < 12 for o in want)
+    seeded = SamplingParams(max_tokens=8, temperature=1.0, top_k=0, top_p=1.0, ignore_eos=True, seed=1234)
+    alone = mk(True).generate([prompts[1]], seeded)[0].output
+    e = mk(True)
+    together = e.generate([prompts[0], prompts[1], prompts[3]], seeded)
+    assert together[1].output == alone

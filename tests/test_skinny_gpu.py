@@ -257,3 +257,52 @@ def test_fused_decode_rope_attention(cuda, D, H, Hk, splits):
     want = ops.decode_attention(qkv2[:, :H * D].reshape(B, H, D), kc2, vc2, bt, lens, num_splits=splits)
     assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
     assert _rel(o[:-1], want.reshape(B, H * D)[:-1]) < 1e-2
+
+
+def test_skinny_fixup_concurrent_streams_and_many_tiles(cuda):
+    """In-kernel split-K fixups running at the same time on two streams (each stream owns its ticket slice),
+    many back-to-back launches with tiles * K groups large (448 tiles x 16 groups), and a graph replayed
+    while eager launches run on another stream: every output equals the separate-fold form bit for bit."""
+    torch.manual_seed(3)
+    shapes = [(64, 28672, 4096, 16), (32, 4096, 14336, 16), (64, 6144, 4096, 8)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    jobs = []
+    for M, N, K, kg in shapes:
+        x = torch.randn(M, K, device=cuda).bfloat16()
+        w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
+        ref = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+        ops.gemm_into(x, w, ref, force_cfg=SKINNY + kg)            # fold form (no tickets)
+        jobs.append((x, w, ref, kg))
+    torch.cuda.synchronize()
+    outs = [[torch.empty_like(j[2]) for _ in range(6)] for j in jobs]
+    for rep in range(6):
+        for si, s in enumerate(streams):
+            with torch.cuda.stream(s):
+                for ji, (x, w, ref, kg) in enumerate(jobs):
+                    if (ji + si) % 2 == 0 or rep % 2 == 0:
+                        ops.gemm_into(x, w, outs[ji][rep], force_cfg=SKINNY_FIX + kg)
+    torch.cuda.synchronize()
+    for ji, (x, w, ref, kg) in enumerate(jobs):
+        for rep in range(6):
+            assert torch.equal(outs[ji][rep], ref), (ji, rep)
+    # a captured graph (its own ticket slice) replayed concurrently with eager launches on another stream
+    x, w, ref, kg = jobs[0]
+    gout = torch.empty_like(ref)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        ops.gemm_into(x, w, gout, force_cfg=SKINNY_FIX + kg)
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(4):
+            ops.gemm_into(x, w, gout, force_cfg=SKINNY_FIX + kg)
+    eout = torch.empty_like(ref)
+    for _ in range(4):
+        with torch.cuda.stream(streams[0]):
+            g.replay()
+        with torch.cuda.stream(streams[1]):
+            for _ in range(4):
+                ops.gemm_into(x, w, eout, force_cfg=SKINNY_FIX + kg)
+    torch.cuda.synchronize()
+    assert torch.equal(gout, ref) and torch.equal(eout, ref)
