@@ -64,6 +64,51 @@ std::string gemm_key(const shai::GemmArgs& g) {
          (lib_supported(g) && !g.residual ? "|lib" : "");
 }
 
+// Prefill GEMMs see a different row count every step (packed varlen prefill: M = tokens in the step), so a
+// tuned choice is also filed under the row-count bucket (64 < M: 96, 128, 192, 256, 384, ...) and reused for
+// every later M of that bucket instead of re-tuning per M.  Convolutions (M from the image geometry) and
+// decode-sized problems (M <= 64) keep exact keys.
+int m_bucket(int M) {
+  if (M <= 64) return M;
+  long p = 64;
+  while (p < M) {
+    if (p + p / 2 >= M) return (int)(p + p / 2);
+    p *= 2;
+  }
+  return (int)p;
+}
+
+std::string gemm_bucket_key(const shai::GemmArgs& g) {
+  if (g.conv || g.M <= 64) return std::string();
+  shai::GemmArgs b = g;
+  b.M = m_bucket(g.M);
+  return gemm_key(b) + "|mbucket";
+}
+
+// exact key first, then the M bucket (a bucket hit is filed under the exact key too).  Caller holds no lock.
+bool lookup_choice(const shai::GemmArgs& g, const std::string& key, Choice* out) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  auto it = g_tuned.find(key);
+  if (it != g_tuned.end()) {
+    *out = it->second;
+    return true;
+  }
+  const std::string bk = gemm_bucket_key(g);
+  if (bk.empty()) return false;
+  it = g_tuned.find(bk);
+  if (it == g_tuned.end()) return false;
+  *out = it->second;
+  g_tuned[key] = it->second;
+  return true;
+}
+
+void store_choice(const shai::GemmArgs& g, const std::string& key, const Choice& c) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  g_tuned[key] = c;
+  const std::string bk = gemm_bucket_key(g);
+  if (!bk.empty() && !g_tuned.count(bk)) g_tuned[bk] = c;
+}
+
 bool autotune_enabled() {
   static const bool on = [] {
     const char* e = getenv("SHAI_GEMM_AUTOTUNE");
@@ -154,9 +199,14 @@ void launch_choice(const shai::GemmArgs& g, const Tensor& like, Choice c) {
     if (!shai::gemm2_cfg_supported(g, c.cfg)) c = fallback_choice(g);
   }
   if (is_skinny(c.cfg)) {
-    launch_skinny_choice(g, like, c.splits, c.cfg == kSkinnyFixCfg);
-    return;
+    if (shai::skinny_supported(g)) {
+      launch_skinny_choice(g, like, c.splits, c.cfg == kSkinnyFixCfg);
+      return;
+    }
+    shai::gemm2_plan(g, &c.cfg, &c.splits);
   }
+  // a choice reused from another row count of the same bucket must still fit this problem
+  if (!shai::gemm2_cfg_supported(g, c.cfg)) c = fallback_choice(g);
   Tensor ws;
   float* wsp = nullptr;
   if (c.splits > 1) {
@@ -224,16 +274,11 @@ Choice tune(const shai::GemmArgs& g_real, const Tensor& like, bool skinny_only =
 void run_skinny(const shai::GemmArgs& g, const Tensor& like) {
   const std::string key = gemm_key(g);
   Choice c{-1, 1};
-  {
-    std::lock_guard<std::mutex> lk(g_tune_mu);
-    auto it = g_tuned.find(key);
-    if (it != g_tuned.end() && is_skinny(it->second.cfg)) c = it->second;
-  }
+  if (!lookup_choice(g, key, &c) || !is_skinny(c.cfg)) c = Choice{-1, 1};
   if (c.cfg < 0) {
     if (!stream_capturing() && autotune_enabled()) {
       c = tune(g, like, true);
-      std::lock_guard<std::mutex> lk(g_tune_mu);
-      g_tuned[key] = c;
+      store_choice(g, key, c);
     } else {
       c = Choice{kSkinnyCfg, shai::skinny_kgroups(g)};
     }
@@ -257,18 +302,13 @@ void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_
   }
   const std::string key = gemm_key(g);
   Choice c{-1, 1};
-  {
-    std::lock_guard<std::mutex> lk(g_tune_mu);
-    auto it = g_tuned.find(key);
-    if (it != g_tuned.end()) c = it->second;
-  }
+  if (!lookup_choice(g, key, &c)) c = Choice{-1, 1};
   if (c.cfg < 0) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     hipStreamIsCapturing(stream(), &cs);
     if (cs == hipStreamCaptureStatusNone && autotune_enabled()) {
       c = tune(g, like);
-      std::lock_guard<std::mutex> lk(g_tune_mu);
-      g_tuned[key] = c;
+      store_choice(g, key, c);
     } else {
       if (shai::skinny_supported(g)) {
         c = Choice{kSkinnyCfg, shai::skinny_kgroups(g)};

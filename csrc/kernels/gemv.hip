@@ -148,8 +148,7 @@ __device__ __forceinline__ int sk_f8_off(int row, int c8) {
 
 template <int MB, bool GLU, int ACT, bool RMS, bool F8>
 __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmArgs p, float* __restrict__ ws,
-                                                                    int kg_steps, unsigned* __restrict__ cnt,
-                                                                    int relaxed_ticket) {
+                                                                    int kg_steps, unsigned* __restrict__ cnt) {
   using G = SkGeom<MB, F8>;
   constexpr int XG = G::XG;
   extern __shared__ __attribute__((aligned(16))) bf16_t sk_smem[];
@@ -306,7 +305,7 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
   if (cnt != nullptr) {
     // ---- split-K fixed up in this launch (no reduce kernel): every K group writes its 64 x MB partial slab
     // (+ MB row sums of squares) write-through (sc1), drains (vmcnt 0 in every wave), joins the workgroup
-    // barrier, then one lane takes a ticket (acq_rel agent-scope atomic on this launch's own ticket slice,
+    // barrier, then one lane takes a ticket (relaxed agent-scope atomic on this launch's own ticket slice,
     // sk_tickets); the workgroup that draws KG-1 re-arms the ticket and reduces the KG slabs with sc1 loads
     // before the fused epilogue.
     // (MI355X_MICROARCH / hip guide "Projection GEMM at M = 256" item 2, write-through form.)
@@ -332,12 +331,15 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
     __syncthreads();
     __shared__ unsigned sk_last;
     if (tid == 0) {
-      // acq_rel at agent scope: this group's slab stores (already write-through) are released before its
-      // arrival counts, and the last arriver's slab reads below are ordered after every arrival it observed
-      // (SHAI_SK_RELAXED_TICKET=1: the relaxed form the write-through slab protocol was first measured with)
-      const unsigned old = relaxed_ticket
-                               ? __hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : __hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      // The hand-off follows the write-through publish form (cdna_hip_programming.md Guideline 16, R1 with
+      // sc1 consumer loads): every slab byte is stored sc1 by its writing wave, EVERY wave drains vmcnt(0)
+      // before the workgroup barrier above, the signal is an agent-scope atomic, and the last arriver reads
+      // the slabs ONLY with sc1 loads into registers (sk_load_wt) -- no other load of this launch touches
+      // bytes another workgroup wrote.  So the ticket is relaxed and the acquire is a wavefront-scope fence
+      // (no instruction: it only keeps the compiler from hoisting the slab loads above the ticket).  An
+      // agent-scope acq_rel here (buffer_wbl2 + buffer_inv of the XCD's L2) measured -7 % Mistral decode.
+      const unsigned old = __hip_atomic_fetch_add(&cnt[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       sk_last = old == (unsigned)(KG - 1);
     }
     __syncthreads();
@@ -518,11 +520,10 @@ static void launch_skinny_mb(const GemmArgs& a, float* ws, int kg, unsigned* cnt
   const int kg_steps = (ksteps + kg - 1) / kg;
   dim3 grid((a.N + SK_BN - 1) / SK_BN, kg), block(SK_WAVES * 64);
   const size_t lds = SkGeom<MB, F8>::LDS;
-  static const int rlx = getenv("SHAI_SK_RELAXED_TICKET") != nullptr && getenv("SHAI_SK_RELAXED_TICKET")[0] == '1';
 #define SK(G, A)                                                                                          \
   do {                                                                                                    \
-    if (a.rms) skinny_gemm_kernel<MB, G, A, true, F8><<<grid, block, lds, s>>>(a, ws, kg_steps, cnt, rlx);  \
-    else skinny_gemm_kernel<MB, G, A, false, F8><<<grid, block, lds, s>>>(a, ws, kg_steps, cnt, rlx);       \
+    if (a.rms) skinny_gemm_kernel<MB, G, A, true, F8><<<grid, block, lds, s>>>(a, ws, kg_steps, cnt);  \
+    else skinny_gemm_kernel<MB, G, A, false, F8><<<grid, block, lds, s>>>(a, ws, kg_steps, cnt);       \
   } while (0)
 #define SK_ACT(G)                                      \
   switch (a.act) {                                     \

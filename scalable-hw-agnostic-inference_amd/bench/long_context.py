@@ -37,15 +37,11 @@ def main(argv=None):
                     mixed_steps=not a.no_mix)
     rng = np.random.default_rng(0)
     params = SamplingParams(temperature=0.7, top_k=50, top_p=0.9, max_tokens=G, ignore_eos=True)
-    bg_params = SamplingParams(temperature=0.7, top_k=50, top_p=0.9, max_tokens=10 ** 6, ignore_eos=True)
-    with torch.inference_mode():
-        eng.warmup_graphs()
-        # warm-up: one short long-prompt pass so GEMM tuning / first-call costs are outside the measurement
-        w = eng.add_request(rng.integers(10, cfg.vocab_size - 10, min(P, 2 * a.chunk)).tolist(),
-                            SamplingParams(max_tokens=2, temperature=0.0, ignore_eos=True))
-        while not w.finished:
-            eng.step()
-        bgs = [eng.add_request(rng.integers(10, cfg.vocab_size - 10, 128).tolist(), bg_params)
+    def scenario():
+        """background decoders streaming -> steady TPOT -> the long prompt arrives -> TTFT / TPOT"""
+        bgs = [eng.add_request(rng.integers(10, cfg.vocab_size - 10, 128).tolist(),
+                               SamplingParams(temperature=0.7, top_k=50, top_p=0.9, max_tokens=10 ** 6,
+                                              ignore_eos=True))
                for _ in range(a.background)]
         while any(not s.output for s in bgs):
             eng.step()
@@ -56,26 +52,36 @@ def main(argv=None):
         for _ in range(32):
             eng.step()
         torch.cuda.synchronize()
-        steady_tpot = (time.perf_counter() - t0) / max(1, (sum(len(s.output) for s in bgs) - n0) / max(1, a.background))
+        steady = (time.perf_counter() - t0) / max(1, (sum(len(s.output) for s in bgs) - n0) / max(1, a.background))
         long = eng.add_request(rng.integers(10, cfg.vocab_size - 10, P).tolist(), params)
         bg0 = sum(len(s.output) for s in bgs)
-        steps_prefill = 0
+        steps = 0
         while long.first_token_time is None:
             eng.step()
-            steps_prefill += 1
-        bg_during = sum(len(s.output) for s in bgs) - bg0
-        ttft = long.first_token_time - long.arrival
+            steps += 1
+        during = sum(len(s.output) for s in bgs) - bg0
         while not long.finished:
             eng.step()
-        tpot = (long.finish_time - long.first_token_time) / max(1, len(long.output) - 1)
+        for s in bgs:   # retire the background sequences
+            s.params.max_tokens = len(s.output) + 1
+        while eng.has_work():
+            eng.step()
         torch.cuda.synchronize()
+        ttft = long.first_token_time - long.arrival
+        tpot = (long.finish_time - long.first_token_time) / max(1, len(long.output) - 1)
+        return ttft, tpot, steady, steps, during, len(long.output)
+
+    with torch.inference_mode():
+        eng.warmup_graphs()
+        scenario()   # warm-up: GEMM tuning of this scenario's row counts, first-call costs
+        ttft, tpot, steady_tpot, steps_prefill, bg_during, n_long = scenario()
     res = {"metric": f"{a.model} long-context: TTFT of a {P}-token prompt beside {a.background} decoding sequences",
            "model": cfg.__class__.__name__ + f"({a.model}, random init, bf16)", "prompt_len": P, "chunk": a.chunk,
            "background_seqs": a.background, "mixed_steps": not a.no_mix,
            "ttft_ms": round(1000 * ttft, 1), "prefill_tok_per_s": round(P / ttft, 1),
            "tpot_ms_long": round(1000 * tpot, 3), "steady_tpot_ms_background": round(1000 * steady_tpot, 3),
            "prefill_steps": steps_prefill, "background_tokens_during_prefill": int(bg_during),
-           "gen_len": len(long.output)}
+           "gen_len": n_long}
     print(json.dumps(res), flush=True)
     return res
 

@@ -91,17 +91,26 @@ def run_flux(rank, world, port):
     from shai_amd.engines.flux import FluxEngine, FluxPipelineConfig
     from shai_amd.parallel import comm
     from shai_amd.parallel.state import TPState, init_distributed, set_tp
+    from shai_amd.models.flux import FluxConfig
     torch.cuda.set_device(0)
     comm.P2P_MAX_BYTES = 8 << 20
+
+    def cfg():  # head dims the GPU flash kernel takes (64 / 128), heads divisible by the TP degree
+        c = FluxPipelineConfig.tiny()
+        c.transformer = FluxConfig(hidden=256, heads=2, head_dim=128, num_layers=2, num_single_layers=2,
+                                   joint_attention_dim=128, pooled_projection_dim=128, axes_dims_rope=(16, 56, 56))
+        c.clip.hidden_size, c.clip.num_attention_heads, c.clip.intermediate_size = 128, 2, 256
+        c.t5.d_model = 128
+        return c
     with torch.inference_mode():
         set_tp(TPState(device=torch.device("cuda", 0)))
-        e1 = FluxEngine(FluxPipelineConfig.tiny(), device="cuda:0")
+        e1 = FluxEngine(cfg(), device="cuda:0")
         ref = e1.generate(["a cat holding a sign"], 3, seed=5, output="tensor").float()
         other = e1.generate(["a cat holding a sign"], 3, seed=6, output="tensor").float()
         del e1
         init_distributed("gloo", tp_size=world, device="cuda")
         assert comm.p2p() is not None
-        e2 = FluxEngine(FluxPipelineConfig.tiny(), device="cuda:0")
+        e2 = FluxEngine(cfg(), device="cuda:0")
         for _ in range(2):   # first call captures the step graph, second replays it
             got = e2.generate(["a cat holding a sign"], 3, seed=5, output="tensor").float()
             rel = ((got - ref).norm() / ref.norm()).item()
