@@ -188,14 +188,21 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
     if constexpr (F8) {
       const int n = n0 + f8row, k = k0 + f8c * 16;
       const uint32_t off = (n < p.N && k < p.K) ? (uint32_t)((long)n * p.ldw + k) : SK_OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (sk_lds_void*)(sw + w * 16 * 32), 16, off, 0, 0, 0);
+      if (p.w_nt) __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (sk_lds_void*)(sw + w * 16 * 32), 16, off, 0, 0, 2);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (sk_lds_void*)(sw + w * 16 * 32), 16, off, 0, 0, 0);
     } else {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int n = n0 + wr[j], k = k0 + wc[j] * 8;
         const uint32_t off = (n < p.N && k < p.K) ? (uint32_t)(((long)n * p.ldw + k) * 2) : SK_OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (sk_lds_void*)(sw + (w * 2 + j) * 8 * SK_BK), 16, off, 0, 0,
-                                                 0);
+        // weights are read once per decode step by one CU: nt (aux 2) shortens issued -> landed
+        // (MI355X_MICROARCH nt-weights); SHAI_SKINNY_NT=0 restores the default policy
+        if (p.w_nt)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (sk_lds_void*)(sw + (w * 2 + j) * 8 * SK_BK), 16, off, 0, 0,
+                                                   2);
+        else
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (sk_lds_void*)(sw + (w * 2 + j) * 8 * SK_BK), 16, off, 0, 0,
+                                                   0);
       }
     }
 #pragma unroll
@@ -544,7 +551,13 @@ static void launch_skinny_mb(const GemmArgs& a, float* ws, int kg, unsigned* cnt
 }
 
 // kg K groups (split-K over workgroups; needs ws of skinny_workspace_bytes_kg, else kg = 1)
-void launch_skinny_kg(const GemmArgs& a, float* ws, int kg, hipStream_t s, bool fixup) {
+void launch_skinny_kg(const GemmArgs& a_in, float* ws, int kg, hipStream_t s, bool fixup) {
+  static const int nt = [] {
+    const char* e = getenv("SHAI_SKINNY_NT");
+    return e ? atoi(e) : 1;
+  }();
+  GemmArgs a = a_in;
+  a.w_nt = nt;
   const int ksteps = (a.K + SK_BK - 1) / SK_BK;
   if (ws == nullptr || kg < 1) kg = 1;
   if (kg > ksteps) kg = ksteps;

@@ -115,6 +115,7 @@ struct GemmArgs {
   float rms_eps;
   // fp8 weights (skinny kernel only): W is e4m3 [N, K] bytes, w_scale[n] fp32 per output row
   const float* w_scale;
+  int w_nt;                 // skinny kernel: weight stream with the nt cache policy (set by its launcher)
 };
 void launch_dequant_fp8_rows(const uint8_t* w8, const float* scale, bf16_t* out, long N, int K, hipStream_t s);
 void launch_gemm(const GemmArgs& a, hipStream_t s);       // v1: register-staged (supports fused GN gather)

@@ -183,7 +183,8 @@ class _DecodeGraph:
 
     NF = 9  # per-row int32 fields before the block table
 
-    def __init__(self, engine: "LLMEngine", Bc: int, cross: bool = False, greedy: bool = False):
+    def __init__(self, engine: "LLMEngine", Bc: int, cross: bool = False, greedy: bool = False,
+                 splits: Optional[int] = None):
         self.Bc = Bc
         dev = engine.device
         mb = engine.max_blocks
@@ -203,7 +204,7 @@ class _DecodeGraph:
         self.host_np = [h.numpy() for h in self.host]
         self.host_ev = [None, None]
         self.flip = 0
-        self.splits = ops.decode_splits(Bc, engine.model.kv_heads_local, engine.max_model_len)
+        self.splits = splits if splits is not None else engine.decode_splits(Bc, 0)
         self.batch = Batch(self.ids, self.pos, self.slots, self.bt, self.lens, None, Bc, 1, False, self.splits)
         self.cross = cross
         self.greedy = greedy
@@ -389,6 +390,19 @@ class LLMEngine:
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "steps": 0, "prefix_hit_tokens": 0}
         self.eos = {cfg.eos_token_id}
 
+    def decode_splits(self, Bc: int, max_ctx: int) -> int:
+        """Split-K factor of the decode attention for a batch whose longest context is ``max_ctx`` tokens:
+        the chip-filling factor for short contexts (``ops.decode_splits``), raised so that no (sequence, KV
+        head) workgroup walks more than ``SHAI_DECODE_SPLIT_TOKENS`` (1024) tokens when a long-context
+        sequence is in the batch (one 16k-token sequence among short ones would otherwise stream its whole
+        cache through 1-2 workgroups per head).  Powers of two: each value is one captured graph."""
+        base = ops.decode_splits(Bc, self.model.kv_heads_local, self.max_model_len)
+        per = int(os.environ.get("SHAI_DECODE_SPLIT_TOKENS", "1024"))
+        need = 1
+        while need < 64 and need * per < max_ctx:
+            need *= 2
+        return max(base, min(need, max(1, (self.max_model_len + KV_BLOCK - 1) // KV_BLOCK)))
+
     def warmup_graphs(self, greedy_too: bool = False) -> int:
         """Capture the decode-step HIP graph of every batch bucket (1, 2, 4, ... >= max_num_seqs) now, so no
         request pays a capture when the running batch first reaches a new bucket.  Returns how many were
@@ -398,9 +412,9 @@ class LLMEngine:
         n, Bc = 0, 1
         while True:
             for greedy in ((False, True) if greedy_too else (False,)):
-                key = (Bc, False, greedy)
+                key = (Bc, False, greedy, self.decode_splits(Bc, 0))
                 if key not in self._graphs:
-                    self._graphs[key] = _DecodeGraph(self, Bc, cross=False, greedy=greedy)
+                    self._graphs[key] = _DecodeGraph(self, Bc, cross=False, greedy=greedy, splits=key[3])
                     n += 1
             if Bc >= self.max_num_seqs:
                 return n
@@ -642,10 +656,11 @@ class LLMEngine:
         Bc = 1 << max(0, math.ceil(math.log2(B)))
         cross = self._cross_tables(seqs) if any(s.cross_blocks for s in seqs) else None
         greedy = all(s.params.temperature <= 0 for s in seqs)
-        key = (Bc, cross is not None, greedy)
+        splits = self.decode_splits(Bc, int(lens.max()) if B else 0)
+        key = (Bc, cross is not None, greedy, splits)
         g = self._graphs.get(key)
         if g is None:
-            g = self._graphs[key] = _DecodeGraph(self, Bc, cross=cross is not None, greedy=greedy)
+            g = self._graphs[key] = _DecodeGraph(self, Bc, cross=cross is not None, greedy=greedy, splits=splits)
         # noise for the token each row samples, at absolute position ctx_before + 1
         u = (seq_uniforms([s.rng_key for s in seqs], [c + 1 for c in ctx_before]) if not greedy
              else np.zeros(B, np.float32))

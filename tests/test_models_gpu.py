@@ -204,3 +204,49 @@ def test_vit_warmup_captures_every_batch(cuda):
     got = eng.logits_u8(x).float().clone()
     assert len(eng._graphs) == 5
     assert torch.allclose(got, eng._forward_u8(x).float(), atol=1e-2, rtol=1e-2)
+
+
+def test_async_decode_batch_shrinks_across_buckets_without_warmup(cuda):
+    """Sequences of different lengths finish at different steps, so the running batch shrinks 4 -> 2 -> 1
+    across graph buckets; nothing is pre-captured, so the async engine captures new buckets (and flips between
+    sampled and all-greedy graphs) while a look-ahead step is in flight.  Tokens must equal the sync engine's."""
+    from shai_amd.engines.llm import LLMEngine, SamplingParams
+    from shai_amd.models.llama import LlamaConfig
+    c = LlamaConfig.tiny()
+    prompts = [[3, 17, 99, 250, 7], [5, 6, 7], [400, 12, 13, 14, 15, 16], [9, 9]]
+    mk = lambda a: LLMEngine(c, device="cuda", max_num_seqs=4, max_model_len=256, enable_prefix_caching=False,
+                             seed=11, async_decode=a)
+    params = [SamplingParams(max_tokens=n, temperature=t, top_k=40, top_p=0.9, ignore_eos=True)
+              for n, t in ((3, 0.8), (6, 0.0), (9, 0.0), (14, 0.0))]
+
+    def run(e):
+        with torch.inference_mode():
+            seqs = [e.add_request(p, sp) for p, sp in zip(prompts, params)]
+            while e.has_work():
+                e.step()
+        return [s.output for s in seqs], e
+    want, _ = run(mk(False))
+    got, e = run(mk(True))
+    assert got == want and [len(o) for o in got] == [3, 6, 9, 14]
+    assert {k[0] for k in e._graphs} >= {1, 2, 4}          # three buckets captured on the fly
+    assert e._inflight is None and e.bm.num_free == e.num_kv_blocks
+
+
+def test_decode_splits_grow_with_long_context(cuda):
+    """A long-context sequence among short ones raises the decode split-K factor (one graph per split count);
+    its tokens match the eager engine."""
+    from shai_amd.engines.llm import LLMEngine, SamplingParams
+    from shai_amd.models.llama import LlamaConfig
+    c = LlamaConfig(vocab_size=1024, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                    num_attention_heads=4, num_key_value_heads=2, head_dim=64, max_position_embeddings=8192)
+    e = LLMEngine(c, device="cuda", max_num_seqs=4, max_model_len=6000, enable_prefix_caching=False, seed=2)
+    assert e.decode_splits(4, 100) < e.decode_splits(4, 5000)
+    prompts = [[(5 * i) % 1000 + 3 for i in range(5000)], [1, 2, 3], [7, 8, 9, 10]]
+    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    with torch.inference_mode():
+        got = [s.output for s in e.generate(prompts, sp)]
+        ref = LLMEngine(c, device="cuda", max_num_seqs=4, max_model_len=6000, enable_prefix_caching=False, seed=2,
+                        use_graphs=False)
+        want = [s.output for s in ref.generate(prompts, sp)]
+    assert got == want
+    assert any(k[3] > e.decode_splits(4, 0) for k in e._graphs)
