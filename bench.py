@@ -356,6 +356,8 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--gen-len", type=int, default=128)
+    ap.add_argument("--llm-model", default="mistral_7b", choices=["mistral_7b", "llama3_8b", "deepseek_r1_distill_70b"],
+                    help="--workload mistral: which Llama-architecture model (BASELINE config 4 is mistral_7b)")
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="tests only: tiny SD2.1 config on the CPU over gloo (launcher / rendezvous / JSON plumbing)")
     ap.add_argument("--tp", type=int, default=None,

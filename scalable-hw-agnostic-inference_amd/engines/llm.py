@@ -121,16 +121,19 @@ def _chain_hash(prev: int, toks: Sequence[int]) -> int:
 
 def sample(logits: torch.Tensor, temps: torch.Tensor, top_k: torch.Tensor, top_p: torch.Tensor,
            gen: Optional[torch.Generator] = None, all_greedy: Optional[bool] = None,
-           uniforms: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+           uniforms: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+           full_vocab: Optional[bool] = None) -> torch.Tensor:
     """Temperature / top-k / top-p sampling; rows with temperature 0 are greedy (an all-greedy batch
     skips the sort / multinomial path entirely).  ``uniforms`` (one U[0,1) per row) makes the draw a
     pure function of its inputs -- what the captured decode step uses (the engine draws them on the host);
     without it they come from ``gen``.  ``out`` (int32) receives the GPU sampler's tokens in place."""
     if all_greedy:
         return logits.float().argmax(-1)
-    if logits.is_cuda and logits.dim() == 2 and os.environ.get("SHAI_TORCH_SAMPLER", "0") != "1":
-        # (top_k <= 0 / > 1024 rows keep their 1024 most likely tokens before the top-p cut)
-        # fused on-device sampler (csrc/kernels/sampling.hip)
+    if full_vocab is None:   # rows without a top-k in (0, 1024] sample over the whole vocabulary (torch path)
+        full_vocab = bool(((top_k <= 0) | (top_k > ops.SAMPLER_MAX_K)).any()) if top_k.numel() else False
+    if (logits.is_cuda and logits.dim() == 2 and not full_vocab
+            and os.environ.get("SHAI_TORCH_SAMPLER", "0") != "1"):
+        # fused on-device sampler (csrc/kernels/sampling.hip): top-k candidates (k <= 1024) -> top-p -> draw
         u = uniforms if uniforms is not None else torch.rand(logits.shape[0], device=logits.device, generator=gen)
         if out is not None:
             ops.sample(logits.contiguous(), temps.float().contiguous(), top_k.int().contiguous(),
@@ -184,8 +187,13 @@ class _DecodeGraph:
     NF = 9  # per-row int32 fields before the block table
 
     def __init__(self, engine: "LLMEngine", Bc: int, cross: bool = False, greedy: bool = False,
-                 splits: Optional[int] = None):
+                 splits: Optional[int] = None, full_vocab: bool = False):
         self.Bc = Bc
+        # full_vocab: some row samples with top_k <= 0 (or > 1024) -- the fused sampler keeps 1024 candidates,
+        # so such steps publish the logits from the graph and sample them exactly over the whole vocabulary
+        # (torch top-k / top-p path, same inverse-CDF rule at the same uniforms) after the replay
+        self.full_vocab = full_vocab
+        self.logits = None
         dev = engine.device
         mb = engine.max_blocks
         self.words = Bc * (self.NF + mb)
@@ -235,10 +243,13 @@ class _DecodeGraph:
         eng = self.engine
         ops.token_feedback(self.ids, self.rowmap, eng.last_tokens)
         logits = eng.model(self.batch, eng.kv)
+        if self.full_vocab:
+            self.logits = logits
+            return
         if self.greedy:
             self.toks.copy_(logits.float().argmax(-1))
-        elif logits.is_cuda:
-            sample(logits, self.temps, self.topk, self.topp, uniforms=self.u, out=self.toks)
+        elif logits.is_cuda:   # full_vocab=False: no host-side inspection of the (captured) top-k values
+            sample(logits, self.temps, self.topk, self.topp, uniforms=self.u, out=self.toks, full_vocab=False)
         else:
             self.toks.copy_(sample(logits, self.temps, self.topk, self.topp, uniforms=self.u))
         eng.last_tokens[:self.Bc].copy_(self.toks)
@@ -297,6 +308,9 @@ class _DecodeGraph:
         else:
             self._program()
         eng = self.engine
+        if self.full_vocab:   # exact full-vocabulary top-k / top-p at the same uniforms, outside the graph
+            self.toks.copy_(sample(self.logits, self.temps, self.topk, self.topp, uniforms=self.u, full_vocab=True))
+            eng.last_tokens[:self.Bc].copy_(self.toks)
         out = eng.tok_host[eng.tok_flip][:Bc]
         eng.tok_flip ^= 1
         out.copy_(self.toks, non_blocking=True)
@@ -657,10 +671,13 @@ class LLMEngine:
         cross = self._cross_tables(seqs) if any(s.cross_blocks for s in seqs) else None
         greedy = all(s.params.temperature <= 0 for s in seqs)
         splits = self.decode_splits(Bc, int(lens.max()) if B else 0)
-        key = (Bc, cross is not None, greedy, splits)
+        full = (not greedy) and any(s.params.temperature > 0 and not 0 < s.params.top_k <= ops.SAMPLER_MAX_K
+                                    for s in seqs)
+        key = (Bc, cross is not None, greedy, splits) + ((True,) if full else ())
         g = self._graphs.get(key)
         if g is None:
-            g = self._graphs[key] = _DecodeGraph(self, Bc, cross=cross is not None, greedy=greedy, splits=splits)
+            g = self._graphs[key] = _DecodeGraph(self, Bc, cross=cross is not None, greedy=greedy, splits=splits,
+                                                 full_vocab=full)
         # noise for the token each row samples, at absolute position ctx_before + 1
         u = (seq_uniforms([s.rng_key for s in seqs], [c + 1 for c in ctx_before]) if not greedy
              else np.zeros(B, np.float32))
@@ -803,7 +820,9 @@ def bench_decode_throughput(args, rank, world):
     assert world % tpd == 0, (world, tpd)
     replicas = world // tpd
     init_distributed(tp_size=tpd)
-    cfg = LlamaConfig.mistral_7b()
+    name = getattr(args, "llm_model", None) or "mistral_7b"
+    cfg = {"mistral_7b": LlamaConfig.mistral_7b, "llama3_8b": LlamaConfig.llama3_8b,
+           "deepseek_r1_distill_70b": LlamaConfig.deepseek_r1_distill_70b}[name]()
     B, P, G = args.batch, args.prompt_len, args.gen_len
     quant = getattr(args, "quantization", None)
     eng = LLMEngine(cfg, device=f"cuda:{torch.cuda.current_device()}", max_num_seqs=max(B, 1),
@@ -833,14 +852,18 @@ def bench_decode_throughput(args, rank, world):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     toks = B * G * args.steps * replicas
+    label = {"mistral_7b": "Mistral-7B", "llama3_8b": "Llama-3-8B",
+             "deepseek_r1_distill_70b": "DeepSeek-R1-Distill-Llama-70B"}[name]
+    hf = {"mistral_7b": "mistralai/Mistral-7B-Instruct-v0.3", "llama3_8b": "meta-llama/Meta-Llama-3-8B-Instruct",
+          "deepseek_r1_distill_70b": "deepseek-ai/DeepSeek-R1-Distill-Llama-70B"}[name]
     return {
-        "metric": ("Mistral-7B output tokens/sec (fp8 e4m3 weights, bf16 activations, continuous batching)"
-                   if quant == "fp8" else "Mistral-7B output tokens/sec (bf16, continuous batching)"),
+        "metric": (f"{label} output tokens/sec (fp8 e4m3 weights, bf16 activations, continuous batching)"
+                   if quant == "fp8" else f"{label} output tokens/sec (bf16, continuous batching)"),
         "value": round(toks / el, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000 * el / args.steps, 2), "higher_is_better": True,
         "scaling": "strong" if replicas == 1 else "weak", "vs_baseline": None, "dtype": "fp8w-bf16a" if quant == "fp8" else "bf16",
         "data": "synthetic prompts, random-init weights",
-        "config": {"model": "mistralai/Mistral-7B-Instruct-v0.3 (architecture)", "global_batch": B * replicas,
+        "config": {"model": f"{hf} (architecture)", "global_batch": B * replicas,
                    "seq_len": P + G, "prompt_len": P, "gen_len": G,
                    "parallelism": (f"dp{replicas}x" if replicas > 1 else "") + f"tp{tpd}"},
         "p50_ttft_ms": round(1000 * float(np.median(ttft)), 2), "p50_tpot_ms": round(1000 * float(np.median(tpot)), 3),

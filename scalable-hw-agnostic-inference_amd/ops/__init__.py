@@ -307,6 +307,11 @@ def paged_attention_varlen(q, k_cache, v_cache, block_table, kv_lens, q_lens, q_
     return o
 
 
+# largest top-k the fused sampler keeps exactly (csrc/kernels/sampling.hip candidate buffer); rows asking for
+# more (or for no top-k at all, top_k <= 0) are sampled over the full vocabulary by the torch path
+SAMPLER_MAX_K = 1024
+
+
 def decode_splits(batch: int, hkv: int, max_ctx: int) -> int:
     """Split-K factor of the paged decode attention: enough (sequence, KV head, split) workgroups to fill
     the chip (``SHAI_DECODE_WG`` of them, default 512 = two per CU), at most one split per 64-token block."""

@@ -233,20 +233,20 @@ def test_async_decode_batch_shrinks_across_buckets_without_warmup(cuda):
 
 
 def test_decode_splits_grow_with_long_context(cuda):
-    """A long-context sequence among short ones raises the decode split-K factor (one graph per split count);
-    its tokens match the eager engine."""
+    """A long-context sequence among many short ones raises the decode split-K factor (one graph per split
+    count); tokens match the eager engine."""
     from shai_amd.engines.llm import LLMEngine, SamplingParams
     from shai_amd.models.llama import LlamaConfig
-    c = LlamaConfig(vocab_size=1024, hidden_size=256, intermediate_size=512, num_hidden_layers=2,
-                    num_attention_heads=4, num_key_value_heads=2, head_dim=64, max_position_embeddings=8192)
-    e = LLMEngine(c, device="cuda", max_num_seqs=4, max_model_len=6000, enable_prefix_caching=False, seed=2)
-    assert e.decode_splits(4, 100) < e.decode_splits(4, 5000)
-    prompts = [[(5 * i) % 1000 + 3 for i in range(5000)], [1, 2, 3], [7, 8, 9, 10]]
-    sp = SamplingParams(max_tokens=6, temperature=0.0, ignore_eos=True)
+    c = LlamaConfig(vocab_size=1024, hidden_size=512, intermediate_size=512, num_hidden_layers=2,
+                    num_attention_heads=8, num_key_value_heads=8, head_dim=64, max_position_embeddings=8192)
+    mk = lambda g: LLMEngine(c, device="cuda", max_num_seqs=32, max_model_len=6000, enable_prefix_caching=False,
+                             seed=2, use_graphs=g)
+    e = mk(True)
+    assert e.decode_splits(32, 100) < e.decode_splits(32, 5000)
+    prompts = [[(5 * i) % 1000 + 3 for i in range(5000)]] + [[1 + j, 2, 3 + j] for j in range(20)]
+    sp = SamplingParams(max_tokens=5, temperature=0.0, ignore_eos=True)
     with torch.inference_mode():
         got = [s.output for s in e.generate(prompts, sp)]
-        ref = LLMEngine(c, device="cuda", max_num_seqs=4, max_model_len=6000, enable_prefix_caching=False, seed=2,
-                        use_graphs=False)
-        want = [s.output for s in ref.generate(prompts, sp)]
+        want = [s.output for s in mk(False).generate(prompts, sp)]
     assert got == want
-    assert any(k[3] > e.decode_splits(4, 0) for k in e._graphs)
+    assert any(k[0] == 32 and k[3] > e.decode_splits(32, 0) for k in e._graphs)

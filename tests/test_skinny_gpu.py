@@ -306,3 +306,20 @@ def test_skinny_fixup_concurrent_streams_and_many_tiles(cuda):
                 ops.gemm_into(x, w, eout, force_cfg=SKINNY_FIX + kg)
     torch.cuda.synchronize()
     assert torch.equal(gout, ref) and torch.equal(eout, ref)
+
+
+def test_sampler_top_k_zero_uses_full_vocabulary(cuda):
+    """top_k <= 0 (no top-k) must sample over the WHOLE vocabulary: with 4096 nearly-equiprobable tokens and a
+    uniform near 1 the inverse-CDF draw lands far beyond the fused sampler's 1024-candidate buffer (the engine
+    routes such rows to the exact full-vocabulary path); top_k = 50 rows stay within their 50."""
+    from shai_amd.engines.llm import sample
+    V, B = 32768, 4
+    logits = torch.full((B, V), -30.0, device=cuda)
+    logits[:, :4096] = -torch.arange(4096, device=cuda).float() * 1e-4   # rank i = token i
+    logits = logits.bfloat16()
+    temps = torch.ones(B, device=cuda)
+    top_k = torch.tensor([0, 0, 50, -1], device=cuda)
+    top_p = torch.ones(B, device=cuda)
+    u = torch.tensor([0.99, 0.5, 0.99, 0.75], device=cuda)
+    toks = sample(logits, temps, top_k, top_p, uniforms=u).cpu().tolist()
+    assert toks[0] > 3000 and 1500 < toks[1] < 2600 and toks[2] < 50 and toks[3] > 2500, toks
