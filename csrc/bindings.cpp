@@ -1074,6 +1074,24 @@ void sched_step(const Tensor& model_out, const Tensor& latents, bool cfg, double
   shai::launch_sched_step(cptr(model_out), mptr(latents), n, cfg, guidance, pred_type, a_t, a_prev, dt, stream());
 }
 
+// step-level batching: every image row of `latents` [B, ...] at its own step; rows_params fp32 [B, 3] =
+// (a_t, a_prev, dt) per row, a_t < 0 = idle row (untouched)
+void sched_step_rows(const Tensor& model_out, const Tensor& latents, bool cfg, double guidance, int64_t pred_type,
+                     const Tensor& rows_params) {
+  check_bf16(model_out, "model_out");
+  check_bf16(latents, "latents");
+  check_f32(rows_params, "rows_params");
+  SHAI_CHECK(model_out.is_contiguous() && latents.is_contiguous() && rows_params.is_contiguous(),
+             "sched_step_rows contiguous");
+  const long n = latents.numel();
+  const long B = latents.size(0);
+  SHAI_CHECK(B > 0 && n % B == 0 && (n / B) % 8 == 0 && model_out.numel() == (cfg ? 2 * n : n) &&
+                 rows_params.numel() == 3 * B,
+             "sched_step_rows sizes");
+  shai::launch_sched_step_rows(cptr(model_out), mptr(latents), n, n / B, cfg, guidance, pred_type,
+                               rows_params.data_ptr<float>(), stream());
+}
+
 void softmax_(const Tensor& x, double scale) {
   check_bf16(x, "x");
   SHAI_CHECK(x.is_contiguous() && x.size(-1) % 8 == 0, "softmax contiguous, D % 8");
@@ -1158,6 +1176,7 @@ TORCH_LIBRARY(shai, m) {
   m.def("sample(Tensor logits, Tensor temps, Tensor top_k, Tensor top_p, Tensor uniforms, Tensor(a!) out) -> ()");
   m.def("rope_qkv_cache(Tensor(a!) qkv, Tensor positions, Tensor cos, Tensor sin, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor slots, int H, int Hkv) -> ()");
   m.def("sched_step(Tensor model_out, Tensor(a!) latents, bool cfg, float guidance, int pred_type, float a_t, float a_prev, float dt) -> ()");
+  m.def("sched_step_rows(Tensor model_out, Tensor(a!) latents, bool cfg, float guidance, int pred_type, Tensor rows_params) -> ()");
   m.def("softmax_(Tensor(a!) x, float scale) -> ()");
   m.def("embedding(Tensor ids, Tensor table, Tensor(a!) out) -> ()");
   m.def("token_feedback(Tensor(a!) ids, Tensor rowmap, Tensor prev) -> ()");
@@ -1190,6 +1209,7 @@ TORCH_LIBRARY_IMPL(shai, CUDA, m) {
   m.impl("sample", &sample);
   m.impl("rope_qkv_cache", &rope_qkv_cache);
   m.impl("sched_step", &sched_step);
+  m.impl("sched_step_rows", &sched_step_rows);
   m.impl("softmax_", &softmax_);
   m.impl("embedding", &embedding);
   m.impl("token_feedback", &token_feedback);

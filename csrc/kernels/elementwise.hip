@@ -132,6 +132,50 @@ void launch_rope_pairs(bf16_t* x, const float* cos, const float* sin, int B, int
 }
 
 // latents [n] (bf16), model_out [2n] when cfg (uncond first) else [n]
+// Per-row variant for step-level batching: latents [B, per_row] where every row (image) is at its own
+// denoising step; rows[3 b .. 3 b + 2] = (a_t, a_prev, dt) of row b, a_t < 0 marks an idle row (left as is).
+__global__ void sched_step_rows_kernel(const bf16_t* __restrict__ mo, bf16_t* __restrict__ lat, long n, long per_row,
+                                       int cfg, float g, int pred, const float* __restrict__ rows) {
+  const long n8 = n >> 3;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const long r = (i << 3) / per_row;
+    const float a_t = rows[3 * r], a_prev = rows[3 * r + 1], dt = rows[3 * r + 2];
+    if (a_t < 0.f) continue;
+    float x[8], e[8];
+    unpack8(reinterpret_cast<const uint4_*>(lat)[i], x);
+    unpack8(reinterpret_cast<const uint4_*>(mo)[i], e);
+    if (cfg) {
+      float c[8];
+      unpack8(reinterpret_cast<const uint4_*>(mo)[i + n8], c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) e[k] = e[k] + g * (c[k] - e[k]);
+    }
+    const float sa = sqrtf(a_t), s1a = sqrtf(1.f - a_t), sp = sqrtf(a_prev), s1p = sqrtf(1.f - a_prev);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (pred == 2) {
+        x[k] = x[k] + dt * e[k];
+      } else {
+        float x0, eps;
+        if (pred == 0) {
+          eps = e[k];
+          x0 = (x[k] - s1a * eps) / sa;
+        } else {
+          x0 = sa * x[k] - s1a * e[k];
+          eps = sa * e[k] + s1a * x[k];
+        }
+        x[k] = sp * x0 + s1p * eps;
+      }
+    }
+    reinterpret_cast<uint4_*>(lat)[i] = pack8(x);
+  }
+}
+
+void launch_sched_step_rows(const bf16_t* mo, bf16_t* lat, long n, long per_row, int cfg, float g, int pred,
+                            const float* rows, hipStream_t s) {
+  sched_step_rows_kernel<<<grid_for(n / 8), 256, 0, s>>>(mo, lat, n, per_row, cfg, g, pred, rows);
+}
+
 __global__ void sched_step_kernel(const bf16_t* __restrict__ mo, bf16_t* __restrict__ lat, long n, int cfg,
                                   float g, int pred, float a_t, float a_prev, float dt) {
   const long n8 = n >> 3;

@@ -70,6 +70,8 @@ void launch_rope_pairs(bf16_t* x, const float* cos, const float* sin, int B, int
 //   eps = eu + g * (ec - eu)  (model_out holds [uncond; cond] halves when cfg)
 //   DDIM (eta=0):  x0 = (x - sqrt(1-a) eps)/sqrt(a) ; x' = sqrt(ap) x0 + sqrt(1-ap) eps
 //   v-prediction variants handled by pred_type (0 eps, 1 v, 2 flow (x' = x + dt * v))
+void launch_sched_step_rows(const bf16_t* mo, bf16_t* lat, long n, long per_row, int cfg, float g, int pred,
+                            const float* rows, hipStream_t s);
 void launch_sched_step(const bf16_t* model_out, bf16_t* latents, long n, int cfg, float guidance, int pred_type,
                        float a_t, float a_prev, float dt, hipStream_t s);
 // Row softmax in-place (fp32 math), bf16 rows of length D

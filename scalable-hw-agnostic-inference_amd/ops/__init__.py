@@ -437,6 +437,15 @@ def sched_step(model_out, latents, cfg: bool, guidance: float, pred_type: int, a
     return latents
 
 
+def sched_step_rows(model_out, latents, cfg: bool, guidance: float, pred_type: int, rows_params):
+    """Per-row fused CFG + scheduler update (step-level batching): latents [B, ...], every row at its own step;
+    rows_params fp32 [B, 3] = (a_t, a_prev, dt) per row, a_t < 0 marks an idle row (left unchanged)."""
+    if not _gpu(latents):
+        return ref.sched_step_rows(model_out, latents, cfg, guidance, pred_type, rows_params)
+    _K().sched_step_rows(model_out, latents, bool(cfg), float(guidance), int(pred_type), rows_params.contiguous())
+    return latents
+
+
 def softmax_(x, scale: float = 1.0):
     if not _gpu(x):
         x.copy_(torch.softmax(x.float() * scale, dim=-1).to(x.dtype))

@@ -338,3 +338,16 @@ def sched_step(model_out, latents, cfg, guidance, pred_type, a_t, a_prev, dt):
         x = math.sqrt(a_prev) * x0 + math.sqrt(1 - a_prev) * eps
     latents.copy_(x.view_as(latents).to(latents.dtype))
     return latents
+
+
+def sched_step_rows(model_out, latents, cfg, guidance, pred_type, rows_params):
+    B = latents.shape[0]
+    mo = model_out.reshape(2 if cfg else 1, B, -1)
+    rp = rows_params.float().cpu().tolist()
+    for b in range(B):
+        a_t, a_prev, dt = rp[b]
+        if a_t < 0:
+            continue
+        out_b = torch.cat([mo[0, b], mo[1, b]]) if cfg else mo[0, b]
+        sched_step(out_b, latents[b], cfg, guidance, pred_type, a_t, a_prev, dt)
+    return latents

@@ -7,14 +7,22 @@ Routes (same paths, request and response JSON):
   GET  /health, /readiness, /metrics, /serve
 Per-request metrics <APP>-counter / <NODEPOOL> / <APP>-latency as in run-sd.py:166-173.
 
-Concurrent /genimage requests with the same step count are batched into one
-CFG-batched UNet pass (``EngineWorker`` dynamic batching); the reference runs
-one pipeline call per request on a shared, unsynchronised pipeline.
+Step-level batching (default, ``SHAI_SD_STEP_BATCHING=1``): requests join the
+running CFG-batched UNet batch at the next denoising-step boundary and leave it
+when their own schedule ends (``engines.diffusion.StepBatcher``), so a request
+never waits for another request's 50 steps; ``SHAI_SD_MAX_BATCH`` (default 32)
+caps the rows.  ``SHAI_SD_STEP_BATCHING=0``: the older request-level batching
+(concurrent requests with the same step count run as one batch,
+``EngineWorker``).  The reference runs one pipeline call per request on a shared,
+unsynchronised pipeline.
 """
 from __future__ import annotations
 
 import os
+import queue
+import threading
 import time
+from concurrent.futures import Future
 from typing import Optional
 
 from .common import METRICS, EngineWorker, ServerEnv, base_app, benchmark, mount_ui, png_b64, run
@@ -30,9 +38,80 @@ def build_engine(env: ServerEnv):
     return StableDiffusionEngine(cfg, device=env.torch_device, model_path=env.model_path)
 
 
-def create_app(engine=None, env: Optional[ServerEnv] = None, max_batch: int = 8, title_suffix: str = ""):
+class StepBatchingWorker:
+    """The engine thread of step-level batching: drains the request queue into the StepBatcher before every
+    denoising step, runs the step, resolves the finished requests' futures.  ``live`` reports progress per
+    step to /health (a hung UNet step turns the replica unhealthy)."""
+
+    def __init__(self, batcher):
+        from ..utils.liveness import Liveness, register
+        self.batcher = batcher
+        self.q: "queue.Queue" = queue.Queue()
+        self.live = register(Liveness())
+        self._futs = {}
+        self.t = threading.Thread(target=self._loop, name="sd-step-engine", daemon=True)
+        self.t.start()
+
+    def submit(self, prompt: str, steps: int, seed: Optional[int] = None) -> Future:
+        f: Future = Future()
+        self.live.work_pending()
+        self.q.put((prompt, int(steps), seed, f))
+        return f
+
+    def call(self, fn, *args):
+        """Run fn on the engine thread (warm-up); returns its result."""
+        f: Future = Future()
+        self.q.put((fn, args, None, f))
+        return f.result()
+
+    def _loop(self):
+        import torch
+        b = self.batcher
+        while True:
+            items = []
+            try:
+                block = not b.has_work()
+                while True:
+                    items.append(self.q.get(block=block))
+                    block = False
+            except queue.Empty:
+                pass
+            for a, steps, seed, f in items:
+                if callable(a):   # engine-thread call
+                    try:
+                        with torch.inference_mode():
+                            f.set_result(a(*steps))
+                    except BaseException as e:  # noqa: BLE001
+                        f.set_exception(e)
+                    continue
+                self._futs[id(b.add(a, steps, seed))] = f
+            if not b.has_work():
+                continue
+            try:
+                with torch.inference_mode():
+                    done = b.step()
+            except BaseException as e:  # noqa: BLE001 -- fail every request in the batch, reset it
+                for f in self._futs.values():
+                    if not f.done():
+                        f.set_exception(e)
+                self._futs.clear()
+                b.waiting, b.active, b.buf = [], [], None
+                continue
+            for r in done:
+                f = self._futs.pop(id(r), None)
+                if f is not None:
+                    f.set_result(r.image)
+            self.live.progress(still_pending=b.has_work() or not self.q.empty())
+
+
+def create_app(engine=None, env: Optional[ServerEnv] = None, max_batch: Optional[int] = None, title_suffix: str = ""):
     env = env or ServerEnv.from_env(app="sd21", num_inference_steps=50)
     engine = engine or build_engine(env)
+    step_batching = os.environ.get("SHAI_SD_STEP_BATCHING", "1") != "0"
+    if max_batch is None:
+        max_batch = int(os.environ.get("SHAI_SD_MAX_BATCH", "32" if step_batching else "8"))
+    if step_batching:
+        return _create_step_app(engine, env, max_batch, title_suffix)
 
     def batch_fn(steps, arg_lists):
         prompts = [a[0] for a in arg_lists]
@@ -80,6 +159,53 @@ def create_app(engine=None, env: Optional[ServerEnv] = None, max_batch: int = 8,
         return {"prompt": prompt, "response": png_b64(img), "latency": latency}
 
     mount_ui(app, f"{env.model_id} on MI355X; pod {env.pod_name}", "/genimage", "{prompt: p}", output="image")
+    return app
+
+
+def _routes(app, env, text2img, run_load):
+    @app.get("/")
+    def read_main():
+        return {"message": "This is" + env.model_id + " pod " + env.pod_name + " in AWS EC2 " + env.device +
+                " instance; try /load/{n_runs}/infer/{n_inf}; /genimage http post with user prompt "}
+
+    @app.get("/load/{n_runs}/infer/{n_inf}")
+    def load(n_runs: int, n_inf: int):
+        t0 = time.time()
+        report = benchmark(n_runs, "stable_diffusion_512", lambda: run_load(n_inf), env.pod_name)
+        METRICS.request_done(env, time.time() - t0)
+        return {"message": "benchmark report:" + report}
+
+    @app.post("/genimage")
+    def generate_image_post(request: dict):
+        prompt = request.get("prompt")
+        img, latency = text2img(prompt)
+        METRICS.request_done(env, float(latency))
+        return {"prompt": prompt, "response": png_b64(img), "latency": latency}
+
+    mount_ui(app, f"{env.model_id} on MI355X; pod {env.pod_name}", "/genimage", "{prompt: p}", output="image")
+
+
+def _create_step_app(engine, env: ServerEnv, max_batch: int, title_suffix: str):
+    from ..engines.diffusion import StepBatcher
+    batcher = StepBatcher(engine, max_batch=max_batch)
+    worker = StepBatchingWorker(batcher)
+
+    # import-time warm-up (run-sd.py:144-146): capture every bucket's UNet-step graph (1, 2, 4, ... max_batch)
+    # so no request pays a capture, then one short request end to end
+    def warm():
+        batcher.warmup()
+    worker.call(warm)
+    worker.submit(WARMUP_PROMPT, min(env.num_inference_steps, 2)).result()
+
+    app = base_app(env, f"{env.model_id} SD2.1{title_suffix}", spaced=False)
+    app.state.engine, app.state.worker, app.state.batcher = engine, worker, batcher
+
+    def text2img(prompt: str, steps: Optional[int] = None):
+        t0 = time.time()
+        img = worker.submit(prompt, int(steps or env.num_inference_steps)).result()
+        return img, str(time.time() - t0)
+
+    _routes(app, env, text2img, lambda n_inf: worker.submit(LOAD_PROMPT, n_inf).result())
     return app
 
 
