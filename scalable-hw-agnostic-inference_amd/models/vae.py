@@ -48,6 +48,8 @@ class VAEConfig:
 
 
 class VAEAttention(nn.Module):
+    SCORE_BYTES = 512 << 20
+
     def __init__(self, ch: int, groups: int):
         super().__init__()
         self.ch = ch
@@ -60,9 +62,23 @@ class VAEAttention(nn.Module):
         h = self.group_norm(x).view(B, H * W, C)
         qkv = self.qkv(h)
         q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
-        s = ops.bmm(q.contiguous(), k.contiguous(), alpha=1.0 / math.sqrt(C))  # [B, HW, HW]
-        ops.softmax_(s)
-        o = ops.bmm(s, v.transpose(1, 2).contiguous())  # [B, HW, C]
+        S = H * W
+        k, vt = k.contiguous(), v.transpose(1, 2).contiguous()
+        # single head, d = 512: score GEMM -> row softmax -> value GEMM, over query-row chunks so the bf16
+        # score buffer stays <= SCORE_BYTES whatever the batch and resolution (768^2: S = 9216 -> 170 MB of
+        # scores per image unchunked)
+        rows = max(64, min(S, self.SCORE_BYTES // max(1, B * S * 2)) // 64 * 64)
+        if rows >= S:
+            s = ops.bmm(q.contiguous(), k, alpha=1.0 / math.sqrt(C))  # [B, S, S]
+            ops.softmax_(s)
+            o = ops.bmm(s, vt)  # [B, S, C]
+        else:
+            o = torch.empty(B, S, C, dtype=x.dtype, device=x.device)
+            for r0 in range(0, S, rows):
+                r1 = min(S, r0 + rows)
+                s = ops.bmm(q[:, r0:r1].contiguous(), k, alpha=1.0 / math.sqrt(C))
+                ops.softmax_(s)
+                o[:, r0:r1] = ops.bmm(s, vt)
         return self.out(o, residual=x.view(B, H * W, C)).view(B, H, W, C)
 
 
