@@ -204,6 +204,8 @@ class StepBatcher:
     membership changes the state rows are gathered into the new bucket's buffers.  Finished rows are decoded
     by the VAE in one batch.  The reference has no cross-request batching at all (run-sd.py:137-142)."""
 
+    VAE_MAX_BATCH = 8
+
     def __init__(self, engine: "StableDiffusionEngine", max_batch: int = 32, guidance_scale: float = 7.5,
                  height: Optional[int] = None, width: Optional[int] = None):
         self.eng = engine
@@ -255,6 +257,15 @@ class StepBatcher:
             if Bc <= self.bucket(self.max_batch) and Bc not in self._graphs:
                 self._buffers(Bc, [(2 * Bc,) + tuple(s) for s in self._kv_shapes1])
                 n += 1
+        # the VAE decodes every batch of finishing rows (1 .. VAE_MAX_BATCH): tune its convs for each size
+        # now, not inside a request
+        z = torch.zeros(1, self.h, self.w, self.eng.cfg.unet.in_channels, dtype=torch.bfloat16,
+                        device=self.eng.device)
+        for k in range(1, min(self.VAE_MAX_BATCH, self.max_batch) + 1):
+            self.eng.vae(z.expand(k, -1, -1, -1).contiguous())
+        # and the text encoder / cross-attention K/V for every admission size
+        for k in range(1, min(self.VAE_MAX_BATCH, self.max_batch) + 1):
+            self.eng.unet.context_kv(self.eng.encode_prompts([""] * k))
         return n
 
     # ------------------------------------------------------------------ one step
@@ -296,11 +307,14 @@ class StepBatcher:
                 fin.append(j)
         if fin:
             with prof.range_("vae_decode"):
-                img = eng.vae(buf.lat[fin[0]:fin[0] + 1] if len(fin) == 1 else buf.lat[torch.tensor(fin, device=dev)])
-            u8 = AutoencoderKLDecoder.to_uint8(img).cpu()
-            now = time.perf_counter()
-            for k, j in enumerate(fin):
-                rows[j].image, rows[j].done, rows[j].finish_time = u8[k], True, now
+                for c0 in range(0, len(fin), self.VAE_MAX_BATCH):   # sizes warmed up by warmup()
+                    part = fin[c0:c0 + self.VAE_MAX_BATCH]
+                    img = eng.vae(buf.lat[part[0]:part[0] + 1] if len(part) == 1
+                                  else buf.lat[torch.tensor(part, device=dev)])
+                    u8 = AutoencoderKLDecoder.to_uint8(img).cpu()
+                    now = time.perf_counter()
+                    for k, j in enumerate(part):
+                        rows[j].image, rows[j].done, rows[j].finish_time = u8[k], True, now
         self.active = rows
         return [rows[j] for j in fin]
 

@@ -9,6 +9,8 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_step_batching_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r3_stepb_tests.log 2>&1 || { tail -30 gpurun_out/r3_stepb_tests.log; exit 1; }
 tail -1 gpurun_out/r3_stepb_tests.log
+timeout -k 10 300 python -u tools/bench_sd_lowk.py > gpurun_out/r3_lowk.log 2>&1 || { tail -20 gpurun_out/r3_lowk.log; exit 1; }
+cat gpurun_out/r3_lowk.log | grep -v amdgpu.ids
 SHAI_SD_MAX_BATCH=16 PORT=8000 HOST=127.0.0.1 NUM_OF_RUNS_INF=50 timeout -k 10 900 python -u -c "import shai_amd.serving.sd as m; m.main()" > gpurun_out/bp_server.log 2>&1 &
 SRV=$!
 ok=0
