@@ -74,6 +74,44 @@ def run_clients(n: int, url: str, duration_s: float, **kw) -> LoadResult:
     return asyncio.run(run_clients_async(n, url, duration_s, **kw))
 
 
+async def run_open_loop_async(rate_rps: float, url: str, duration_s: float, method: str = "GET",
+                              body: Optional[dict] = None, seed: int = 0, timeout_s: float = 600.0) -> LoadResult:
+    """Open-loop load: requests arrive as a Poisson process of ``rate_rps`` for ``duration_s`` seconds whether or
+    not earlier ones have finished (real user traffic, unlike the closed-loop clients whose arrivals align with
+    the server's completions); every request's latency is recorded."""
+    import random
+
+    import httpx
+    res = LoadResult()
+    rng = random.Random(seed)
+    t0 = time.time()
+
+    async def one(client):
+        s = time.time()
+        try:
+            r = await (client.post(url, json=body) if method == "POST" else client.get(url))
+            code = r.status_code
+        except Exception:
+            code = 599
+        res.latencies.append(time.time() - s)
+        res.codes.append(code)
+    async with httpx.AsyncClient(timeout=timeout_s, limits=httpx.Limits(max_connections=1000)) as client:
+        tasks, t = [], t0
+        while True:
+            t += rng.expovariate(rate_rps)
+            if t >= t0 + duration_s:
+                break
+            await asyncio.sleep(max(0.0, t - time.time()))
+            tasks.append(asyncio.create_task(one(client)))
+        await asyncio.gather(*tasks)
+    res.duration_s = time.time() - t0
+    return res
+
+
+def run_open_loop(rate_rps: float, url: str, duration_s: float, **kw) -> LoadResult:
+    return asyncio.run(run_open_loop_async(rate_rps, url, duration_s, **kw))
+
+
 def main():
     ap = argparse.ArgumentParser(description="closed-loop load client (call-model.sh equivalent)")
     ap.add_argument("--endpoint", default=os.environ.get("SERVE_ENDPOINT", "http://127.0.0.1:8000"))
