@@ -109,6 +109,14 @@ void store_choice(const shai::GemmArgs& g, const std::string& key, const Choice&
   if (!bk.empty() && !g_tuned.count(bk)) g_tuned[bk] = c;
 }
 
+bool skinny2_enabled() {  // SHAI_SKINNY2=0 keeps the wide skinny kernel out of the tuner (A/B)
+  static const bool on = [] {
+    const char* e = getenv("SHAI_SKINNY2");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 bool autotune_enabled() {
   static const bool on = [] {
     const char* e = getenv("SHAI_GEMM_AUTOTUNE");
@@ -139,7 +147,9 @@ constexpr int kSkinnyCfg = 1000;
 // same kernel, split-K partials reduced inside the launch by the last-arriving K group of each tile
 // (no separate fold kernel); tuned against the fold form per shape
 constexpr int kSkinnyFixCfg = 1100;
-inline bool is_skinny(int cfg) { return cfg == kSkinnyCfg || cfg == kSkinnyFixCfg; }
+// Choice.cfg of the wide skinny kernel (csrc/kernels/gemv2.hip, 128-row W tiles); Choice.splits = K groups
+constexpr int kSkinny2Cfg = 1200;
+inline bool is_skinny(int cfg) { return cfg == kSkinnyCfg || cfg == kSkinnyFixCfg || cfg == kSkinny2Cfg; }
 
 // Last resort when neither the tuner nor the planner produced a usable config: the highest-numbered
 // config that supports the problem (the v2 128x64 tile supports everything v2 runs).
@@ -153,6 +163,17 @@ bool stream_capturing() {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   hipStreamIsCapturing(stream(), &cs);
   return cs != hipStreamCaptureStatusNone;
+}
+
+void launch_skinny2_choice(const shai::GemmArgs& g, const Tensor& like, int kg) {
+  Tensor ws;
+  float* wsp = nullptr;
+  const size_t bytes = shai::skinny2_workspace_bytes(g, kg);
+  if (bytes > 0) {
+    ws = at::empty({(long)(bytes / sizeof(float))}, like.options().dtype(at::kFloat));
+    wsp = ws.data_ptr<float>();
+  }
+  shai::launch_skinny2(g, wsp, kg, stream());
 }
 
 void launch_skinny_choice(const shai::GemmArgs& g, const Tensor& like, int kg, bool fixup) {
@@ -197,6 +218,10 @@ void launch_choice(const shai::GemmArgs& g, const Tensor& like, Choice c) {
     // falls back to the planner's tile config
     shai::gemm2_plan(g, &c.cfg, &c.splits);
     if (!shai::gemm2_cfg_supported(g, c.cfg)) c = fallback_choice(g);
+  }
+  if (c.cfg == kSkinny2Cfg && shai::skinny2_supported(g)) {
+    launch_skinny2_choice(g, like, c.splits);
+    return;
   }
   if (is_skinny(c.cfg)) {
     if (shai::skinny_supported(g)) {
@@ -243,6 +268,8 @@ Choice tune(const shai::GemmArgs& g_real, const Tensor& like, bool skinny_only =
       cands.push_back({kSkinnyCfg, kg});
       if (kg > 1) cands.push_back({kSkinnyFixCfg, kg});
     }
+  if (shai::skinny2_supported(g) && skinny2_enabled())
+    for (int kg = 1; kg <= shai::skinny2_max_kgroups(g); kg *= 2) cands.push_back({kSkinny2Cfg, kg});
   // residual epilogues are in place (C aliases the residual): timing them into the scratch output is not
   // equivalent, so only bias-or-nothing problems race the library
   if (!skinny_only && lib_enabled() && lib_supported(g_real) && !g_real.residual) cands.push_back({kLibCfg, 1});
@@ -628,12 +655,15 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
   const long a_bytes = (batched ? (long)a.size(0) * a.stride(0) : (long)g.M * g.lda) * 2;
   // tests / tools bypass the tuner: force_cfg = gemm2 config, 1000 = skinny kernel (heuristic K groups),
   // 1000 + kg = skinny kernel with kg K groups (separate fold), 1100 + kg = the same with the in-kernel fixup
+  // 1200 + kg = the wide skinny kernel (gemv2.hip) with kg K groups (in-kernel fixup)
+  const bool force_s2 = force_cfg > kSkinny2Cfg && force_cfg < kLibCfg;
   const bool force_skinny = force_cfg >= kSkinnyCfg && force_cfg != kLibCfg;
-  const bool force_fix = force_cfg > kSkinnyFixCfg && force_cfg != kLibCfg;
-  const int force_kg = force_fix ? (int)(force_cfg - kSkinnyFixCfg)
+  const bool force_fix = force_cfg > kSkinnyFixCfg && force_cfg != kLibCfg && !force_s2;
+  const int force_kg = force_s2 ? (int)(force_cfg - kSkinny2Cfg)
+                       : force_fix ? (int)(force_cfg - kSkinnyFixCfg)
                        : force_cfg > kSkinnyCfg ? (int)(force_cfg - kSkinnyCfg)
                                                 : shai::skinny_kgroups(g);
-  const int force_skcfg = force_fix ? kSkinnyFixCfg : kSkinnyCfg;
+  const int force_skcfg = force_s2 ? kSkinny2Cfg : force_fix ? kSkinnyFixCfg : kSkinnyCfg;
   if (rms_eps >= 0) {
     // RMSNorm(a) folded in (norm gain pre-multiplied into w): fused into the skinny kernel for
     // decode-shaped problems, otherwise an explicit unweighted RMSNorm pass feeds the GEMM.
@@ -668,7 +698,8 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
   }
   if (force_cfg >= 0) {
     if (force_skinny) {
-      SHAI_CHECK(shai::skinny_supported(g) && force_kg >= 1 && force_kg <= 64,
+      SHAI_CHECK((force_s2 ? shai::skinny2_supported(g) : shai::skinny_supported(g)) && force_kg >= 1 &&
+                     force_kg <= 64,
                  "skinny kernel does not support this problem");
       launch_choice(g, a, Choice{force_skcfg, force_kg});
     } else {

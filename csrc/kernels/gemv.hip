@@ -521,6 +521,8 @@ static unsigned* sk_tickets(hipStream_t s, int ntiles) {
   return slice;
 }
 
+unsigned* skinny_ticket_slice(hipStream_t s, int ntiles) { return sk_tickets(s, ntiles); }
+
 template <int MB, bool F8>
 static void launch_skinny_mb(const GemmArgs& a, float* ws, int kg, unsigned* cnt, hipStream_t s) {
   const int ksteps = (a.K + SK_BK - 1) / SK_BK;

@@ -144,6 +144,14 @@ size_t skinny_workspace_bytes(const GemmArgs& a);
 size_t skinny_workspace_bytes_kg(const GemmArgs& a, int kg);
 void launch_skinny(const GemmArgs& a, float* ws, hipStream_t s);
 void launch_skinny_kg(const GemmArgs& a, float* ws, int kg, hipStream_t s, bool fixup = false);
+// this launch's slice of the in-kernel split-K arrival tickets (nullptr: none available -> no fixup)
+unsigned* skinny_ticket_slice(hipStream_t s, int ntiles);
+// skinny2 (gemv2.hip): 128-row W tiles, whole K-step per wave, M <= 64, bf16 weights; split-K always fixed up
+// in the launch (ws of skinny2_workspace_bytes)
+bool skinny2_supported(const GemmArgs& a);
+int skinny2_max_kgroups(const GemmArgs& a);
+size_t skinny2_workspace_bytes(const GemmArgs& a, int kg);
+void launch_skinny2(const GemmArgs& a, float* ws, int kg, hipStream_t s);
 void gemm2_cfg_info(int cfg, int* bm, int* bn);
 
 // ---------------------------------------------------------------- attention

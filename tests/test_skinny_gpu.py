@@ -323,3 +323,57 @@ def test_sampler_top_k_zero_uses_full_vocabulary(cuda):
     u = torch.tensor([0.99, 0.5, 0.99, 0.75], device=cuda)
     toks = sample(logits, temps, top_k, top_p, uniforms=u).cpu().tolist()
     assert toks[0] > 3000 and 1500 < toks[1] < 2600 and toks[2] < 50 and toks[3] > 2500, toks
+
+
+SKINNY2 = 1200
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 6144, 4096), (1, 1088, 512), (48, 4096, 1024), (17, 256, 4160)])
+@pytest.mark.parametrize("kg", [1, 2, 4, 8])
+@pytest.mark.parametrize("rms", [False, True])
+def test_skinny2_kernel(cuda, M, N, K, kg, rms):
+    """Wide skinny kernel (gemv2.hip): 128-row tiles incl. a ragged last tile, M < 64 rows, a K tail, split-K
+    with the in-kernel fixup, folded RMSNorm -- vs fp32 torch."""
+    torch.manual_seed(M * 7 + N + kg)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16()
+    out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    ops.gemm_into(x, w, out, b, force_cfg=SKINNY2 + kg, rms_eps=1e-5 if rms else -1.0)
+    xf = x.float()
+    if rms:
+        xf = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)
+    assert _rel(out, xf @ w.float().t() + b.float()) < 1e-2
+
+
+@pytest.mark.parametrize("kg", [1, 4])
+def test_skinny2_glu_residual_and_graph(cuda, kg):
+    torch.manual_seed(kg)
+    M, N, K = 64, 2048, 4096
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
+    out = torch.empty(M, N // 2, device=cuda, dtype=torch.bfloat16)
+    ops.gemm_into(x, w, out, act="silu", glu=True, force_cfg=SKINNY2 + kg)
+    y = x.float() @ w.float().t()
+    want = y[:, 0::2] * torch.nn.functional.silu(y[:, 1::2])
+    assert _rel(out, want) < 1e-2
+    r = torch.randn(M, N, device=cuda).bfloat16()
+    r0 = r.clone()
+    ops.gemm_into(x, w, r, residual=r, force_cfg=SKINNY2 + kg)          # in place: C aliases the residual
+    assert _rel(r, y + r0.float()) < 1e-2
+    # graph replay re-arms the tickets
+    o2 = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.gemm_into(x, w, o2, force_cfg=SKINNY2 + kg)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(3):
+            ops.gemm_into(x, w, o2, force_cfg=SKINNY2 + kg)
+    for _ in range(3):
+        x.copy_(torch.randn(M, K, device=cuda).bfloat16())
+        g.replay()
+        torch.cuda.synchronize()
+        assert _rel(o2, x.float() @ w.float().t()) < 1e-2

@@ -65,7 +65,7 @@ def bench_decode(rows):
                 it[0] = (it[0] + 1) % ncopy
                 return ws[it[0]]
             res = {}
-            for c in list(range(cfgs)) + [1000]:
+            for c in list(range(cfgs)) + [1000] + [1200 + kg for kg in (1, 2, 4, 8, 16)]:
                 try:
                     res[c] = timeit(lambda: ops.gemm_into(a, nxt(), out, force_cfg=c), iters=48)
                 except Exception as e:  # noqa
@@ -74,7 +74,9 @@ def bench_decode(rows):
             t_tuned = timeit(lambda: ops.linear(a, nxt()), iters=48)
             del ws
             gb = N * K * 2 / 1e9
+            s2 = min((v, k - 1200) for k, v in res.items() if k > 1200 and v == v)
             rows.append(dict(op="decode_gemm", shape=f"{M}x{N}x{K}", skinny_us=res[1000] * 1e6,
+                             skinny2_us=s2[0] * 1e6, skinny2_kg=s2[1], skinny2_TBps=N * K * 2 / 1e9 / s2[0] / 1e3,
                              best_tile_us=min((v for k, v in res.items() if k != 1000), default=float("nan")) * 1e6,
                              tuned_us=t_tuned * 1e6, torch_us=t_t * 1e6,
                              skinny_TBps=gb / res[1000] / 1e3, torch_TBps=gb / t_t / 1e3))
