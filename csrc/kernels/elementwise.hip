@@ -282,6 +282,22 @@ void launch_token_feedback(int* ids, const int* rowmap, const int* prev, int n, 
   token_feedback_kernel<<<(n + 255) / 256, 256, 0, s>>>(ids, rowmap, prev, n);
 }
 
+// Streams `bytes` of a scratch buffer through the cache hierarchy with plain loads (clean lines: no write-back
+// traffic left behind), evicting whatever the Infinity Cache / L2 held.  The sum feeds a store that never
+// happens (the data is zeros), so the loads are not dead.
+__global__ void cache_flush_kernel(const uint4_* __restrict__ buf, long n, unsigned* __restrict__ sink) {
+  unsigned acc = 0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const uint4_ v = buf[i];
+    acc |= v.x | v.y | v.z | v.w;
+  }
+  if (acc == 0xdeadbeefu) sink[0] = acc;
+}
+
+void launch_cache_flush(const void* buf, size_t bytes, unsigned* sink, hipStream_t s) {
+  cache_flush_kernel<<<2048, 256, 0, s>>>(reinterpret_cast<const uint4_*>(buf), (long)(bytes / 16), sink);
+}
+
 void launch_embedding(const int* ids, const bf16_t* table, bf16_t* out, long T, int D, hipStream_t s) {
   embedding_kernel<<<grid_for(T * (D / 8)), 256, 0, s>>>(ids, table, out, T, D);
 }

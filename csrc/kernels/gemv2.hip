@@ -12,7 +12,7 @@
 //   per step, no cross-wave reduction: each wave's accumulators are its final (or split-K partial) outputs.
 // * Per step: W tile 128 x 64 (16 KB) + X tile 64 x 64 (8 KB) by LDS-DMA (buffer_load ... lds, 16 B per
 //   lane, range-checked zero fill for rows >= N / M and K tails), X : W = 1 : 2.  A ring of S2_STAGES
-//   = 3 x 24 KB, so two workgroups fit a CU (four stages of W in flight per CU); counted vmcnt + one
+//   = 3 x 24 KB, so two workgroups fit a CU (four stages of W in flight per CU), or 6 x 24 KB for one; counted vmcnt + one
 //   s_barrier per step.  The weight stream carries the nt cache policy (read once per decode step).
 // * Folded RMSNorm (GemmArgs::rms): every wave accumulates the sum of squares of the X fragments it reads
 //   anyway (the same for all waves: no sharing needed), rstd[m] is applied before the epilogue.
@@ -30,13 +30,14 @@ typedef __attribute__((address_space(3))) void s2_lds_void;
 constexpr int S2_BN = 128;                     // W rows per workgroup
 constexpr int S2_BK = 64;                      // K per step
 constexpr int S2_MB = 64;                      // X rows (two 32-row groups)
-constexpr int S2_STAGES = 3;
 constexpr int S2_W_ELEMS = S2_BN * S2_BK;      // 8192 bf16 = 16 KB
 constexpr int S2_X_ELEMS = S2_MB * S2_BK;      // 4096 bf16 = 8 KB
 constexpr int S2_STAGE = S2_W_ELEMS + S2_X_ELEMS;
 constexpr int S2_PER = 6;                      // DMA wave-instructions per wave per step (4 W + 2 X)
 constexpr uint32_t S2_OOB = 0x80000000u;
-constexpr size_t S2_LDS = (size_t)S2_STAGES * S2_STAGE * 2;  // 72 KB
+// ring depth: 3 stages (72 KB, two workgroups per CU) or 6 stages (144 KB, one workgroup per CU with five
+// steps of W in flight -- for grids of about one tile per CU, e.g. lm_head / gate_up without split-K)
+constexpr size_t s2_lds(int stages) { return (size_t)stages * S2_STAGE * 2; }
 
 __device__ __forceinline__ int s2_swz(int row, int ch) { return row * S2_BK + ((ch ^ ((row >> 1) & 7)) << 3); }
 
@@ -49,6 +50,16 @@ __device__ __forceinline__ void s2_store_wt(__amdgpu_buffer_rsrc_t r, uint32_t o
 }
 __device__ __forceinline__ float s2_load_wt(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 16));
+}
+typedef unsigned s2_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void s2_store4_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, const float* v) {
+  s2_u4 u = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+  __builtin_amdgcn_raw_buffer_store_b128(u, r, (int)off, 0, 16);
+}
+__device__ __forceinline__ void s2_load4_wt(__amdgpu_buffer_rsrc_t r, uint32_t off, float* v) {
+  const s2_u4 u = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = __uint_as_float(u[i]);
 }
 
 template <int N>
@@ -100,7 +111,7 @@ __device__ __forceinline__ void s2_epilogue(const GemmArgs& p, int nbase, int fr
   }
 }
 
-template <bool GLU, int ACT, bool RMS>
+template <bool GLU, int ACT, bool RMS, int S2_STAGES>
 __global__ void __launch_bounds__(256) skinny2_kernel(const GemmArgs p, float* __restrict__ ws, int kg_steps,
                                                       unsigned* __restrict__ cnt) {
   extern __shared__ __attribute__((aligned(16))) bf16_t s2_smem[];
@@ -211,22 +222,21 @@ __global__ void __launch_bounds__(256) skinny2_kernel(const GemmArgs p, float* _
     s2_epilogue<GLU, ACT>(p, nbase, fr, fh, v, rs);
     return;
   }
-  // ---- split-K: slab [tile][kg] = 4 waves x (2 x 16 floats per lane) + 64 row sums of squares; the
-  // write-through publish form (every wave drains, barrier, one relaxed agent-scope ticket; the last arriver
-  // reads only sc1 loads into registers)
-  constexpr int SLAB = 4 * 64 * 32 + S2_MB;
+  // ---- split-K: slab [tile][kg] = 8 chunks of 256 lanes x 4 floats (chunk c = 4 consecutive accumulator
+  // registers of one X group: coalesced 16-byte stores / loads, 4 KB per wave instruction) + 64 row sums of
+  // squares.  The write-through publish form (every wave drains, barrier, one relaxed agent-scope ticket; the
+  // last arriver reads only sc1 loads into registers).
+  constexpr int SLAB = 8 * 256 * 4 + S2_MB;
   const __amdgpu_buffer_rsrc_t rws = s2_rsrc(ws, 0x7fffffffu);
   const uint32_t tile_base = (uint32_t)((long)tile * KG * SLAB * 4);
   const uint32_t my_base = tile_base + (uint32_t)(kg * SLAB * 4);
-  const uint32_t lane_off = (uint32_t)((w * 64 + lane) * 32 * 4);
+  auto chunk_off = [&](int c) { return (uint32_t)((c * 256 + tid) * 16); };
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s2_store_wt(rws, my_base + lane_off + (uint32_t)((j * 16 + r) * 4), v[j][r]);
+  for (int c = 0; c < 8; ++c) s2_store4_wt(rws, my_base + chunk_off(c), &v[c >> 2][(c & 3) * 4]);
   if constexpr (RMS) {
     if (w == 0 && fh == 0) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) s2_store_wt(rws, my_base + (uint32_t)((4 * 64 * 32 + 32 * j + fr) * 4), ss[j]);
+      for (int j = 0; j < 2; ++j) s2_store_wt(rws, my_base + (uint32_t)((8 * 256 * 4 + 32 * j + fr) * 4), ss[j]);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -240,37 +250,37 @@ __global__ void __launch_bounds__(256) skinny2_kernel(const GemmArgs p, float* _
   __syncthreads();
   if (s2_last == 0u) return;
   if (tid == 0) __hip_atomic_store(&cnt[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // sum the KG slabs in K-group order (own slab from registers): the result does not depend on arrival order
+  // sum the KG slabs in K-group order (own slab from registers; two slabs' loads in flight before their
+  // adds): the result does not depend on arrival order
   float sum[2][16], ssum[2] = {0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) sum[j][r] = 0.f;
-  for (int q = 0; q < KG; ++q) {
-    const uint32_t b = tile_base + (uint32_t)(q * SLAB * 4);
-    if (q == kg) {
+  for (int q0 = 0; q0 < KG; q0 += 2) {
+    float t[2][2][16], ts[2][2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+    for (int u = 0; u < 2; ++u) {
+      const int q = q0 + u < KG ? q0 + u : kg;  // past KG / own slot: re-read own slab, dropped below
+      const uint32_t b = tile_base + (uint32_t)(q * SLAB * 4);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sum[j][r] += v[j][r];
+      for (int c = 0; c < 8; ++c) s2_load4_wt(rws, b + chunk_off(c), &t[u][c >> 2][(c & 3) * 4]);
       if constexpr (RMS) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) ssum[j] += ss[j];
+        for (int j = 0; j < 2; ++j) ts[u][j] = s2_load_wt(rws, b + (uint32_t)((8 * 256 * 4 + 32 * j + fr) * 4));
       }
-      continue;
     }
-    float t[2][16];
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int u = 0; u < 2; ++u) {
+      const int q = q0 + u;
+      if (q >= KG) continue;
+      const bool mine = q == kg;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) t[j][r] = s2_load_wt(rws, b + lane_off + (uint32_t)((j * 16 + r) * 4));
+      for (int j = 0; j < 2; ++j) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sum[j][r] += t[j][r];
-    if constexpr (RMS) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) ssum[j] += s2_load_wt(rws, b + (uint32_t)((4 * 64 * 32 + 32 * j + fr) * 4));
+        for (int r = 0; r < 16; ++r) sum[j][r] += mine ? v[j][r] : t[u][j][r];
+        if constexpr (RMS) ssum[j] += mine ? ss[j] : ts[u][j];
+      }
     }
   }
   float rs[2] = {1.f, 1.f};
@@ -297,11 +307,11 @@ int skinny2_max_kgroups(const GemmArgs& a) {
 size_t skinny2_workspace_bytes(const GemmArgs& a, int kg) {
   if (kg <= 1) return 0;
   const size_t tiles = (a.N + S2_BN - 1) / S2_BN;
-  return tiles * kg * (size_t)(4 * 64 * 32 + S2_MB) * sizeof(float);
+  return tiles * kg * (size_t)(8 * 256 * 4 + S2_MB) * sizeof(float);
 }
 
 // kg > 1 needs ws (skinny2_workspace_bytes) and a ticket slice; without either it runs with kg = 1.
-void launch_skinny2(const GemmArgs& a_in, float* ws, int kg, hipStream_t s) {
+void launch_skinny2(const GemmArgs& a_in, float* ws, int kg, bool deep, hipStream_t s) {
   static const int nt = [] {
     const char* e = getenv("SHAI_SKINNY_NT");
     return e ? atoi(e) : 1;
@@ -317,10 +327,15 @@ void launch_skinny2(const GemmArgs& a_in, float* ws, int kg, hipStream_t s) {
   const int kg_steps = (ksteps + kg - 1) / kg;
   kg = (ksteps + kg_steps - 1) / kg_steps;  // no empty K groups (their tickets would never arrive)
   dim3 grid(tiles, kg), block(256);
-#define S2(G, A)                                                                                     \
-  do {                                                                                               \
-    if (a.rms) skinny2_kernel<G, A, true><<<grid, block, S2_LDS, s>>>(a, ws, kg_steps, cnt);         \
-    else skinny2_kernel<G, A, false><<<grid, block, S2_LDS, s>>>(a, ws, kg_steps, cnt);              \
+#define S2R(G, A, ST)                                                                                   \
+  do {                                                                                                  \
+    if (a.rms) skinny2_kernel<G, A, true, ST><<<grid, block, s2_lds(ST), s>>>(a, ws, kg_steps, cnt);    \
+    else skinny2_kernel<G, A, false, ST><<<grid, block, s2_lds(ST), s>>>(a, ws, kg_steps, cnt);         \
+  } while (0)
+#define S2(G, A)              \
+  do {                        \
+    if (deep) S2R(G, A, 6);   \
+    else S2R(G, A, 3);        \
   } while (0)
 #define S2_ACT(G)                                      \
   switch (a.act) {                                     \
@@ -337,6 +352,7 @@ void launch_skinny2(const GemmArgs& a_in, float* ws, int kg, hipStream_t s) {
   }
 #undef S2_ACT
 #undef S2
+#undef S2R
 }
 
 }  // namespace shai

@@ -46,6 +46,7 @@ void launch_groupnorm_stats(const GroupNormArgs& a, hipStream_t s);
 void launch_groupnorm_apply(const GroupNormArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------------- elementwise
+void launch_cache_flush(const void* buf, size_t bytes, unsigned* sink, hipStream_t s);
 // out[t, i] = act(x[t, i]) * x[t, F + i]   (gated MLP, unfused fallback), F = D/2
 void launch_gated_act(const bf16_t* x, bf16_t* out, long rows, int F, long x_stride, int act, int gate_first,
                       hipStream_t s);
@@ -151,7 +152,7 @@ unsigned* skinny_ticket_slice(hipStream_t s, int ntiles);
 bool skinny2_supported(const GemmArgs& a);
 int skinny2_max_kgroups(const GemmArgs& a);
 size_t skinny2_workspace_bytes(const GemmArgs& a, int kg);
-void launch_skinny2(const GemmArgs& a, float* ws, int kg, hipStream_t s);
+void launch_skinny2(const GemmArgs& a, float* ws, int kg, bool deep, hipStream_t s);
 void gemm2_cfg_info(int cfg, int* bm, int* bn);
 
 // ---------------------------------------------------------------- attention

@@ -326,52 +326,55 @@ def test_sampler_top_k_zero_uses_full_vocabulary(cuda):
 
 
 SKINNY2 = 1200
+SKINNY2_DEEP = 1250
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 6144, 4096), (1, 1088, 512), (48, 4096, 1024), (17, 256, 4160)])
 @pytest.mark.parametrize("kg", [1, 2, 4, 8])
 @pytest.mark.parametrize("rms", [False, True])
-def test_skinny2_kernel(cuda, M, N, K, kg, rms):
-    """Wide skinny kernel (gemv2.hip): 128-row tiles incl. a ragged last tile, M < 64 rows, a K tail, split-K
-    with the in-kernel fixup, folded RMSNorm -- vs fp32 torch."""
+@pytest.mark.parametrize("base", [SKINNY2, SKINNY2_DEEP])
+def test_skinny2_kernel(cuda, M, N, K, kg, rms, base):
+    """Wide skinny kernel (gemv2.hip), 3- and 6-stage rings: 128-row tiles incl. a ragged last tile, M < 64
+    rows, a K tail, split-K with the in-kernel fixup, folded RMSNorm -- vs fp32 torch."""
     torch.manual_seed(M * 7 + N + kg)
     x = torch.randn(M, K, device=cuda).bfloat16()
     w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
     b = torch.randn(N, device=cuda).bfloat16()
     out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
-    ops.gemm_into(x, w, out, b, force_cfg=SKINNY2 + kg, rms_eps=1e-5 if rms else -1.0)
+    ops.gemm_into(x, w, out, b, force_cfg=base + kg, rms_eps=1e-5 if rms else -1.0)
     xf = x.float()
     if rms:
         xf = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)
     assert _rel(out, xf @ w.float().t() + b.float()) < 1e-2
 
 
-@pytest.mark.parametrize("kg", [1, 4])
-def test_skinny2_glu_residual_and_graph(cuda, kg):
+@pytest.mark.parametrize("cfg", [SKINNY2 + 1, SKINNY2 + 4, SKINNY2_DEEP + 1, SKINNY2_DEEP + 8])
+def test_skinny2_glu_residual_and_graph(cuda, cfg):
+    kg = cfg % 50
     torch.manual_seed(kg)
     M, N, K = 64, 2048, 4096
     x = torch.randn(M, K, device=cuda).bfloat16()
     w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
     out = torch.empty(M, N // 2, device=cuda, dtype=torch.bfloat16)
-    ops.gemm_into(x, w, out, act="silu", glu=True, force_cfg=SKINNY2 + kg)
+    ops.gemm_into(x, w, out, act="silu", glu=True, force_cfg=cfg)
     y = x.float() @ w.float().t()
     want = y[:, 0::2] * torch.nn.functional.silu(y[:, 1::2])
     assert _rel(out, want) < 1e-2
     r = torch.randn(M, N, device=cuda).bfloat16()
     r0 = r.clone()
-    ops.gemm_into(x, w, r, residual=r, force_cfg=SKINNY2 + kg)          # in place: C aliases the residual
+    ops.gemm_into(x, w, r, residual=r, force_cfg=cfg)          # in place: C aliases the residual
     assert _rel(r, y + r0.float()) < 1e-2
     # graph replay re-arms the tickets
     o2 = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
-        ops.gemm_into(x, w, o2, force_cfg=SKINNY2 + kg)
+        ops.gemm_into(x, w, o2, force_cfg=cfg)
     torch.cuda.current_stream().wait_stream(s)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         for _ in range(3):
-            ops.gemm_into(x, w, o2, force_cfg=SKINNY2 + kg)
+            ops.gemm_into(x, w, o2, force_cfg=cfg)
     for _ in range(3):
         x.copy_(torch.randn(M, K, device=cuda).bfloat16())
         g.replay()

@@ -65,7 +65,10 @@ def bench_decode(rows):
                 it[0] = (it[0] + 1) % ncopy
                 return ws[it[0]]
             res = {}
-            for c in list(range(cfgs)) + [1000] + [1200 + kg for kg in (1, 2, 4, 8, 16)]:
+            kgs = (1, 2, 4, 8, 16)
+            v1 = [1000] + [1100 + kg for kg in kgs[1:]]
+            v2 = [1200 + kg for kg in kgs] + [1250 + kg for kg in kgs]
+            for c in list(range(cfgs)) + v1 + v2:
                 try:
                     res[c] = timeit(lambda: ops.gemm_into(a, nxt(), out, force_cfg=c), iters=48)
                 except Exception as e:  # noqa
@@ -74,12 +77,15 @@ def bench_decode(rows):
             t_tuned = timeit(lambda: ops.linear(a, nxt()), iters=48)
             del ws
             gb = N * K * 2 / 1e9
-            s2 = min((v, k - 1200) for k, v in res.items() if k > 1200 and v == v)
-            rows.append(dict(op="decode_gemm", shape=f"{M}x{N}x{K}", skinny_us=res[1000] * 1e6,
-                             skinny2_us=s2[0] * 1e6, skinny2_kg=s2[1], skinny2_TBps=N * K * 2 / 1e9 / s2[0] / 1e3,
-                             best_tile_us=min((v for k, v in res.items() if k != 1000), default=float("nan")) * 1e6,
-                             tuned_us=t_tuned * 1e6, torch_us=t_t * 1e6,
-                             skinny_TBps=gb / res[1000] / 1e3, torch_TBps=gb / t_t / 1e3))
+
+            def best(keys):
+                return min(((res[k], k) for k in keys if res[k] == res[k]), default=(float("nan"), -1))
+            s1, s2 = best(v1), best(v2)
+            rows.append(dict(op="decode_gemm", shape=f"{M}x{N}x{K}", skinny_us=s1[0] * 1e6, skinny_cfg=s1[1],
+                             skinny2_us=s2[0] * 1e6, skinny2_cfg=s2[1], skinny2_TBps=gb / s2[0] / 1e3,
+                             best_tile_us=min((res[k] for k in range(cfgs)), default=float("nan")) * 1e6,
+                             tuned_us=t_tuned * 1e6, tuned_TBps=gb / t_tuned / 1e3, torch_us=t_t * 1e6,
+                             skinny_TBps=gb / s1[0] / 1e3, torch_TBps=gb / t_t / 1e3))
 
 
 def bench_decode_fp8(rows):
