@@ -1230,7 +1230,70 @@ void dequant_fp8(const Tensor& w8, const Tensor& scale, const Tensor& out) {
                                 w8.size(0), w8.size(1), stream());
 }
 
+// W8A8 fp8 GEMM (gemm_f8.hip): a8 [M, K] / w8 [N, K] float8_e4m3fn, a_scale [M] / w_scale [N] fp32.
+// cfg < 0 picks the tile: 256 x 128 when that still yields >= 256 tiles, else 128 x 128.
+void gemm_f8(const Tensor& a8, const Tensor& w8, const Tensor& a_scale, const Tensor& w_scale, const Tensor& c,
+             const optional<Tensor>& bias, const optional<Tensor>& residual, double res_alpha, int64_t act, bool glu,
+             int64_t cfg) {
+  SHAI_CHECK(a8.is_cuda() && a8.scalar_type() == at::kFloat8_e4m3fn && a8.dim() == 2 && a8.stride(1) == 1,
+             "gemm_f8: a8 must be float8_e4m3fn [M, K] with unit column stride");
+  SHAI_CHECK(w8.is_cuda() && w8.scalar_type() == at::kFloat8_e4m3fn && w8.dim() == 2 && w8.is_contiguous(),
+             "gemm_f8: w8 must be a contiguous float8_e4m3fn [N, K]");
+  check_f32(a_scale, "a_scale");
+  check_f32(w_scale, "w_scale");
+  check_bf16(c, "c");
+  const long M = a8.size(0), K = a8.size(1), N = w8.size(0);
+  SHAI_CHECK(w8.size(1) == K && a_scale.numel() == M && w_scale.numel() == N, "gemm_f8 shapes");
+  SHAI_CHECK(c.dim() == 2 && c.size(0) == M && c.size(1) == (glu ? N / 2 : N) && c.stride(1) == 1, "gemm_f8: c shape");
+  shai::GemmArgs g{};
+  g.M = (int)M;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.lda = a8.stride(0);
+  g.ldw = K;
+  g.C = mptr(c);
+  g.ldc = c.stride(0);
+  g.alpha = 1.f;
+  g.res_alpha = (float)res_alpha;
+  g.act = (int)act;
+  g.glu = glu ? 1 : 0;
+  g.batch = 1;
+  if (bias.has_value()) {
+    check_bf16(*bias, "bias");
+    SHAI_CHECK(bias->numel() == N, "gemm_f8: bias [N]");
+    g.bias = cptr(*bias);
+  }
+  if (residual.has_value()) {
+    check_bf16(*residual, "residual");
+    SHAI_CHECK(residual->dim() == 2 && residual->size(0) == M && residual->size(1) == c.size(1) &&
+                   residual->stride(1) == 1, "gemm_f8: residual shape");
+    g.residual = cptr(*residual);
+    g.ldr = residual->stride(0);
+  }
+  SHAI_CHECK(shai::gemm_f8_supported(g), "gemm_f8: unsupported problem (K, lda multiples of 16; GLU needs N % 4 == 0)");
+  if (cfg < 0) cfg = ((M + 255) / 256) * ((N + 127) / 128) >= 256 ? 0 : 1;
+  shai::launch_gemm_f8(g, reinterpret_cast<const uint8_t*>(a8.data_ptr()), reinterpret_cast<const uint8_t*>(w8.data_ptr()),
+                       a_scale.data_ptr<float>(), w_scale.data_ptr<float>(), (int)cfg, stream());
+}
+
+void quant_rows_fp8(const Tensor& x, const Tensor& out, const Tensor& scale, double rms_eps) {
+  check_bf16(x, "x");
+  SHAI_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "quant_rows_fp8: x [M, K], 16-B aligned rows");
+  SHAI_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat8_e4m3fn && out.dim() == 2 && out.stride(1) == 1 &&
+                 out.size(0) == x.size(0) && out.size(1) == x.size(1) && out.stride(0) % 8 == 0,
+             "quant_rows_fp8: out float8_e4m3fn [M, K]");
+  check_f32(scale, "scale");
+  SHAI_CHECK(scale.numel() == x.size(0), "quant_rows_fp8: scale [M]");
+  SHAI_CHECK(shai::quant_rows_fp8_supported((int)x.size(1)), "quant_rows_fp8: K % 8 == 0");
+  if (x.size(0) == 0) return;
+  shai::launch_quant_rows_fp8(cptr(x), x.stride(0), (int)x.size(0), (int)x.size(1),
+                              reinterpret_cast<uint8_t*>(out.data_ptr()), out.stride(0), scale.data_ptr<float>(),
+                              (float)rms_eps, stream());
+}
+
 TORCH_LIBRARY(shai, m) {
+  m.def("gemm_f8(Tensor a8, Tensor w8, Tensor a_scale, Tensor w_scale, Tensor(a!) c, Tensor? bias, Tensor? residual, float res_alpha, int act, bool glu, int cfg=-1) -> ()");
+  m.def("quant_rows_fp8(Tensor x, Tensor(a!) out, Tensor(b!) scale, float rms_eps) -> ()");
   m.def("rmsnorm(Tensor x, Tensor? w, Tensor(a!) out, Tensor? residual, Tensor(b!)? residual_out, float eps, float w_offset) -> ()");
   m.def("layernorm(Tensor x, Tensor? w, Tensor? b, Tensor(a!) out, Tensor? residual, Tensor(b!)? residual_out, float eps) -> ()");
   m.def("groupnorm_stats(Tensor x, Tensor? x2, Tensor? gamma, Tensor? beta, Tensor(a!) partials, Tensor(b!) scale, Tensor(c!) shift, Tensor(d!)? counters, int G, float eps) -> ()");
@@ -1270,6 +1333,8 @@ TORCH_LIBRARY_IMPL(shai, CUDA, m) {
   m.impl("groupnorm_apply", &groupnorm_apply);
   m.impl("gemm", &gemm);
   m.impl("dequant_fp8", &dequant_fp8);
+  m.impl("gemm_f8", &gemm_f8);
+  m.impl("quant_rows_fp8", &quant_rows_fp8);
   m.impl("layernorm_mod", &layernorm_mod);
   m.impl("qk_norm_rope", &qk_norm_rope);
   m.impl("conv2d", &conv2d);

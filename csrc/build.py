@@ -33,7 +33,8 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 KERNEL_SRCS = ["kernels/norm.hip", "kernels/gemm.hip", "kernels/gemm_lds.hip", "kernels/gemm_pipe.hip", "kernels/gemm_8ph.hip", "kernels/attention.hip", "kernels/attention2.hip", "kernels/elementwise.hip", "kernels/dit.hip",
-               "kernels/sampling.hip", "kernels/gemv.hip", "kernels/gemv2.hip"]
+               "kernels/sampling.hip", "kernels/gemv.hip", "kernels/gemv2.hip",
+               "kernels/gemm_f8.hip"]
 BINDING_SRCS = ["bindings.cpp"]
 RUNTIME_SRCS = ["runtime/block_manager.cpp", "runtime/scheduler.cpp"]
 COMM_SRCS = ["comm/p2p_allreduce.hip"]

@@ -355,7 +355,26 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
   // q stays bf16 (exact: it is the QKV GEMM's bf16 output) for the packed bf16 dot products; the softmax scale
   // is applied to the f32 score
   bf16_t* sQb = reinterpret_cast<bf16_t*>(sQ);
+  // first block's DMA before the q prologue: its HBM latency overlaps the q / RoPE-table loads
+  if (blk0 < blk1) stage(0, blk0);
   const int rpos = fused ? p.positions[b] : 0;
+  // this step's k / v (fused path, last split) loaded now and consumed after the loop, so their latency is hidden
+  const bool new_tok = fused && split == p.num_splits - 1 && p.slots[b] >= 0;
+  float kn0 = 0.f, kn1 = 0.f, kc0 = 0.f, ks0 = 0.f;
+  uint32_t vn_pair = 0u;
+  float vn_one = 0.f;
+  if (new_tok) {
+    const bf16_t* kn = p.knew + (long)b * p.new_bs + (long)hk * D;
+    const bf16_t* vn = p.vnew + (long)b * p.new_bs + (long)hk * D;
+    if (lane < D / 2) {
+      kn0 = bf2f(kn[lane]);
+      kn1 = bf2f(kn[lane + D / 2]);
+      kc0 = p.rope_cos[(long)rpos * (D / 2) + lane];
+      ks0 = p.rope_sin[(long)rpos * (D / 2) + lane];
+    }
+    if constexpr (D == 128) vn_pair = *reinterpret_cast<const uint32_t*>(vn + 2 * lane);
+    else vn_one = bf2f(vn[lane]);
+  }
   if (fused) {  // NeoX RoPE on q (f32 math, bf16 result: what rope_qkv_cache would have stored)
     const bf16_t* qs = p.q + (long)b * p.q_bs + (long)hq * D;
     const float* cp = p.rope_cos + (long)rpos * (D / 2);
@@ -371,7 +390,6 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
   const float sl2 = p.scale * kLog2e;
   float m_run = -INFINITY, l_run = 0.f;
   float o0 = 0.f, o1 = 0.f;  // D=128: this lane's d = 2 lane, 2 lane + 1; D=64: d = lane
-  if (blk0 < blk1) stage(0, blk0);
   // (no barrier here: each wave reads only its own sQ row; the loop's barrier publishes the ring)
   for (int bi = blk0, slot = 0; bi < blk1; ++bi, slot ^= 1) {
     if (bi + 1 < blk1) {
@@ -451,17 +469,14 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
     }
     __builtin_amdgcn_s_barrier();  // every wave is done with this slot before it is refilled (block bi+2)
   }
-  if (fused && split == p.num_splits - 1 && p.slots[b] >= 0) {
+  if (new_tok) {
     // this step's token: roped k (rounded to bf16, as the cache stores it) and v from the QKV rows, one more
     // online-softmax key; wave 0 writes both into the cache (no workgroup of this launch reads that row: the
     // block DMA range-checks it out)
     const int slot_new = p.slots[b];
-    const bf16_t* kn = p.knew + (long)b * p.new_bs + (long)hk * D;
-    const bf16_t* vn = p.vnew + (long)b * p.new_bs + (long)hk * D;
     float kr0 = 0.f, kr1 = 0.f, part = 0.f;
     if (lane < D / 2) {
-      const float x0 = bf2f(kn[lane]), x1 = bf2f(kn[lane + D / 2]);
-      const float c = p.rope_cos[(long)rpos * (D / 2) + lane], sn = p.rope_sin[(long)rpos * (D / 2) + lane];
+      const float x0 = kn0, x1 = kn1, c = kc0, sn = ks0;
       kr0 = bf2f(f2bf(x0 * c - x1 * sn));
       kr1 = bf2f(f2bf(x1 * c + x0 * sn));
       part = kr0 * bf2f(sQb[w * D + lane]) + kr1 * bf2f(sQb[w * D + lane + D / 2]);
@@ -474,11 +489,10 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
     l_run = l_run * alpha + e;
     m_run = m_new;
     if constexpr (D == 128) {
-      const uint32_t vv = *reinterpret_cast<const uint32_t*>(vn + 2 * lane);
-      o0 = o0 * alpha + e * bf2f(vv & 0xffff);
-      o1 = o1 * alpha + e * bf2f(vv >> 16);
+      o0 = o0 * alpha + e * bf2f(vn_pair & 0xffff);
+      o1 = o1 * alpha + e * bf2f(vn_pair >> 16);
     } else {
-      o0 = o0 * alpha + e * bf2f(vn[lane]);
+      o0 = o0 * alpha + e * vn_one;
     }
     if (w == 0) {
       const long dst = (((long)(slot_new >> 6) * p.Hkv + hk) * 64 + (slot_new & 63)) * D;
@@ -488,6 +502,7 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
         kc[dst + lane] = f2bf(kr0);
         kc[dst + lane + D / 2] = f2bf(kr1);
       }
+      const bf16_t* vn = p.vnew + (long)b * p.new_bs + (long)hk * D;
       for (int i = lane; i < D; i += 64) vc[dst + i] = vn[i];
     }
   }

@@ -27,6 +27,9 @@
 //   max yet, the wave takes the exact path for that tile (tile max, O / l rescale, recompute P).  P is
 //   therefore bounded by 2^8 in the fast path (bf16 P, fp32 O / l absorb it), as with v1's deferred max.
 // * Causal masking (with offset), per-batch q / kv lengths, GQA.  Additive bias and paged K/V stay on v1.
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -99,6 +102,10 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
   constexpr int NPI = KT / RPI;          // DMA instructions per operand per tile
   constexpr int NPW = 2 * NPI / 8;       // DMA instructions per wave per tile (K and V)
   constexpr int TILE = 2 * KT * D;       // ring slot: K tile then V tile (elements)
+  // D = 64 (softmax-issue-bound): Q is pre-multiplied by scale * log2(e) and the score accumulators start at
+  // -m (the running max they are computed against), so the fast path's exponent is the raw accumulator --
+  // one v_exp per score, no v_fma.  Costs one bf16 rounding of the scaled Q (|rel| <= 2^-9 per element).
+  constexpr bool PRE = D == 64 && !(EXP & 16);  // EXP & 16: the unscaled form (A/B: SHAI_FLASH2_PRE=0)
   static_assert(NPW >= 1 && (2 * NPI) % 8 == 0, "bad D");
   extern __shared__ __attribute__((aligned(16))) bf16_t f2_smem[];
 
@@ -124,6 +131,13 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
     for (int s = 0; s < NS; ++s) {
       uint4_ v = *reinterpret_cast<const uint4_*>(qp + 16 * s + 8 * fh);
       if (qi >= q_len) v = uint4_{0u, 0u, 0u, 0u};
+      if constexpr (PRE) {  // Q * scale * log2(e): the MFMA then yields exponent-domain scores
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= p.scale * kF2Log2e;
+        v = pack8(f);
+      }
       qf[s] = __builtin_bit_cast(bf16x8a, v);
     }
   }
@@ -167,6 +181,10 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
     for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
   const float sl2 = p.scale * kF2Log2e;
+  // PRE: the max the next tile's scores are computed against (m_run does not change between a tile's QK^T and
+  // its softmax: the previous tile's softmax has already run)
+  auto m_base = [&]() { return m_run == -INFINITY ? 0.f : m_run; };
+  auto s_init = [&]() { return PRE ? -m_base() : 0.f; };
   float16_ sacc[2];
   bf16x8a pf[2][2];
 
@@ -182,7 +200,7 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[kb][r] = 0.f;
+      for (int r = 0; r < 16; ++r) sacc[kb][r] = s_init();
 #pragma unroll
       for (int s = 0; s < NS; ++s) sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][s], qf[s], sacc[kb], 0, 0, 0);
     }
@@ -217,12 +235,18 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
   // P(t) from S(t) with running max m; returns this lane's partial row sum
   // All 32 exponentials first, then the sums and bf16 packs: consuming each v_exp result right away
   // made hipcc pad every one with an s_nop (transcendental-result hazard).
-  auto expo = [&](float m) {
+  // PRE: ADD = false is the fast path (the exponent is the accumulator itself), ADD = true adds m
+  auto expo = [&](float m, auto add) {
+    constexpr bool ADD = decltype(add)::value;
     float e[2][16];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) e[kb][r] = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], sl2, -m));
+      for (int r = 0; r < 16; ++r) {
+        if constexpr (!PRE) e[kb][r] = __builtin_amdgcn_exp2f(fmaf(sacc[kb][r], sl2, -m));
+        else if constexpr (ADD) e[kb][r] = __builtin_amdgcn_exp2f(sacc[kb][r] + m);
+        else e[kb][r] = __builtin_amdgcn_exp2f(sacc[kb][r]);
+      }
     __builtin_amdgcn_sched_barrier(0);
     float ls4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -255,7 +279,7 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
     float ls = 0.f;
     bool slow = __any(m_run == -INFINITY);
     if (!slow) {
-      ls = expo(m_run);
+      ls = expo(m_run, std::false_type{});  // PRE: the accumulators already hold s - m_run
       slow = __any(!(ls <= kF2SumThr));
     }
     if (slow) {  // exact path: tile max, rescale O and l, recompute P
@@ -265,7 +289,9 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) m4[r & 3] = fmaxf(m4[r & 3], sacc[kb][r]);
       float mloc = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
-      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64)) * sl2;  // scale > 0: max commutes with scaling
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      // scale > 0: max commutes with scaling; PRE accumulators are s - base in the exponent domain
+      mloc = PRE ? mloc + m_base() : mloc * sl2;
       const float m_new = fmaxf(m_run, mloc);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);  // 0 when m_run = -inf
@@ -274,8 +300,9 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
       l_run *= alpha;
+      const float shift = m_base() - m_use;  // PRE: exponent = (s - base) + (base - m_new)
       m_run = m_new;
-      ls = expo(m_use);
+      ls = expo(PRE ? shift : m_use, std::true_type{});
     }
     l_run += ls;
   };
@@ -327,7 +354,7 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
       __builtin_amdgcn_sched_barrier(0);
       if (!(EXP & 2) && more) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[0][r] = 0.f;
+        for (int r = 0; r < 16; ++r) sacc[0][r] = s_init();
 #pragma unroll
         for (int s = 0; s < NS; ++s) sacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[0][s], qf[s], sacc[0], 0, 0, 0);
       }
@@ -337,7 +364,7 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
       vreads(t, 1, vr1);
       if (!(EXP & 2) && more) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[1][r] = 0.f;
+        for (int r = 0; r < 16; ++r) sacc[1][r] = s_init();
 #pragma unroll
         for (int s = 0; s < NS; ++s) sacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[1][s], qf[s], sacc[1], 0, 0, 0);
       }
@@ -422,8 +449,17 @@ void launch_flash2(const AttnArgs& a, hipStream_t s) {
     if (a.causal) flash2_kernel<128, true><<<grid, 512, lds, s>>>(a);
     else flash2_kernel<128, false><<<grid, 512, lds, s>>>(a);
   } else {
-    if (a.causal) flash2_kernel<64, true><<<grid, 512, lds, s>>>(a);
-    else flash2_kernel<64, false><<<grid, 512, lds, s>>>(a);
+    static const bool pre = [] {
+      const char* e = getenv("SHAI_FLASH2_PRE");
+      return e == nullptr || atoi(e) != 0;
+    }();
+    if (pre) {
+      if (a.causal) flash2_kernel<64, true><<<grid, 512, lds, s>>>(a);
+      else flash2_kernel<64, false><<<grid, 512, lds, s>>>(a);
+    } else {
+      if (a.causal) flash2_kernel<64, true, 16><<<grid, 512, lds, s>>>(a);
+      else flash2_kernel<64, false, 16><<<grid, 512, lds, s>>>(a);
+    }
   }
 }
 

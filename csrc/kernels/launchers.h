@@ -121,6 +121,16 @@ struct GemmArgs {
   int w_nt;                 // skinny kernel: weight stream with the nt cache policy (set by its launcher)
 };
 void launch_dequant_fp8_rows(const uint8_t* w8, const float* scale, bf16_t* out, long N, int K, hipStream_t s);
+// fp8 e4m3 MFMA GEMM (gemm_f8.hip): C = epi(a_scale[m] w_scale[n] A8 W8^T); A8 / W8 are e4m3 bytes, lda / ldw in
+// bytes; cfg 0 = 256 x 128 tile, 1 = 128 x 128
+bool gemm_f8_supported(const GemmArgs& a);
+void launch_gemm_f8(const GemmArgs& a, const uint8_t* A8, const uint8_t* W8, const float* a_scale,
+                    const float* w_scale, int cfg, hipStream_t s);
+// per-row e4m3 quantisation of a bf16 activation (scale = absmax / 448, times the row's RMSNorm rstd when
+// rms_eps >= 0)
+bool quant_rows_fp8_supported(int K);
+void launch_quant_rows_fp8(const bf16_t* x, long ldx, int M, int K, uint8_t* out, long ldo, float* scale,
+                           float rms_eps, hipStream_t s);
 void launch_gemm(const GemmArgs& a, hipStream_t s);       // v1: register-staged (supports fused GN gather)
 // v2: LDS-DMA staged, tile configs + split-K (ws: fp32 workspace of gemm2_workspace_bytes, may be null)
 void launch_gemm2(const GemmArgs& a, float* ws, hipStream_t s);

@@ -24,7 +24,7 @@ from .reference import (ACT_GELU, ACT_GELU_TANH, ACT_NONE, ACT_QUICK_GELU, ACT_R
 __all__ = [
     "rmsnorm", "layernorm", "groupnorm_stats", "groupnorm_apply", "groupnorm", "linear", "conv2d", "attention",
     "paged_attention", "decode_attention", "kv_write", "rope", "rope_pairs", "gated_act", "bias_act", "sched_step",
-    "softmax_", "embedding", "token_feedback", "decode_attention_rope", "quantize_fp8_rows", "dequant_fp8", "pack_conv_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
+    "softmax_", "embedding", "token_feedback", "decode_attention_rope", "quantize_fp8_rows", "dequant_fp8", "quant_rows_fp8", "gemm_f8", "pack_conv_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
     "ACT_GELU_TANH", "ACT_QUICK_GELU", "ACT_RELU", "decode_splits",
 ]
 
@@ -147,6 +147,39 @@ def dequant_fp8(w8: torch.Tensor, scale: torch.Tensor, dtype=torch.bfloat16) -> 
     return out
 
 
+# fp8 weights on problems of more than 64 rows (prefill): "w8a8" quantises the activation per row on the fly and
+# runs the fp8 MFMA GEMM (gemm_f8.hip); "dequant" widens the weights to bf16 and runs the bf16 GEMMs
+FP8_PREFILL = os.environ.get("SHAI_FP8_PREFILL", "w8a8")
+
+
+def quant_rows_fp8(x: torch.Tensor, rms_eps: Optional[float] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-row e4m3 quantisation of a 2-D bf16 activation: x ~= a8 * scale[:, None] (scale = absmax / 448).
+    With ``rms_eps`` the row's RMSNorm rstd is multiplied into the scale (the consumer's weights carry the
+    folded norm gain), so the product a8 @ w^T * scale is the product of the normalised row."""
+    if not _gpu(x):
+        return ref.quant_rows_fp8(x, rms_eps)
+    M, K = x.shape
+    a8 = torch.empty(M, K, dtype=torch.float8_e4m3fn, device=x.device)
+    scale = torch.empty(M, dtype=torch.float32, device=x.device)
+    _K().quant_rows_fp8(x, a8, scale, float(rms_eps) if rms_eps is not None else -1.0)
+    return a8, scale
+
+
+def gemm_f8(a8: torch.Tensor, w8: torch.Tensor, a_scale: torch.Tensor, w_scale: torch.Tensor,
+            bias: Optional[torch.Tensor] = None, act=None, residual: Optional[torch.Tensor] = None,
+            glu: bool = False, res_alpha: float = 1.0, cfg: int = -1,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """W8A8 GEMM on the fp8 MFMA: act(a_scale[m] * w_scale[n] * a8 @ w8^T + bias) (+ res_alpha * residual),
+    GLU as in ``linear``; bf16 output."""
+    if not _gpu(a8):
+        return ref.gemm_f8(a8, w8, a_scale, w_scale, bias, act, residual, glu, res_alpha)
+    N = w8.shape[0]
+    y = out if out is not None else torch.empty(a8.shape[0], N // 2 if glu else N, dtype=torch.bfloat16,
+                                                device=a8.device)
+    _K().gemm_f8(a8, w8, a_scale, w_scale, y, bias, residual, float(res_alpha), act_id(act), bool(glu), int(cfg))
+    return y
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act=None,
            residual: Optional[torch.Tensor] = None, glu: bool = False, alpha: float = 1.0,
            res_alpha: float = 1.0, rms_eps: Optional[float] = None,
@@ -159,11 +192,21 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     folded into w's columns); on the GPU this is fused into the decode GEMM.
     w_scale: ``w`` is fp8 e4m3 with one fp32 scale per row (``quantize_fp8_rows``).  Decode-shaped
     problems (<= 64 rows) stream the fp8 bytes through the skinny kernel (half the weight
-    traffic); larger ones dequantize to bf16 first and run the bf16 GEMMs.
+    traffic); larger ones run W8A8 on the fp8 MFMA (``FP8_PREFILL``: the activation is quantised per row, with
+    the folded RMSNorm in its row scale) or dequantize to bf16 first and run the bf16 GEMMs.
     """
     if w_scale is not None:
         M = x.numel() // x.shape[-1]
-        if not _gpu(x) or M > 64 or x.shape[-1] % 16 != 0:
+        K = x.shape[-1]
+        if (_gpu(x) and M > 64 and FP8_PREFILL == "w8a8" and alpha == 1.0 and K % 16 == 0
+                and (not glu or w.shape[0] % 4 == 0)):
+            x2 = x.reshape(-1, K) if (x.dim() == 2 or x.is_contiguous()) else x.contiguous().reshape(-1, K)
+            a8, a_scale = quant_rows_fp8(x2, rms_eps)
+            N = w.shape[0] // 2 if glu else w.shape[0]
+            r2 = residual.reshape(-1, N) if residual is not None else None
+            y = gemm_f8(a8, w, a_scale, w_scale, bias, act, r2, glu, res_alpha)
+            return y.view(*x.shape[:-1], N)
+        if not _gpu(x) or M > 64 or K % 16 != 0:
             w = dequant_fp8(w, w_scale)
             w_scale = None
     if not _gpu(x):

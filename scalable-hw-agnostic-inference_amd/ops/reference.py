@@ -351,3 +351,26 @@ def sched_step_rows(model_out, latents, cfg, guidance, pred_type, rows_params):
         out_b = torch.cat([mo[0, b], mo[1, b]]) if cfg else mo[0, b]
         sched_step(out_b, latents[b], cfg, guidance, pred_type, a_t, a_prev, dt)
     return latents
+
+
+def quant_rows_fp8(x, rms_eps=None):
+    """Per-row e4m3 quantisation (scale = absmax / 448, times the RMSNorm rstd with ``rms_eps``)."""
+    xf = x.float()
+    s = (xf.abs().amax(dim=-1) / 448.0).clamp(min=1e-30)
+    a8 = (xf / s[:, None]).clamp(-448.0, 448.0).to(torch.float8_e4m3fn)
+    if rms_eps is not None:
+        s = s * torch.rsqrt(xf.pow(2).mean(-1) + rms_eps)
+    return a8, s
+
+
+def gemm_f8(a8, w8, a_scale, w_scale, bias=None, act=None, residual=None, glu=False, res_alpha=1.0):
+    y = (a8.float() @ w8.float().t()) * a_scale.float()[:, None] * w_scale.float()[None, :]
+    if bias is not None:
+        y = y + bias.float()
+    if glu:
+        y = y[:, 0::2] * apply_act(y[:, 1::2], act)
+    else:
+        y = apply_act(y, act)
+    if residual is not None:
+        y = y + res_alpha * residual.float()
+    return y.to(torch.bfloat16)

@@ -260,6 +260,27 @@ def test_flash2_varlen_strided_gqa(cuda, D, causal):
         close(o[b, :n], orf[b, :n], 2e-2)
 
 
+@pytest.mark.parametrize("causal", [False, True])
+def test_flash2_d64_long_spikes_varlen(cuda, causal):
+    """flash2 at D = 64 (Sq, Skv >= 2048: the SD2.1 self-attention kernel, pre-scaled Q and max-folded score
+    accumulators): spikes in the first tile and past the fast-path bound, a moderate max growth, per-batch
+    lengths with a partial last query tile, GQA 2:1."""
+    torch.manual_seed(16)
+    B, S, Hq, Hkv, D = 2, 2200, 4, 2, 64
+    q, k, v = rnd(B, S, Hq, D), rnd(B, S, Hkv, D), rnd(B, S, Hkv, D)
+    k[:, 3] = q[:, 700, :Hkv] * 3
+    k[:, 1500] = q[:, 10, :Hkv] * 5
+    k[:, S - 2] = q[:, S - 300, :Hkv] * 5
+    k[:, 1025] = q[:, 600, :Hkv] * 0.7
+    kl = torch.tensor([2200, 2090], device="cuda", dtype=torch.int32)
+    ql = kl.clone() if causal else None
+    o = ops.attention(q, k, v, causal=causal, kv_lens=kl, q_lens=ql)
+    orf = ref.attention(q, k, v, 1 / math.sqrt(D), causal, 0, kl, ql)
+    for b in range(B):
+        n = int((ql if ql is not None else torch.full_like(kl, S))[b])
+        close(o[b, :n], orf[b, :n], 2e-2)
+
+
 def test_flash2_causal_offset_chunk(cuda):
     """Chunked-prefill shape: 600 new queries attending causally over 1500 keys (offset 900)."""
     torch.manual_seed(15)

@@ -166,7 +166,8 @@ def bench_conv(rows):
 
 
 def bench_attn(rows):
-    shapes = [(8, 4096, 4096, 5, 64), (8, 1024, 1024, 10, 64), (8, 4096, 77, 5, 64), (1, 4608, 4608, 24, 128),
+    shapes = [(64, 4096, 4096, 5, 64), (8, 4096, 4096, 5, 64), (8, 1024, 1024, 10, 64), (8, 4096, 77, 5, 64),
+              (1, 4608, 4608, 24, 128),
               (4, 2048, 2048, 32, 128), (16, 197, 197, 12, 64)]
     for B, Sq, Skv, H, D in shapes:
         q, k, v = rnd(B, Sq, H, D), rnd(B, Skv, H, D), rnd(B, Skv, H, D)
@@ -195,6 +196,24 @@ def bench_norm(rows):
         rows.append(dict(op="rmsnorm", shape=f"{T}x{D}", shai_us=t_s * 1e6, shai_GBps=by / t_s / 1e9))
 
 
+def bench_f8(rows):
+    """W8A8 fp8 MFMA GEMM (both tile configs, quantisation excluded / included) vs the bf16 GEMM on LLM prefill
+    shapes; TF/s on the true FLOP count."""
+    for M, N, K in [(4096, 4096, 4096), (8192, 8192, 8192), (4096, 28672, 4096), (4096, 4096, 14336),
+                    (2048, 6144, 4096)]:
+        x = rnd(M, K)
+        w = rnd(N, K) / K ** 0.5
+        a8, a_s = ops.quant_rows_fp8(x)
+        w8, w_s = ops.quantize_fp8_rows(w)
+        f = 2 * M * N * K
+        t = {c: timeit(lambda: ops.gemm_f8(a8, w8, a_s, w_s, cfg=c)) for c in (0, 1)}
+        t_q = timeit(lambda: ops.linear(x, w8, w_scale=w_s))
+        t_b = timeit(lambda: ops.linear(x, w))
+        rows.append(dict(op="gemm_f8", shape=f"{M}x{N}x{K}", f8_256x128_us=t[0] * 1e6, f8_128x128_us=t[1] * 1e6,
+                         f8_TFs=f / min(t.values()) / 1e12, w8a8_linear_TFs=f / t_q / 1e12,
+                         bf16_TFs=f / t_b / 1e12))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="gemm,conv,attn,norm")
@@ -204,7 +223,7 @@ def main():
     with torch.inference_mode():
         for name in a.only.split(","):
             {"gemm": bench_gemm, "conv": bench_conv, "attn": bench_attn, "norm": bench_norm,
-             "decode": bench_decode, "decode_fp8": bench_decode_fp8, "sdgemm": bench_sdgemm}[name](rows)
+             "decode": bench_decode, "decode_fp8": bench_decode_fp8, "sdgemm": bench_sdgemm, "f8": bench_f8}[name](rows)
     for r in rows:
         print("  ".join(f"{k}={v:.1f}" if isinstance(v, float) else f"{k}={v}" for k, v in r.items()), flush=True)
     if a.json:
