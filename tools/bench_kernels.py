@@ -206,10 +206,11 @@ def bench_f8(rows):
         a8, a_s = ops.quant_rows_fp8(x)
         w8, w_s = ops.quantize_fp8_rows(w)
         f = 2 * M * N * K
-        t = {c: timeit(lambda: ops.gemm_f8(a8, w8, a_s, w_s, cfg=c)) for c in (0, 1)}
+        t = {c: timeit(lambda: ops.gemm_f8(a8, w8, a_s, w_s, cfg=c)) for c in (0, 1, 2)}
         t_q = timeit(lambda: ops.linear(x, w8, w_scale=w_s))
         t_b = timeit(lambda: ops.linear(x, w))
         rows.append(dict(op="gemm_f8", shape=f"{M}x{N}x{K}", f8_256x128_us=t[0] * 1e6, f8_128x128_us=t[1] * 1e6,
+                         f8_256x256_us=t[2] * 1e6,
                          f8_TFs=f / min(t.values()) / 1e12, w8a8_linear_TFs=f / t_q / 1e12,
                          bf16_TFs=f / t_b / 1e12))
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Full GPU test suite, then the given bench workloads (default: sd21 + mistral).  Each step has its own
 # time limit; the script stops at the first failing step.
-#   bash tools/gpu_check.sh [workload ...]
+#   bash tools/gpu_runs/gpu_check.sh [workload ...]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp

@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel trace of one bench step (after warm-up); markdown summary -> gpurun_out/prof_<workload>.md
-# usage: bash tools/gpu_prof.sh <sd21|mistral|flux|mllama> [extra bench.py args]
+# usage: bash tools/gpu_runs/gpu_prof.sh <sd21|mistral|flux|mllama> [extra bench.py args]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp

@@ -2,8 +2,8 @@
 # Re-measure the tuning-cache entries selected by a Python predicate over (key, cfg, splits), then run
 # the given bench workloads so those shapes are raced again against every config (including ones added
 # since they were measured).  Result: gpurun_out/tune_subset.json (full cache) -> review, then merge.
-#   bash tools/gpu_retune_subset.sh '<predicate>' "<bench args>" ["<bench args>" ...]
-# e.g. bash tools/gpu_retune_subset.sh 'cfg in (9, 10)' "--workload sd21 --steps 1 --warmup 1 --latency-runs 0"
+#   bash tools/gpu_runs/gpu_retune_subset.sh '<predicate>' "<bench args>" ["<bench args>" ...]
+# e.g. bash tools/gpu_runs/gpu_retune_subset.sh 'cfg in (9, 10)' "--workload sd21 --steps 1 --warmup 1 --latency-runs 0"
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp

@@ -9,7 +9,7 @@ timeout -k 10 600 python -u -m pytest tests/test_mllama_gpu.py tests/test_kernel
 rc=$?
 tail -4 gpurun_out/pytest_s2.log
 [ $rc -eq 0 ] || exit $rc
-bash tools/gpu_prof.sh sd21 || exit $?
+bash tools/gpu_runs/gpu_prof.sh sd21 || exit $?
 timeout -k 10 600 python -u bench.py --workload mllama --steps 1 --warmup 1 --latency-runs 2 --batch 8 \
   > gpurun_out/bench_mllama.log 2>&1
 rc=$?
