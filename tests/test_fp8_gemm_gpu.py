@@ -36,7 +36,7 @@ def test_quant_rows_fp8_matches_reference(cuda, M, K, rms):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 512, 512), (300, 1000, 4096), (4096, 4096, 4096), (129, 128, 208)])
-@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("cfg", [0, 1, 2])
 def test_gemm_f8_matches_dequantized_fp32(cuda, M, N, K, cfg):
     """Exact fp8 operands (quantised once), fp32 product of the same codes: only accumulation order differs."""
     torch.manual_seed(M * 3 + N + K)
