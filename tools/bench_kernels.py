@@ -215,6 +215,36 @@ def bench_f8(rows):
                          bf16_TFs=f / t_b / 1e12))
 
 
+def bench_dattn(rows):
+    """Paged decode attention (Mistral-7B layer: 32 q heads, 8 KV heads, D 128), fused RoPE + KV write, per
+    split count and context length; KV bytes read / time."""
+    import math
+    h, hk, D = 32, 8, 128
+    for B, ctx in [(64, 192), (64, 1024), (16, 4096), (1, 16384)]:
+        nblk = (ctx + 63) // 64
+        pool = B * nblk + 8
+        kc = rnd(pool, hk, 64, D)
+        vc = rnd(pool, hk, 64, D)
+        bt = torch.randperm(pool, device="cuda")[:B * nblk].view(B, nblk).int()
+        ctx_l = torch.full((B,), ctx, device="cuda", dtype=torch.int32)
+        pos = ctx_l - 1
+        cos, sin = torch.rand(ctx + 1, D // 2, device="cuda"), torch.rand(ctx + 1, D // 2, device="cuda")
+        slots = (bt[:, (ctx - 1) // 64] * 64 + (ctx - 1) % 64).int()
+        qkv = rnd(B, (h + 2 * hk) * D)
+        gb = B * hk * (ctx - 1) * D * 2 * 2 / 1e9
+        r = dict(op="decode_attn", shape=f"B{B} ctx{ctx}")
+        for sp in (1, 2, 4, 8, 16):
+            if sp > nblk:
+                continue
+            t = timeit(lambda: ops.decode_attention_rope(qkv, kc, vc, bt, ctx_l, pos, cos, sin, slots, h, hk,
+                                                         num_splits=sp), iters=48)
+            r[f"s{sp}_us"] = t * 1e6
+        best = min(v for k, v in r.items() if k.endswith("_us"))
+        r["best_GBps"] = gb / (best / 1e6)
+        r["auto_splits"] = ops.decode_splits(B, hk, ctx)
+        rows.append(r)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="gemm,conv,attn,norm")
@@ -224,7 +254,8 @@ def main():
     with torch.inference_mode():
         for name in a.only.split(","):
             {"gemm": bench_gemm, "conv": bench_conv, "attn": bench_attn, "norm": bench_norm,
-             "decode": bench_decode, "decode_fp8": bench_decode_fp8, "sdgemm": bench_sdgemm, "f8": bench_f8}[name](rows)
+             "decode": bench_decode, "decode_fp8": bench_decode_fp8, "sdgemm": bench_sdgemm, "f8": bench_f8,
+             "dattn": bench_dattn}[name](rows)
     for r in rows:
         print("  ".join(f"{k}={v:.1f}" if isinstance(v, float) else f"{k}={v}" for k, v in r.items()), flush=True)
     if a.json:
