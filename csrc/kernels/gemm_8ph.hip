@@ -73,11 +73,36 @@ __device__ __forceinline__ void g4_glds(__amdgpu_buffer_rsrc_t r, bf16_t* lds, u
 //   bit 1: static priority (waves 4-7 at prio 1 for the whole loop) instead of per-segment setprio
 //   bit 2: LDS-DMA issued over phases 0-1 (halves) instead of over phases 0-2 (quarter, half, quarter)
 //   bit 3: persistent tile loop with the next tile's first K-tile prefetched under the epilogue
+//   bit 4: wide epilogue (W rows permuted in pairs of 16-column MFMA blocks, see g4_wperm: 16-B stores)
 // Phase p of a K-tile issues the DMA instructions g in [G_p, G_{p+1}) of the next tile.
 template <int VAR, int GT>
 struct G4Sched {
   static constexpr int G1 = (VAR & 4) ? (GT + 1) / 2 : GT / 4, G2 = (VAR & 4) ? GT : (3 * GT) / 4;
 };
+
+// Wide epilogue.  A lane of a v_mfma_f32_16x16x32 block owns 4 consecutive output columns (4 fq .. 4 fq + 3),
+// so the plain epilogue issues one 8-byte store per block and row: 40 store instructions per lane per tile
+// at BN = 320, and a low-K tile (K = 320: 5 K-steps) spends about as long in those stores as in its MFMAs
+// (stores are priced per wave-instruction, MI355X_MICROARCH "attention epilogue store tail").  The W tile
+// is therefore staged with its rows permuted inside each pair of 16-column blocks (2q, 2q + 1) of a wave:
+// LDS row 16 (2q + h) + n holds output column 32 q + 8 (n >> 2) + 4 h + (n & 3).  The MFMA is unchanged;
+// lane fq of block 2q + h now owns columns 32 q + 8 fq + 4 h .. + 3, i.e. the pair gives the lane 8
+// consecutive columns: one 16-byte store (bias / residual loads widen the same way).  A fifth block
+// (BN = 320) keeps the identity mapping.  The permutation lives only in the DMA source row address.
+template <int BN>
+__device__ __forceinline__ int g4_wperm(int r) {  // LDS row of the W tile -> tile-local output column
+  constexpr int WC = BN / 4, NP = BN / 128;       // columns per wave, block pairs per wave
+  const int g = r / WC, loc = r - g * WC;
+  const int jb = loc >> 4, nn = loc & 15;
+  return jb < 2 * NP ? g * WC + (jb >> 1) * 32 + (nn >> 2) * 8 + (jb & 1) * 4 + (nn & 3) : r;
+}
+// tile-local first column of the 4 that lane quad fq of MFMA block j owns (within the wave's WC columns)
+template <int BN, bool WIDE>
+__device__ __forceinline__ int g4_col(int j, int fq) {
+  constexpr int NP = BN / 128;
+  if constexpr (WIDE) return j < 2 * NP ? (j >> 1) * 32 + 8 * fq + 4 * (j & 1) : j * 16 + 4 * fq;
+  else return j * 16 + 4 * fq;
+}
 
 // Scalar (wave-uniform) position of a K-tile inside the implicit-GEMM conv: filter tap (kh, kw) and
 // channel base c (Cin % 64 == 0, so a 64-deep K-tile never straddles a tap or the concat split).
@@ -89,6 +114,8 @@ struct G4ConvPos {
 template <int CONV, bool GLU, int ACT, bool SPLITK, int VAR, int BN>
 __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __restrict__ ws, int k_per_split) {
   constexpr bool STAGGER = !(VAR & 1), STATIC_PRIO = (VAR & 2) != 0, PERSIST = (VAR & 8) != 0 && !SPLITK;
+  constexpr bool WIDE = (VAR & 16) != 0;
+  constexpr int NP = WIDE ? BN / 128 : 0;  // 16-column block pairs per wave with 8 consecutive columns per lane
   constexpr int G4_STAGE = G4T<BN>::STAGE, NJ = G4T<BN>::NJ, WC = G4T<BN>::WC, NWJ = G4T<BN>::NWJ;
   constexpr int GT = G4T<BN>::GT;
   constexpr int G4_G0 = 0, G4_G1 = G4Sched<VAR, GT>::G1, G4_G2 = G4Sched<VAR, GT>::G2, G4_G3 = GT;
@@ -154,7 +181,8 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
     for (int j = 0; j < 4; ++j) kch[j] = (lpos ^ (((wid * 32 + j * 8 + lrow) >> 1) & 7)) * 8;
 #pragma unroll
     for (int j = 0; j < NWJ; ++j) {
-      const int n = n0 + wid * (BN / 8) + j * 8 + lrow;
+      const int r = wid * (BN / 8) + j * 8 + lrow;  // LDS row
+      const int n = n0 + (WIDE ? g4_wperm<BN>(r) : r);
       woff[j] = n < p.N ? (uint32_t)(((long)n * p.ldw + kchw[j]) * 2) : G4_OOB;
     }
 #pragma unroll
@@ -254,8 +282,19 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
     for (int g = 0; g < GT; ++g) stage_one(0, k_begin, cpos, g);
   }
   bf16x8q wf[NJ], xf[4];
+  // VAR bit 5 (persistent only): the wide epilogue's stores stay in flight into the next tile.  The top of
+  // the loop then waits only for the next tile's first K-tile (DMA issued BEFORE the epilogue): vmcnt
+  // counts in issue order, and the fast wide epilogue issues at least G4_NOUT vector-memory instructions
+  // (its stores) after that DMA.  Any other epilogue path drains with vmcnt(0) below.
+  constexpr bool NODRAIN = (VAR & 32) != 0 && PERSIST && WIDE;
+  constexpr int G4_NOUT = 8 * (NP + (2 * NP < NJ ? 1 : 0));
+  static_assert(G4_NOUT < 63, "vmcnt range");
+  bool first = true, wide_done = false;
   while (true) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!NODRAIN || first || !wide_done) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G4_NOUT) : "memory");
+    first = false;
+    wide_done = false;
     __builtin_amdgcn_s_barrier();
     if (STAGGER && wm == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs half a phase behind
     if (STATIC_PRIO && wm == 1) __builtin_amdgcn_s_setprio(1);
@@ -331,6 +370,10 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
         cpos = conv_pos(k_begin);
 #pragma unroll
         for (int g = 0; g < GT; ++g) stage_one(0, k_begin, cpos, g);
+        if constexpr (NODRAIN) {  // pin the DMA ahead of the epilogue's loads and stores (vmcnt order)
+          asm volatile("" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     }
     auto epilogue = [&, fr0 = fr, fq0 = fq](const int m0, const int n0) {
@@ -347,7 +390,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
           if (m >= p.M) continue;
     #pragma unroll
           for (int j = 0; j < NJ; ++j) {
-            const int n = n0 + wn * WC + j * 16 + 4 * fq;
+            const int n = n0 + wn * WC + g4_col<BN, WIDE>(j, fq);
             if (n + 3 < p.N) {
               *reinterpret_cast<float4_*>(Wp + (long)m * p.N + n) = acc[i][j];
             } else {
@@ -360,7 +403,130 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
         const bf16_t* __restrict__ R = p.residual ? p.residual + (long)b * p.batch_r : nullptr;
         const bool fast = m0 + G4_BM <= p.M && n0 + BN <= p.N && p.bias2d == nullptr && p.gate == nullptr &&
                           (p.ldc & 3) == 0 && (R == nullptr || (p.ldr & 3) == 0);
-        if (fast) {
+        if constexpr (WIDE) {
+          // 16-byte C / residual / bias accesses: 8-element aligned rows and bases
+          const bool wide = fast && (((p.ldc | (R ? p.ldr : 0)) & 7) == 0) &&
+                            ((((uintptr_t)C) | (uintptr_t)R | (uintptr_t)p.bias) & 15) == 0;
+          if (wide) {
+            const bf16_t* __restrict__ bias = p.bias;
+            float bq[NP][8];
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+              const int n = n0 + wn * WC + q * 32 + 8 * fq;
+              if (bias) unpack8(*reinterpret_cast<const uint4_*>(bias + n), bq[q]);
+              else
+#pragma unroll
+                for (int e = 0; e < 8; ++e) bq[q][e] = 0.f;
+            }
+            constexpr bool TAIL = 2 * NP < NJ;  // BN = 320: block 4 keeps 4 columns per lane
+            float bt[4] = {0.f, 0.f, 0.f, 0.f};
+            const int nt4 = n0 + wn * WC + 2 * NP * 16 + 4 * fq;
+            if (TAIL && bias) {
+              const uint2_ bb = *reinterpret_cast<const uint2_*>(bias + nt4);
+              bt[0] = bf2f(bb[0] & 0xffff); bt[1] = bf2f(bb[0] >> 16);
+              bt[2] = bf2f(bb[1] & 0xffff); bt[3] = bf2f(bb[1] >> 16);
+            }
+            constexpr int IG = NJ == 4 ? 4 : 2;
+#pragma unroll
+            for (int i0 = 0; i0 < 8; i0 += IG) {
+              if constexpr (!GLU) {
+                uint4_ rr[IG][NP];
+                uint2_ rt[IG];
+                if (R) {
+#pragma unroll
+                  for (int ii = 0; ii < IG; ++ii) {
+                    const bf16_t* rrow = R + (long)(m0 + wm * 128 + (i0 + ii) * 16 + fr) * p.ldr + n0 + wn * WC;
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) rr[ii][q] = *reinterpret_cast<const uint4_*>(rrow + q * 32 + 8 * fq);
+                    if (TAIL) rt[ii] = *reinterpret_cast<const uint2_*>(rrow + 2 * NP * 16 + 4 * fq);
+                  }
+                }
+#pragma unroll
+                for (int ii = 0; ii < IG; ++ii) {
+                  const int i = i0 + ii;
+                  bf16_t* crow = C + (long)(m0 + wm * 128 + i * 16 + fr) * p.ldc + n0 + wn * WC;
+#pragma unroll
+                  for (int q = 0; q < NP; ++q) {
+                    float v[8];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                      v[e] = apply_act<ACT>(acc[i][2 * q][e] * p.alpha + bq[q][e]);
+                      v[4 + e] = apply_act<ACT>(acc[i][2 * q + 1][e] * p.alpha + bq[q][4 + e]);
+                    }
+                    if (R) {
+                      float r8[8];
+                      unpack8(rr[ii][q], r8);
+#pragma unroll
+                      for (int e = 0; e < 8; ++e) v[e] += r8[e] * p.res_alpha;
+                    }
+                    *reinterpret_cast<uint4_*>(crow + q * 32 + 8 * fq) = pack8(v);
+                  }
+                  if constexpr (TAIL) {
+                    float v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = apply_act<ACT>(acc[i][NJ - 1][e] * p.alpha + bt[e]);
+                    if (R) {
+                      v[0] += bf2f(rt[ii][0] & 0xffff) * p.res_alpha; v[1] += bf2f(rt[ii][0] >> 16) * p.res_alpha;
+                      v[2] += bf2f(rt[ii][1] & 0xffff) * p.res_alpha; v[3] += bf2f(rt[ii][1] >> 16) * p.res_alpha;
+                    }
+                    uint2_ o;
+                    o[0] = pack2(v[0], v[1]);
+                    o[1] = pack2(v[2], v[3]);
+                    *reinterpret_cast<uint2_*>(crow + 2 * NP * 16 + 4 * fq) = o;
+                  }
+                }
+              } else {
+                // GLU: (value, gate) column pairs -> the lane's 8 columns give 4 consecutive outputs
+                uint2_ rr[IG][NP];
+                uint32_t rt[IG];
+                if (R) {
+#pragma unroll
+                  for (int ii = 0; ii < IG; ++ii) {
+                    const bf16_t* rrow = R + (long)(m0 + wm * 128 + (i0 + ii) * 16 + fr) * p.ldr + ((n0 + wn * WC) >> 1);
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) rr[ii][q] = *reinterpret_cast<const uint2_*>(rrow + q * 16 + 4 * fq);
+                    if (TAIL) rt[ii] = *reinterpret_cast<const uint32_t*>(rrow + NP * 16 + 2 * fq);
+                  }
+                }
+#pragma unroll
+                for (int ii = 0; ii < IG; ++ii) {
+                  const int i = i0 + ii;
+                  bf16_t* crow = C + (long)(m0 + wm * 128 + i * 16 + fr) * p.ldc + ((n0 + wn * WC) >> 1);
+#pragma unroll
+                  for (int q = 0; q < NP; ++q) {
+                    float o[4];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                      const int j = 2 * q + h;
+                      o[2 * h] = (acc[i][j][0] * p.alpha + bq[q][4 * h]) * apply_act<ACT>(acc[i][j][1] * p.alpha + bq[q][4 * h + 1]);
+                      o[2 * h + 1] = (acc[i][j][2] * p.alpha + bq[q][4 * h + 2]) * apply_act<ACT>(acc[i][j][3] * p.alpha + bq[q][4 * h + 3]);
+                    }
+                    if (R) {
+                      o[0] += bf2f(rr[ii][q][0] & 0xffff) * p.res_alpha; o[1] += bf2f(rr[ii][q][0] >> 16) * p.res_alpha;
+                      o[2] += bf2f(rr[ii][q][1] & 0xffff) * p.res_alpha; o[3] += bf2f(rr[ii][q][1] >> 16) * p.res_alpha;
+                    }
+                    uint2_ w;
+                    w[0] = pack2(o[0], o[1]);
+                    w[1] = pack2(o[2], o[3]);
+                    *reinterpret_cast<uint2_*>(crow + q * 16 + 4 * fq) = w;
+                  }
+                  if constexpr (TAIL) {
+                    float o0 = (acc[i][NJ - 1][0] * p.alpha + bt[0]) * apply_act<ACT>(acc[i][NJ - 1][1] * p.alpha + bt[1]);
+                    float o1 = (acc[i][NJ - 1][2] * p.alpha + bt[2]) * apply_act<ACT>(acc[i][NJ - 1][3] * p.alpha + bt[3]);
+                    if (R) {
+                      o0 += bf2f(rt[ii] & 0xffff) * p.res_alpha;
+                      o1 += bf2f(rt[ii] >> 16) * p.res_alpha;
+                    }
+                    *reinterpret_cast<uint32_t*>(crow + NP * 16 + 2 * fq) = pack2(o0, o1);
+                  }
+                }
+              }
+            }
+            wide_done = true;
+            return;
+          }
+        }
+        if (fast && !WIDE) {
           // interior tile: per-column bias hoisted, residual rows prefetched in groups of IG row blocks (all 8
           // at NJ = 4; 2 at NJ = 5, where 160 accumulator registers leave no room for 80 more)
           const bf16_t* __restrict__ bias = p.bias;
@@ -448,7 +614,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
           if (m >= p.M) continue;
     #pragma unroll
           for (int j = 0; j < NJ; ++j) {
-            const int n = n0 + wn * WC + j * 16 + 4 * fq;
+            const int n = n0 + wn * WC + g4_col<BN, WIDE>(j, fq);
             if (n >= p.N) continue;
             float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
             epilogue4<GLU, ACT>(p, C, R, m, n, v, b);
@@ -513,8 +679,11 @@ void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t 
   if (ws == nullptr) splits = 1;
   const long kt = (a.K + G4_BK - 1) / G4_BK;
   const int kps = (int)(((kt + splits - 1) / splits) * G4_BK);
-  if (persist && splits <= 1) g4_dispatch<12>(a, ws, splits, kps, bn, s);
-  else g4_dispatch<4>(a, ws, splits, kps, bn, s);
+  // wide epilogue (VAR bit 4) in production: +1-3 % on K >= 2048, +14-24 % on the K = 320 SD2.1 GEMMs
+  // (tools/gemm_lab, profiles/gemm_wide_epilogue_round3.md)
+  // persistent: + VAR bit 5 (the epilogue's stores stay in flight into the next tile; lab +0-4 %)
+  if (persist && splits <= 1) g4_dispatch<60>(a, ws, splits, kps, bn, s);
+  else g4_dispatch<20>(a, ws, splits, kps, bn, s);
   if (splits > 1) launch_splitk_epilogue(a, ws, splits, s);
 }
 
@@ -544,23 +713,17 @@ static void g4_dispatch(const GemmArgs& a, float* ws, int splits, int kps, int b
   }
 }
 
-// Lab entry: schedule variant `var` (see G4Sched) of the plain / conv no-activation kernel, no split-K.
+#ifdef SHAI_GEMM_LAB
+// Lab entry (tools/gemm_lab, built with -DSHAI_GEMM_LAB only): schedule variant `var` (see G4Sched) with the
+// full epilogue dispatch (conv / GLU / activations), no split-K.
 void launch_gemm4_var(const GemmArgs& a, int var, int bn, hipStream_t s) {
   const int kps = (int)(((a.K + G4_BK - 1) / G4_BK) * G4_BK);
-#define SHAI_G4V(V)                                                               \
-  case V:                                                                         \
-    if (a.conv) {                                                                 \
-      if (a.upsample) g4_launch<2, false, ACT_NONE, V>(a, nullptr, 1, kps, bn, s); \
-      else g4_launch<1, false, ACT_NONE, V>(a, nullptr, 1, kps, bn, s);            \
-    } else {                                                                      \
-      g4_launch<0, false, ACT_NONE, V>(a, nullptr, 1, kps, bn, s);                \
-    }                                                                             \
-    break;
   switch (var) {
-    SHAI_G4V(0) SHAI_G4V(4) SHAI_G4V(6) SHAI_G4V(12)
+    case 20: g4_dispatch<20>(a, nullptr, 1, kps, bn, s); break;
+    case 60: g4_dispatch<60>(a, nullptr, 1, kps, bn, s); break;
     default: break;
   }
-#undef SHAI_G4V
 }
+#endif
 
 }  // namespace shai

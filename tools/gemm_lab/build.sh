@@ -4,7 +4,7 @@ set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
 OUT=$ROOT/build/gemm_lab
 mkdir -p "$OUT"
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=fast -I$ROOT/csrc"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=fast -I$ROOT/csrc -DSHAI_GEMM_LAB"
 for src in gemm_lds gemm_pipe gemm_8ph attention attention2; do
   # incremental: rebuild an object only when its source or a shared header is newer
   if [ ! -f "$OUT/$src.o" ] || [ -n "$(find "$ROOT/csrc/kernels/$src.hip" "$ROOT/csrc/kernels/"*.h -newer "$OUT/$src.o")" ]; then

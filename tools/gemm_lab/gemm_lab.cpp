@@ -81,6 +81,16 @@ __global__ void ref_conv(const bf16_t* X, const bf16_t* W, float* C, int Nimg, i
   C[m * Cout + co] = s;
 }
 
+// GLU reference in place of the fp32 product: out[m, c] = h[m, 2c] * gelu(h[m, 2c + 1]) (erf GELU)
+__global__ void ref_glu(const float* H, float* O, long M, int N) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= M * (N / 2)) return;
+  const long m = i / (N / 2);
+  const int c = (int)(i % (N / 2));
+  const float a = H[m * N + 2 * c], g = H[m * N + 2 * c + 1];
+  O[i] = a * 0.5f * g * (1.f + erff(g * 0.70710678f));
+}
+
 __global__ void err_kernel(const bf16_t* C, const float* R, long n, float* out) {
   float e = 0.f, r = 0.f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -95,12 +105,17 @@ struct Problem {
   std::string name;
   int M, N, K;            // plain GEMM (conv: M = N*OH*OW, K = KH*KW*Cin)
   int conv = 0, Nimg = 0, H = 0, Wd = 0, Cin = 0, KH = 1, stride = 1, pad = 0, ups = 0;
-  bool bias = false, res = false;
+  bool bias = false, res = false, glu = false;
 };
 
 static Problem gemm(const char* nm, int M, int N, int K, bool bias = false, bool res = false) {
   Problem p;
   p.name = nm; p.M = M; p.N = N; p.K = K; p.bias = bias; p.res = res;
+  return p;
+}
+static Problem geglu(const char* nm, int M, int N, int K) {
+  Problem p = gemm(nm, M, N, K, true);
+  p.glu = true;
   return p;
 }
 static Problem conv(const char* nm, int Nimg, int H, int Cin, int Cout, int KH, int ups = 0) {
@@ -116,7 +131,8 @@ static shai::GemmArgs make_args(const Problem& P, bf16_t* A, bf16_t* W, bf16_t* 
   memset(&g, 0, sizeof(g));
   g.A = A; g.W = W; g.C = C; g.bias = P.bias ? bias : nullptr; g.residual = P.res ? R : nullptr;
   g.M = P.M; g.N = P.N; g.K = P.K;
-  g.lda = P.conv ? P.Cin : P.K; g.ldw = P.K; g.ldc = P.N; g.ldr = P.N;
+  g.lda = P.conv ? P.Cin : P.K; g.ldw = P.K; g.ldc = P.glu ? P.N / 2 : P.N; g.ldr = g.ldc;
+  if (P.glu) { g.glu = 1; g.act = shai::ACT_GELU; }
   g.batch = 1; g.rows_per_bias2d = 1; g.alpha = 1.f; g.res_alpha = 1.f; g.rows_per_gate = 1;
   if (P.conv) {
     g.conv = 1; g.Nimg = P.Nimg; g.H = P.H; g.Wd = P.Wd; g.Cin = P.Cin; g.KH = P.KH; g.KW = P.KH;
@@ -135,7 +151,12 @@ int main(int argc, char** argv) {
       gemm("flux_ff_up", 4608, 12288, 3072, true),
       gemm("flux_ff_dn", 4608, 3072, 12288, false, true),
       gemm("sd_ff_up", 262144 / 4, 2560, 320, true),
+      geglu("sd_geglu64", 262144, 2560, 320),
+      geglu("sd_geglu32", 65536, 5120, 640),
+      geglu("sd_geglu16", 16384, 10240, 1280),
       gemm("sd_qkv", 262144, 960, 320),
+      gemm("sd_proj_res", 262144, 320, 320, true, true),
+      gemm("sd_ff_dn_res", 65536, 640, 2560, true, true),
       gemm("llm_pf_qkv", 8192, 6144, 4096),
       conv("unet64_320", 64, 64, 320, 320, 3),
       conv("unet32_640", 64, 32, 640, 640, 3),
@@ -165,7 +186,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&C, maxC * 2));
   CK(hipMalloc(&R, maxC * 2));
   CK(hipMalloc(&bias, 65536 * 2));
-  CK(hipMalloc(&ref, maxC * 4));
+  CK(hipMalloc(&ref, maxC * 6));  // GLU problems keep the product and the GLU output
   CK(hipMalloc(&err, 8));
   CK(hipMalloc(&ws, 64));
   fill_kernel<<<4096, 256>>>(A, maxA, 1u, 1.f);
@@ -182,8 +203,7 @@ int main(int argc, char** argv) {
     const char* name;
     int kind;  // 0: v3 256 4-stage, 1: v3 256 2-stage, 2: v3 320 2-stage, 10+v: v4 schedule variant v
   };
-  const Var vars[] = {{"v3_256x4", 0}, {"v3_256x2", 1}, {"v3_320x2", 2}, {"v4_256", 14}, {"v4_256v6", 16},
-                      {"v4_320", 114}, {"v4_320v6", 116}, {"v4_320v0", 110}};
+  const Var vars[] = {{"v4_256w", 30}, {"v4_256pwn", 70}, {"v4_320w", 130}, {"v4_320pwn", 170}};
   constexpr int NV = sizeof(vars) / sizeof(vars[0]);
   auto run = [&](const Var& v, const shai::GemmArgs& g) {
     switch (v.kind) {
@@ -204,7 +224,13 @@ int main(int argc, char** argv) {
       ref_gemm<<<dim3((P.N + 127) / 128, P.M), 128>>>(A, W, P.bias ? bias : nullptr, P.res ? R : nullptr, ref, P.M,
                                                       P.N, P.K);
     }
+    if (P.glu) {  // ref holds the M x N product; the GLU output (M x N/2) goes behind it
+      const long no = (long)P.M * (P.N / 2);
+      ref_glu<<<(unsigned)((no + 255) / 256), 256>>>(ref, ref + (long)P.M * P.N, P.M, P.N);
+    }
     CK(hipDeviceSynchronize());
+    const float* refc = P.glu ? ref + (long)P.M * P.N : ref;
+    const long nout = P.glu ? (long)P.M * (P.N / 2) : (long)P.M * P.N;
     const double flop = 2.0 * P.M * P.N * P.K;
     printf("== %s M=%d N=%d K=%d%s\n", P.name.c_str(), P.M, P.N, P.K, P.conv ? " (conv)" : "");
     std::vector<float> best(NV, 1e30f);
@@ -215,7 +241,7 @@ int main(int argc, char** argv) {
       run(vars[vi], g);
       CK(hipGetLastError());
       CK(hipDeviceSynchronize());
-      err_kernel<<<1024, 256>>>(C, ref, (long)P.M * P.N, err);
+      err_kernel<<<1024, 256>>>(C, refc, nout, err);
       float he[2];
       CK(hipMemcpy(he, err, 8, hipMemcpyDeviceToHost));
       const float tol = 0.02f * he[1] + 0.05f;
