@@ -21,6 +21,7 @@
 #include "launchers.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace shai {
 
@@ -270,8 +271,264 @@ __global__ void __launch_bounds__(256, 2) flash_fwd_kernel(const AttnArgs p) {
   }
 }
 
+// ----------------------------------------------------------------------------
+// flash64: the v1 structure above (4 waves x 32 queries, register-staged K/V, double-buffered swizzled
+// LDS, several workgroups per CU so that one wave's MFMAs overlap another's softmax) specialised for
+// D = 64 without bias / paged K/V -- every SD2.1 attention.  At D = 64 the loop is bound by VALU issue
+// (the softmax costs about what the 16 MFMAs of a 64-key tile do), so the VALU per tile is cut from
+// ~125 to ~70 instructions:
+//  * Q is pre-multiplied by scale * log2(e) (one bf16 rounding of the scaled Q, |rel| <= 2^-9 per element):
+//    the scores arrive in the exp2 domain.
+//  * -m enters each 32-key score chain as one extra v_mfma (A = a ones column, B = -m; the running max is
+//    kept on the bf16 grid so it is exact as a bf16 operand): the accumulators start at the inline constant
+//    0 and P = exp2(acc) is one v_exp per score, no FMA / no accumulator initialisation moves.
+//  * Max-free fast path (as flash2): the running max stays unchanged while every lane's partial row sum of
+//    the tile is <= 2^8 (P then stays bounded by 2^8: bf16 P, fp32 O / l absorb it); otherwise, or before a
+//    row has a max, the tile takes the exact path (tile max, O / l rescale, recompute P).
+//  * Fragment reads at immediate offsets from six per-stage base addresses (the XOR swizzle depends on
+//    the lane only).
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) flash64_kernel(const AttnArgs p) {
+  constexpr int D = 64, KT = 64, CPR = 8, NST = KT * CPR / 256, NS = 4, ND = 2;
+  constexpr float kSumThr = 256.f;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  bf16_t* sK = smem;
+  bf16_t* sV = smem + 2 * KT * D;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 31, fh = lane >> 5;
+  const int b = blockIdx.z, hq = blockIdx.y;
+  const int hk = hq / (p.Hq / p.Hkv);
+  const int q_len = p.q_lens ? p.q_lens[b] : p.Sq;
+  const int kv_len = p.kv_lens ? p.kv_lens[b] : p.Skv;
+  const int c_off = p.q_lens ? kv_len - q_len : p.causal_offset;
+  if ((int)blockIdx.x * 128 >= q_len) return;
+  const int q0 = blockIdx.x * 128;
+  const int qi = q0 + wid * 32 + fr;
+  const float sl2 = p.scale * kLog2e;
+
+  bf16x8 qf[NS];
+  {
+    const bf16_t* qp = p.q + (p.q_start ? (long)p.q_start[b] * p.q_ts : (long)b * p.q_bs) +
+                        (long)min(qi, q_len - 1) * p.q_ts + (long)hq * D;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      uint4_ v = *reinterpret_cast<const uint4_*>(qp + 16 * s + 8 * fh);
+      if (qi >= q_len) v = uint4_{0u, 0u, 0u, 0u};
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= sl2;
+      qf[s] = __builtin_bit_cast(bf16x8, pack8(f));
+    }
+  }
+
+  int kv_end = kv_len;
+  if (CAUSAL) kv_end = min(kv_end, q0 + 127 + c_off + 1);
+  const int ntiles = kv_end > 0 ? (kv_end + KT - 1) / KT : 0;
+  const bf16_t* kbase = p.k + (long)b * p.k_bs + (long)hk * D;
+  const bf16_t* vbase = p.v + (long)b * p.v_bs + (long)hk * D;
+
+  uint4_ rk[NST], rv[NST];
+  auto load_tile = [&](int t) {
+    const int key0 = t * KT;
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int id = tid + 256 * i;
+      const int row = id / CPR, ch = id % CPR;
+      const bool ok = key0 + row < kv_len;
+      rk[i] = ok ? *reinterpret_cast<const uint4_*>(kbase + (long)(key0 + row) * p.k_ts + ch * 8) : uint4_{0u, 0u, 0u, 0u};
+      rv[i] = ok ? *reinterpret_cast<const uint4_*>(vbase + (long)(key0 + row) * p.v_ts + ch * 8) : uint4_{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store_tile = [&](int stage) {
+    bf16_t* ks = sK + stage * KT * D;
+    bf16_t* vs = sV + stage * KT * D;
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int id = tid + 256 * i;
+      const int row = id / CPR, ch = id % CPR;
+      *reinterpret_cast<uint4_*>(ks + k_swz<D>(row, ch)) = rk[i];
+      *reinterpret_cast<uint4_*>(vs + v_swz<D>(row, ch)) = rv[i];
+    }
+  };
+
+  float16_ o[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+  auto m_base = [&]() { return m_run == -INFINITY ? 0.f : m_run; };
+  // -m MFMA operands: A[key][k] = (k == 0), B[k][query] = (k == 0) * -m_base (lanes 0-31 hold k 0..7)
+  const bf16x8 a_one = __builtin_bit_cast(bf16x8, uint4_{lane < 32 ? 0x3F80u : 0u, 0u, 0u, 0u});
+  bf16x8 b_negm = __builtin_bit_cast(bf16x8, uint4_{0u, 0u, 0u, 0u});
+
+  const int g16 = lane >> 4, i16 = lane & 15;
+  const int tq = i16 >> 2, tp = i16 & 3;
+  int koff[NS], voff[ND];  // element offsets inside a stage (key block 0 / first transposed-read row)
+#pragma unroll
+  for (int s = 0; s < NS; ++s) koff[s] = k_swz<D>(fr, 2 * s + fh);
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    const int col = d * 32 + 16 * (g16 & 1) + 4 * tp;
+    voff[d] = v_swz<D>(4 * fh + tq, col >> 3) + 4 * ((col >> 2) & 1);
+  }
+
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+
+  float16_ sacc[2];
+  bf16x8 pf[2][2];
+  // P from the accumulators (+ add when ADD); returns this lane's partial row sum.  All 32 exponentials
+  // first: consuming each v_exp result right away pads it with an s_nop (transcendental hazard).
+  auto expo = [&](float add, auto addt) {
+    constexpr bool ADD = decltype(addt)::value;
+    float e[2][16];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) e[kb][r] = __builtin_amdgcn_exp2f(ADD ? sacc[kb][r] + add : sacc[kb][r]);
+    __builtin_amdgcn_sched_barrier(0);
+    float ls4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ls4[j & 3] += e[kb][8 * s + j];
+          v[j] = (__bf16)e[kb][8 * s + j];
+        }
+        pf[kb][s] = v;
+      }
+    return (ls4[0] + ls4[1]) + (ls4[2] + ls4[3]);
+  };
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < ntiles) load_tile(t + 1);
+    const bf16_t* ks = sK + cur * KT * D;
+    const bf16_t* vs = sV + cur * KT * D;
+
+    // ---- S^T - m = K Q^T - m for two 32-key blocks
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const float16_ z = {};
+      sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, b_negm, z, 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + koff[s] + kb * 2048);
+        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kb], 0, 0, 0);
+      }
+    }
+    const int key0 = t * KT;
+    const bool need_mask = (key0 + KT > kv_len) || (CAUSAL && key0 + KT - 1 > q0 + c_off);
+    if (need_mask) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          const bool bad = key >= kv_len || (CAUSAL && key > qi + c_off);
+          sacc[kb][r] = bad ? -INFINITY : sacc[kb][r];
+        }
+    }
+    float ls = 0.f;
+    bool slow = __any(m_run == -INFINITY);
+    if (!slow) {
+      ls = expo(0.f, std::false_type{});
+      slow = __any(!(ls <= kSumThr));
+    }
+    if (slow) {  // exact path: tile max, rescale O and l, recompute P
+      float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) m4[r & 3] = fmaxf(m4[r & 3], sacc[kb][r]);
+      float mloc = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64)) + m_base();  // accumulators hold s - m_base
+      const float m_new = bf16_up(fmaxf(m_run, mloc));
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);  // 0 when m_run = -inf
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+      l_run *= alpha;
+      const float shift = m_base() - m_use;
+      m_run = m_new;
+      const uint32_t nb = __float_as_uint(-m_base()) >> 16;  // bf16-exact
+      b_negm = __builtin_bit_cast(bf16x8, uint4_{lane < 32 ? nb : 0u, 0u, 0u, 0u});
+      ls = expo(shift, std::true_type{});
+    }
+    l_run += ls;
+
+    // ---- O^T += V^T P^T
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16_t* a0 = vs + voff[d] + kb * 2048 + s * 1024;
+          const s4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(a0));
+          const s4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(a0 + 512));
+          short8 vv;
+          vv[0] = t0[0]; vv[1] = t0[1]; vv[2] = t0[2]; vv[3] = t0[3];
+          vv[4] = t1[0]; vv[5] = t1[1]; vv[6] = t1[2]; vv[7] = t1[3];
+          o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vv), pf[kb][s], o[d], 0, 0, 0);
+        }
+      }
+    }
+    if (t + 1 < ntiles) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (qi < q_len) {
+    bf16_t* op = p.o + (p.q_start ? (long)p.q_start[b] * p.o_ts : (long)b * p.o_bs) + (long)qi * p.o_ts +
+                 (long)hq * D;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int dd = d * 32 + 8 * g + 4 * fh;
+        uint2_ w;
+        w[0] = pack2(o[d][4 * g] * inv, o[d][4 * g + 1] * inv);
+        w[1] = pack2(o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv);
+        *reinterpret_cast<uint2_*>(op + dd) = w;
+      }
+    }
+  }
+}
+
+bool flash64_supported(const AttnArgs& a) {
+  static const bool on = [] {
+    const char* e = getenv("SHAI_FLASH64");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on && a.D == 64 && a.bias == nullptr && a.block_table == nullptr && ((a.k_ts | a.v_ts | a.q_ts) & 7) == 0;
+}
+
+void launch_flash64(const AttnArgs& a, hipStream_t s) {
+  dim3 grid((a.Sq + 127) / 128, a.Hq, a.B);
+  const size_t lds = (size_t)4 * 64 * 64 * sizeof(bf16_t);
+  if (a.causal) flash64_kernel<true><<<grid, 256, lds, s>>>(a);
+  else flash64_kernel<false><<<grid, 256, lds, s>>>(a);
+}
+
 void launch_flash_attn(const AttnArgs& a, hipStream_t s) {
   static const bool v1_only = getenv("SHAI_FLASH_V1") != nullptr;  // A/B and tests: pin the v1 kernel
+  if (!v1_only && flash64_supported(a)) {  // D = 64 (every SD2.1 / ViT / BERT attention)
+    launch_flash64(a, s);
+    return;
+  }
   if (!v1_only && flash2_supported(a)) {  // 8-wave ping-pong kernel (attention2.hip)
     launch_flash2(a, s);
     return;

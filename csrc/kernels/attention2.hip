@@ -81,6 +81,23 @@ __device__ __forceinline__ bf16x8a f2_b128_read(const bf16_t* ptr) {
   return r;
 }
 
+// The same reads with a compile-time byte offset (the instruction's 16-bit offset field): the lane's base
+// address is computed once per ring slot and every fragment of the tile is an immediate away from it.
+template <int OFF>
+__device__ __forceinline__ s4a f2_tr_read_o(uint32_t a) {
+  s4a r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ bf16x8a f2_b128_read_o(uint32_t a) {
+  bf16x8a r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
+  return r;
+}
+__device__ __forceinline__ uint32_t f2_lds_addr(const bf16_t* ptr) {
+  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)ptr);
+}
 // LDS-DMA through a device helper: a direct call of the target builtin inside the kernel template's
 // lambda makes the host pass drop the kernel's launch stubs (undefined __device_stub__ at load time).
 __device__ __forceinline__ void f2_glds(__amdgpu_buffer_rsrc_t r, bf16_t* lds, uint32_t off) {
@@ -106,6 +123,12 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
   // -m (the running max they are computed against), so the fast path's exponent is the raw accumulator --
   // one v_exp per score, no v_fma.  Costs one bf16 rounding of the scaled Q (|rel| <= 2^-9 per element).
   constexpr bool PRE = D == 64 && !(EXP & 16);  // EXP & 16: the unscaled form (A/B: SHAI_FLASH2_PRE=0)
+  // D = 64 M segment (EXP & 32 restores the previous form for A/B): (a) every LDS fragment read is an immediate
+  // offset from one of six per-tile base addresses (was one v_add per read: 29 VALU per tile); (b) the score
+  // accumulators start at zero (inline constant) and -m enters through one extra MFMA per 32-key block,
+  // A = a ones column, B = -m on the bf16 grid (was 32 v_mov per tile).  VALU issue, not the matrix pipe,
+  // bounds this loop at D = 64 (profiles/flash_attn_v2_round2.md), so 2 MFMAs buy back ~60 VALU.
+  constexpr bool NEWM = PRE && !(EXP & 32);
   static_assert(NPW >= 1 && (2 * NPI) % 8 == 0, "bad D");
   extern __shared__ __attribute__((aligned(16))) bf16_t f2_smem[];
 
@@ -187,6 +210,13 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
   auto s_init = [&]() { return PRE ? -m_base() : 0.f; };
   float16_ sacc[2];
   bf16x8a pf[2][2];
+  // NEWM operands of the -m MFMA: A[key][k] = (k == 0), B[k][query] = (k == 0) * -m_base (lanes 0-31 own k 0-7)
+  const bf16x8a a_one = __builtin_bit_cast(bf16x8a, uint4_{lane < 32 ? 0x3F80u : 0u, 0u, 0u, 0u});
+  bf16x8a b_negm = __builtin_bit_cast(bf16x8a, uint4_{0u, 0u, 0u, 0u});
+  auto set_negm = [&]() {  // m_base() is bf16-exact under NEWM
+    const uint32_t nb = __float_as_uint(-m_base()) >> 16;
+    b_negm = __builtin_bit_cast(bf16x8a, uint4_{lane < 32 ? nb : 0u, 0u, 0u, 0u});
+  };
 
   auto qk = [&](int t) {  // S^T(t) = K(t) Q^T for two 32-key blocks; every K fragment read issued first
     const bf16_t* ks = f2_smem + (t & 3) * TILE;
@@ -292,7 +322,7 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
       mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
       // scale > 0: max commutes with scaling; PRE accumulators are s - base in the exponent domain
       mloc = PRE ? mloc + m_base() : mloc * sl2;
-      const float m_new = fmaxf(m_run, mloc);
+      const float m_new = NEWM ? bf16_up(fmaxf(m_run, mloc)) : fmaxf(m_run, mloc);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);  // 0 when m_run = -inf
 #pragma unroll
@@ -302,10 +332,23 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
       l_run *= alpha;
       const float shift = m_base() - m_use;  // PRE: exponent = (s - base) + (base - m_new)
       m_run = m_new;
+      if constexpr (NEWM) set_negm();
       ls = expo(PRE ? shift : m_use, std::true_type{});
     }
     l_run += ls;
   };
+
+  // NEWM: the lane's byte offsets inside a ring slot (K: row fr of key block 0, chunk 2 s + fh; V: the first
+  // transposed-read row 4 fh + tq of key block 0, chunk of d block d); everything else is an immediate
+  const uint32_t lds0 = f2_lds_addr(f2_smem);
+  uint32_t kofs[NS], vofs[ND];
+#pragma unroll
+  for (int s2 = 0; s2 < NS; ++s2) kofs[s2] = (uint32_t)f2_kswz<D>(fr, 2 * s2 + fh) * 2;
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    const int col = d * 32 + 16 * (g16 & 1) + 4 * tp;
+    vofs[d] = (uint32_t)(KT * D + f2_vswz<D>(4 * fh + tq, col >> 3) + 4 * ((col >> 2) & 1)) * 2;
+  }
 
   // ---- prologue: tiles 0..2 in flight, 0 and 1 landed; S(0), P(0) by every wave
   stage(0);
@@ -338,7 +381,59 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
     stamp();
     stage(t + 3);
     s4a vr0[ND][2][2], vr1[ND][2][2];
-    if constexpr (D == 64) {
+    if constexpr (NEWM) {
+      const bool more = t + 1 < nt;
+      const uint32_t kslot = lds0 + (uint32_t)(((t + 1) & 3) * TILE * 2);
+      const uint32_t vslot = lds0 + (uint32_t)((t & 3) * TILE * 2);
+      uint32_t ka[NS], va[ND];
+#pragma unroll
+      for (int s2 = 0; s2 < NS; ++s2) ka[s2] = kslot + kofs[s2];
+#pragma unroll
+      for (int d = 0; d < ND; ++d) va[d] = vslot + vofs[d];
+      bf16x8a kf[2][NS];
+      // K block 0, K block 1 (kb 1 = 32 rows = 4096 B further), then V^T of key block 0
+      kf[0][0] = f2_b128_read_o<0>(ka[0]); kf[0][1] = f2_b128_read_o<0>(ka[1]);
+      kf[0][2] = f2_b128_read_o<0>(ka[2]); kf[0][3] = f2_b128_read_o<0>(ka[3]);
+      kf[1][0] = f2_b128_read_o<4096>(ka[0]); kf[1][1] = f2_b128_read_o<4096>(ka[1]);
+      kf[1][2] = f2_b128_read_o<4096>(ka[2]); kf[1][3] = f2_b128_read_o<4096>(ka[3]);
+      // V^T(t) fragment (d, s, e) of key block kb: rows kb*32 + 16 s + 8 e (+ the lane's row), 128 B per row
+#define F2_VR(VR, KB, D_)                                   \
+  VR[D_][0][0] = f2_tr_read_o<(KB) * 4096 + 0>(va[D_]);    \
+  VR[D_][0][1] = f2_tr_read_o<(KB) * 4096 + 1024>(va[D_]); \
+  VR[D_][1][0] = f2_tr_read_o<(KB) * 4096 + 2048>(va[D_]); \
+  VR[D_][1][1] = f2_tr_read_o<(KB) * 4096 + 3072>(va[D_]);
+      F2_VR(vr0, 0, 0)
+      F2_VR(vr0, 0, 1)
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");  // K kb0
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(EXP & 2) && more) {
+        const float16_ z = {};
+        sacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, b_negm, z, 0, 0, 0);
+#pragma unroll
+        for (int s2 = 0; s2 < NS; ++s2) sacc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[0][s2], qf[s2], sacc[0], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // K kb1
+      __builtin_amdgcn_sched_barrier(0);
+      F2_VR(vr1, 1, 0)
+      F2_VR(vr1, 1, 1)
+#undef F2_VR
+      if (!(EXP & 2) && more) {
+        const float16_ z = {};
+        sacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, b_negm, z, 0, 0, 0);
+#pragma unroll
+        for (int s2 = 0; s2 < NS; ++s2) sacc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[1][s2], qf[s2], sacc[1], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // V^T kb0
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(EXP & 2)) pv_mfma(0, vr0);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // V^T kb1
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(EXP & 2)) pv_mfma(1, vr1);
+    } else if constexpr (D == 64) {
       // every fragment read issued by asm in consumption order (K kb0, K kb1, V^T kb0 | V^T kb1), counted
       // lgkmcnt waits before each 4-MFMA group (LDS returns in order; at most 15 outstanding)
       const bool more = t + 1 < nt;
@@ -478,7 +573,7 @@ void launch_flash2_exp(const AttnArgs& a, int exp, hipStream_t s) {
     else flash2_kernel<64, false, E><<<grid, 512, lds, s>>>(a);              \
     break;
   switch (exp) {
-    SHAI_F2X(0) SHAI_F2X(1) SHAI_F2X(2) SHAI_F2X(4) SHAI_F2X(8) SHAI_F2X(12)
+    SHAI_F2X(0) SHAI_F2X(1) SHAI_F2X(2) SHAI_F2X(4) SHAI_F2X(8) SHAI_F2X(12) SHAI_F2X(32)
     default: break;
   }
 #undef SHAI_F2X

@@ -90,6 +90,15 @@ __device__ __forceinline__ float gelu_tanh_f(float x) {
 
 __device__ __forceinline__ float quick_gelu_f(float x) { return x / (1.0f + __expf(-1.702f * x)); }
 
+// smallest bf16-representable float >= x (finite x; -inf stays -inf): flash attention keeps its running max on
+// the bf16 grid so that -m can enter the score MFMA exactly as a bf16 operand
+__device__ __forceinline__ float bf16_up(float x) {
+  uint32_t u = __float_as_uint(x);
+  if ((u & 0xffffu) == 0u) return x;
+  if (!(u >> 31)) u += 0x10000u;  // positive: round the magnitude up; negative: truncation rounds up
+  return __uint_as_float(u & 0xffff0000u);
+}
+
 enum Act : int { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_GELU_TANH = 3, ACT_QUICK_GELU = 4, ACT_RELU = 5 };
 
 template <int ACT>

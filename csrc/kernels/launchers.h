@@ -189,6 +189,8 @@ struct AttnArgs {
 void launch_flash_attn(const AttnArgs& a, hipStream_t s);
 // v2 (attention2.hip): 8-wave ping-pong, LDS-DMA K/V ring; launch_flash_attn dispatches to it when supported
 bool flash2_supported(const AttnArgs& a);
+bool flash64_supported(const AttnArgs& a);
+void launch_flash64(const AttnArgs& a, hipStream_t s);
 void launch_flash2(const AttnArgs& a, hipStream_t s);
 
 struct DecodeAttnArgs {

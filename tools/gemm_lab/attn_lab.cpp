@@ -88,7 +88,8 @@ int main() {
       const int rows = 64;
       float* ref;
       CK(hipMalloc(&ref, rows * c.D * 4));
-      shai::launch_flash2_exp(a, 0, 0);
+      if (c.D == 64) shai::launch_flash64(a, 0);  // production d64 kernel
+      else shai::launch_flash2_exp(a, 0, 0);
       ref_rows<<<1, 64>>>(q, k, v, ref, c.S, c.H, c.D, rows, a.scale);
       CK(hipDeviceSynchronize());
       std::vector<float> hr(rows * c.D);
@@ -104,16 +105,17 @@ int main() {
           err = fmax(err, fabs(f - hr[i * c.D + d]));
           mx = fmax(mx, fabs(hr[i * c.D + d]));
         }
-      printf("  flash2 max_abs_err %.4f (max |ref| %.3f) %s\n", err, mx, err < 0.02 * mx + 0.01 ? "OK" : "MISMATCH");
+      printf("  %s max_abs_err %.4f (max |ref| %.3f) %s\n", c.D == 64 ? "flash64" : "flash2", err, mx, err < 0.02 * mx + 0.01 ? "OK" : "MISMATCH");
       CK(hipFree(ref));
     }
     struct V { const char* name; int exp; };  // exp < 0: v1
-    const V vars[] = {{"v1", -1}, {"flash2", 0}, {"f2-noprio", 8}, {"f2-nosoftmax", 1}};
+    const V vars[] = {{"v1", -1}, {"flash2", 0}, {"flash64", -2}, {"f2-nosoftmax", 1}};
     float best[4] = {1e30f, 1e30f, 1e30f, 1e30f};
     for (int r = 0; r < 5; ++r)
       for (int vi = 0; vi < 4; ++vi) {
         auto run = [&]() {
-          if (vars[vi].exp < 0) shai::launch_flash_attn(a, 0);
+          if (vars[vi].exp == -2) { if (c.D == 64) shai::launch_flash64(a, 0); }
+          else if (vars[vi].exp < 0) shai::launch_flash_attn(a, 0);
           else shai::launch_flash2_exp(a, vars[vi].exp, 0);
         };
         run();

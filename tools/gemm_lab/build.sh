@@ -14,6 +14,7 @@ done
 hipcc $FLAGS -x hip -c "$ROOT/tools/gemm_lab/gemm_lab.cpp" -o "$OUT/gemm_lab.o" &
 hipcc $FLAGS -x hip -c "$ROOT/tools/gemm_lab/attn_lab.cpp" -o "$OUT/attn_lab.o" &
 wait
+[ -s "$OUT/gemm_lab.o" ] && [ "$OUT/gemm_lab.o" -nt "$ROOT/tools/gemm_lab/gemm_lab.cpp" ] || { echo "gemm_lab.o stale"; exit 1; }
 mkdir -p "$ROOT/tools/gemm_lab/bin"
 hipcc --offload-arch=gfx950 "$OUT"/gemm_lab.o "$OUT"/gemm_lds.o "$OUT"/gemm_pipe.o "$OUT"/gemm_8ph.o \
   -o "$ROOT/tools/gemm_lab/bin/gemm_lab"

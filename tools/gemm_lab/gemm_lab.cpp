@@ -132,7 +132,7 @@ static shai::GemmArgs make_args(const Problem& P, bf16_t* A, bf16_t* W, bf16_t* 
   g.A = A; g.W = W; g.C = C; g.bias = P.bias ? bias : nullptr; g.residual = P.res ? R : nullptr;
   g.M = P.M; g.N = P.N; g.K = P.K;
   g.lda = P.conv ? P.Cin : P.K; g.ldw = P.K; g.ldc = P.glu ? P.N / 2 : P.N; g.ldr = g.ldc;
-  if (P.glu) { g.glu = 1; g.act = shai::ACT_GELU; }
+  if (P.glu) { g.glu = 1; g.act = 2; }  // ACT_GELU (erf)
   g.batch = 1; g.rows_per_bias2d = 1; g.alpha = 1.f; g.res_alpha = 1.f; g.rows_per_gate = 1;
   if (P.conv) {
     g.conv = 1; g.Nimg = P.Nimg; g.H = P.H; g.Wd = P.Wd; g.Cin = P.Cin; g.KH = P.KH; g.KW = P.KH;
