@@ -332,6 +332,55 @@ def bench_vit(args, rank, world):
     }
 
 
+REF_T5_CAPTION_S = 0.20  # reference T5-v1.1-large caption embedding latency, inf2 (cova/README.md:98)
+
+
+def bench_t5(args, rank, world):
+    """T5-v1.1-large mean-pooled embeddings (t5_model_api.py / the cova chain).  One step = one batch of
+    ``--batch`` captions padded to ``--prompt-len`` tokens (the server's ``max_new_tokens``); the reference's
+    single-request caption / prompt embedding latencies (0.20 s / 0.09 s, inf2) are matched by the p50 of
+    single requests at the same length.  Eager encoder (no graph), tokenizer on the host included."""
+    import numpy as np
+    import torch
+    from shai_amd.engines.encoders import TextEmbeddingEngine
+    from shai_amd.models.t5 import T5Config
+
+    eng = TextEmbeddingEngine(T5Config.v1_1_large(), device="cuda", seed=rank)
+    L = args.prompt_len
+    caption = ("a photograph of an astronaut riding a horse on the surface of mars, dramatic lighting, "
+               "red dust, highly detailed")
+    texts = [caption] * args.batch
+    for _ in range(max(1, args.warmup)):
+        eng.embed(texts, L)
+        eng.embed(texts[:1], L)
+    lat = []
+    for _ in range(max(args.latency_runs, 5)):  # single-request latency (reference semantics), untimed
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e = eng.embed(texts[:1], L)
+        lat.append(time.perf_counter() - t0)
+    _barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        e = eng.embed(texts, L)
+    _barrier(world)
+    elapsed = _max_over_ranks(time.perf_counter() - t0, world)
+    p50 = statistics.median(lat)
+    return {
+        "metric": "T5-v1.1-large embeddings/sec (mean-pooled, %d tokens)" % L, "value": round(args.batch * args.steps * world / elapsed, 2),
+        "unit": "embeddings/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": round(REF_T5_CAPTION_S / p50, 3), "dtype": "bf16",
+        "data": "synthetic caption, random-init weights (full T5-v1.1-large encoder)",
+        "config": {"model": "google/t5-v1_1-large (encoder architecture)", "global_batch": args.batch * world,
+                   "per_gpu_batch": args.batch, "seq_len": L, "parallelism": f"dp{world}"},
+        "p50_latency_ms_bs1": round(1000 * p50, 2),
+        "embedding_dim": int(e.shape[-1]), "outputs_finite": bool(np.isfinite(e).all()),
+        "baseline_note": "vs_baseline = 0.20 s (reference T5 caption embedding latency, inf2, cova/README.md:98) / our "
+                         "p50 single-request latency",
+    }
+
+
 def bench_mistral(args, rank, world):
     import torch
     from shai_amd.engines.llm import bench_decode_throughput
@@ -343,7 +392,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="sd21", choices=["sd21", "mistral", "flux", "mllama", "vit"])
+    ap.add_argument("--workload", default="sd21", choices=["sd21", "mistral", "flux", "mllama", "vit", "t5"])
     ap.add_argument("--batch", type=int, default=None,
                     help="per-GPU batch: images per step (sd21: 32, flux: 1) / concurrent sequences (mistral: 64, "
                          "mllama: 8)")
@@ -372,12 +421,12 @@ def main():
     if args.tp is None:
         args.tp = args.gpus if args.workload in ("mistral", "mllama") else 1
     if args.batch is None:  # dynamic-batching caps a serving replica would use for each workload
-        args.batch = {"sd21": 32, "mistral": 64, "flux": 1, "mllama": 8, "vit": 32}[args.workload]
+        args.batch = {"sd21": 32, "mistral": 64, "flux": 1, "mllama": 8, "vit": 32, "t5": 32}[args.workload]
     import torch
     rank, world, local = _dist_init(args.gpus)
     with torch.inference_mode():
         fn = {"sd21": bench_sd21, "mistral": bench_mistral, "flux": bench_flux,
-              "mllama": bench_mllama, "vit": bench_vit}[args.workload]
+              "mllama": bench_mllama, "vit": bench_vit, "t5": bench_t5}[args.workload]
         res = fn(args, rank, world)
     if DEVICE == "cpu":
         res["data"] = "CPU DRY RUN (tiny config, gloo): plumbing check, not a measurement"
