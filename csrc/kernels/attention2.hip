@@ -122,13 +122,13 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
   // D = 64 (softmax-issue-bound): Q is pre-multiplied by scale * log2(e) and the score accumulators start at
   // -m (the running max they are computed against), so the fast path's exponent is the raw accumulator --
   // one v_exp per score, no v_fma.  Costs one bf16 rounding of the scaled Q (|rel| <= 2^-9 per element).
-  constexpr bool PRE = D == 64 && !(EXP & 16);  // EXP & 16: the unscaled form (A/B: SHAI_FLASH2_PRE=0)
+  constexpr bool PRE = !(EXP & 16);  // EXP & 16: the unscaled form (A/B: SHAI_FLASH2_PRE=0)
   // D = 64 M segment (EXP & 32 restores the previous form for A/B): (a) every LDS fragment read is an immediate
   // offset from one of six per-tile base addresses (was one v_add per read: 29 VALU per tile); (b) the score
   // accumulators start at zero (inline constant) and -m enters through one extra MFMA per 32-key block,
   // A = a ones column, B = -m on the bf16 grid (was 32 v_mov per tile).  VALU issue, not the matrix pipe,
   // bounds this loop at D = 64 (profiles/flash_attn_v2_round2.md), so 2 MFMAs buy back ~60 VALU.
-  constexpr bool NEWM = PRE && !(EXP & 32);
+  constexpr bool NEWM = PRE && !(EXP & 32);  // D = 64 and D = 128
   static_assert(NPW >= 1 && (2 * NPI) % 8 == 0, "bad D");
   extern __shared__ __attribute__((aligned(16))) bf16_t f2_smem[];
 
@@ -381,7 +381,7 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
     stamp();
     stage(t + 3);
     s4a vr0[ND][2][2], vr1[ND][2][2];
-    if constexpr (NEWM) {
+    if constexpr (NEWM && D == 64) {
       const bool more = t + 1 < nt;
       const uint32_t kslot = lds0 + (uint32_t)(((t + 1) & 3) * TILE * 2);
       const uint32_t vslot = lds0 + (uint32_t)((t & 3) * TILE * 2);
@@ -433,6 +433,60 @@ __global__ void __launch_bounds__(512) flash2_kernel(const AttnArgs p) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // V^T kb1
       __builtin_amdgcn_sched_barrier(0);
       if (!(EXP & 2)) pv_mfma(1, vr1);
+    } else if constexpr (NEWM) {  // D = 128
+      // Same scheme at D = 128 (8 K fragments and 16 transposed V reads per 32-key block): reads issued in
+      // consumption order in groups of 8 so that at most 16 are outstanding (lgkmcnt counts to 15), each group
+      // waited for by a counted lgkmcnt before the MFMAs that consume it.  Row = 256 B: key block 8192 B,
+      // 16-row V half 4096 B, 8-row V step 2048 B -- all immediates.
+      const bool more = t + 1 < nt;
+      const uint32_t kslot = lds0 + (uint32_t)(((t + 1) & 3) * TILE * 2);
+      const uint32_t vslot = lds0 + (uint32_t)((t & 3) * TILE * 2);
+      uint32_t ka[NS], va[ND];
+#pragma unroll
+      for (int s2 = 0; s2 < NS; ++s2) ka[s2] = kslot + kofs[s2];
+#pragma unroll
+      for (int d = 0; d < ND; ++d) va[d] = vslot + vofs[d];
+      bf16x8a kf[NS];
+#define F2_K(KB)                                                                                       \
+  kf[0] = f2_b128_read_o<(KB) * 8192>(ka[0]); kf[1] = f2_b128_read_o<(KB) * 8192>(ka[1]);             \
+  kf[2] = f2_b128_read_o<(KB) * 8192>(ka[2]); kf[3] = f2_b128_read_o<(KB) * 8192>(ka[3]);             \
+  kf[4] = f2_b128_read_o<(KB) * 8192>(ka[4]); kf[5] = f2_b128_read_o<(KB) * 8192>(ka[5]);             \
+  kf[6] = f2_b128_read_o<(KB) * 8192>(ka[6]); kf[7] = f2_b128_read_o<(KB) * 8192>(ka[7]);
+#define F2_VR(VR, KB, D_)                                   \
+  VR[D_][0][0] = f2_tr_read_o<(KB) * 8192 + 0>(va[D_]);    \
+  VR[D_][0][1] = f2_tr_read_o<(KB) * 8192 + 2048>(va[D_]); \
+  VR[D_][1][0] = f2_tr_read_o<(KB) * 8192 + 4096>(va[D_]); \
+  VR[D_][1][1] = f2_tr_read_o<(KB) * 8192 + 6144>(va[D_]);
+#define F2_QK(KB)                                                                                               \
+  if (!(EXP & 2) && more) {                                                                                     \
+    const float16_ z = {};                                                                                      \
+    sacc[KB] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, b_negm, z, 0, 0, 0);                              \
+    _Pragma("unroll") for (int s2 = 0; s2 < NS; ++s2)                                                           \
+      sacc[KB] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s2], qf[s2], sacc[KB], 0, 0, 0);                   \
+  }
+#define F2_WAIT(N)                                             \
+  __builtin_amdgcn_sched_barrier(0);                           \
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");  \
+  __builtin_amdgcn_sched_barrier(0);
+      F2_K(0)                    // [K0]
+      F2_VR(vr0, 0, 0) F2_VR(vr0, 0, 1)  // [K0 | V0 d0-1]
+      F2_WAIT(8)
+      F2_QK(0)
+      F2_K(1)                    // [V0 d0-1 | K1]
+      F2_WAIT(8)
+      F2_VR(vr0, 0, 2) F2_VR(vr0, 0, 3)  // [K1 | V0 d2-3]
+      F2_WAIT(8)
+      F2_QK(1)
+      F2_VR(vr1, 1, 0) F2_VR(vr1, 1, 1)  // [V0 d2-3 | V1 d0-1]
+      F2_WAIT(8)
+      if (!(EXP & 2)) pv_mfma(0, vr0);
+      F2_VR(vr1, 1, 2) F2_VR(vr1, 1, 3)  // [V1 d0-1 | V1 d2-3]
+      F2_WAIT(0)
+      if (!(EXP & 2)) pv_mfma(1, vr1);
+#undef F2_WAIT
+#undef F2_QK
+#undef F2_VR
+#undef F2_K
     } else if constexpr (D == 64) {
       // every fragment read issued by asm in consumption order (K kb0, K kb1, V^T kb0 | V^T kb1), counted
       // lgkmcnt waits before each 4-MFMA group (LDS returns in order; at most 15 outstanding)
@@ -573,7 +627,7 @@ void launch_flash2_exp(const AttnArgs& a, int exp, hipStream_t s) {
     else flash2_kernel<64, false, E><<<grid, 512, lds, s>>>(a);              \
     break;
   switch (exp) {
-    SHAI_F2X(0) SHAI_F2X(1) SHAI_F2X(2) SHAI_F2X(4) SHAI_F2X(8) SHAI_F2X(12) SHAI_F2X(32)
+    SHAI_F2X(0) SHAI_F2X(1) SHAI_F2X(2) SHAI_F2X(4) SHAI_F2X(8) SHAI_F2X(12) SHAI_F2X(32) SHAI_F2X(48)
     default: break;
   }
 #undef SHAI_F2X
