@@ -451,22 +451,45 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const float* __restric
   gn_finalize_image(part, gamma, beta, scale, shift, blockIdx.x, HW, C, G, NB, eps, false);
 }
 
+// Apply pass, y = (silu)(x * scale[n, c] + shift[n, c]) over channels-last [N, HW, C] (two sources: channels
+// [0, C1) from x, [C1, C) from x2).  The launcher makes the grid's thread count a multiple of C / 8, so every
+// thread keeps ONE 8-channel vector for the whole grid-stride loop: its scale / shift (4 x 16 B) are loaded once
+// per image instead of once per 16 B of x, and the pixel index advances by a constant -- no 64-bit division per
+// element group (both dominated the old loop's issue).
 __global__ void __launch_bounds__(256) gn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ x2,
                                                        int C1, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, bf16_t* __restrict__ out,
                                                        long total8, int HW, int C, int silu) {
   const int C8 = C >> 3, C18 = C1 >> 3, C28 = (C - C1) >> 3;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total8; i += (long)gridDim.x * blockDim.x) {
-    const long pix = i / C8;
-    const int cv = (int)(i - pix * C8);
-    const int n = (int)(pix / HW);
-    float f[8];
-    if (cv < C18) unpack8(reinterpret_cast<const uint4_*>(x)[pix * C18 + cv], f);  // (x2 == null: C1 == C)
-    else unpack8(reinterpret_cast<const uint4_*>(x2)[pix * C28 + (cv - C18)], f);
+  const long stride = (long)gridDim.x * blockDim.x;  // a multiple of C8
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= total8) return;
+  const int cv = (int)(i % C8);
+  long pix = i / C8;
+  const long pstep = stride / C8;
+  int n = (int)(pix / HW);
+  long next = (long)(n + 1) * HW;
+  const bool first = cv < C18;
+  const uint4_* src = first ? reinterpret_cast<const uint4_*>(x) + cv : reinterpret_cast<const uint4_*>(x2) + (cv - C18);
+  const int srcw = first ? C18 : C28;
+  float4_ a0, a1, b0, b1;
+  auto load_ss = [&]() {
     const float* sc = scale + (long)n * C + cv * 8;
     const float* sh = shift + (long)n * C + cv * 8;
-    const float4_ a0 = *reinterpret_cast<const float4_*>(sc), a1 = *reinterpret_cast<const float4_*>(sc + 4);
-    const float4_ b0 = *reinterpret_cast<const float4_*>(sh), b1 = *reinterpret_cast<const float4_*>(sh + 4);
+    a0 = *reinterpret_cast<const float4_*>(sc);
+    a1 = *reinterpret_cast<const float4_*>(sc + 4);
+    b0 = *reinterpret_cast<const float4_*>(sh);
+    b1 = *reinterpret_cast<const float4_*>(sh + 4);
+  };
+  load_ss();
+  for (; i < total8; i += stride, pix += pstep) {
+    if (pix >= next) {  // crossed into another image (rare unless HW is small)
+      n = (int)(pix / HW);
+      next = (long)(n + 1) * HW;
+      load_ss();
+    }
+    float f[8];
+    unpack8(src[pix * srcw], f);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       f[k] = f[k] * a0[k] + b0[k];
@@ -510,6 +533,12 @@ void launch_groupnorm_apply(const GroupNormArgs& a, hipStream_t s) {
   const long total8 = (long)a.N * a.HW * a.C / 8;
   long blocks = (total8 + 255) / 256;
   if (blocks > 4096) blocks = 4096;
+  // grid threads a multiple of C / 8 (the kernel keeps one channel vector per thread)
+  const int C8 = a.C / 8;
+  int g = C8, b = 256;
+  while (b) { const int t = g % b; g = b; b = t; }  // gcd(C8, 256)
+  const long unit = C8 / g;
+  blocks = (blocks + unit - 1) / unit * unit;
   gn_apply_kernel<<<(int)blocks, 256, 0, s>>>(a.x, a.x2, a.x2 ? a.C1 : a.C, a.scale, a.shift, a.out, total8, a.HW,
                                               a.C, a.silu);
 }
