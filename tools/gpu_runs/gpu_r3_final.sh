@@ -13,7 +13,7 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 tail -1 gpurun_out/r3z_smoke.log | cut -c1-300
 timeout -k 10 500 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r3z_bench_sd21.log 2>&1 || exit $?
 echo "== sd21"; tail -1 gpurun_out/r3z_bench_sd21.log
-for wl in mistral flux vit mllama; do
+for wl in mistral flux vit mllama t5; do
   timeout -k 10 500 python -u bench.py --workload $wl > gpurun_out/r3z_bench_$wl.log 2>&1 || exit $?
   echo "== $wl"; tail -1 gpurun_out/r3z_bench_$wl.log
 done
