@@ -991,11 +991,46 @@ void decode_attn(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, 
 // Fused decode step on the packed QKV rows [B, (h + 2 hk) D]: RoPE on q and k, this step's k / v into the paged
 // cache at slots, attention over the cached context plus the new token (replaces rope_qkv_cache +
 // decode_attn in the decode graph).
+// Decode QKV projection with a folded RMSNorm, left as split-K partials for decode_attn_rope to fold (one launch
+// fewer per layer): the skinny kernel with the tuned K-group count (at least 2), no fold launch.  Returns the fp32
+// workspace [kg][M][N] partials followed by [kg][M] row sums of squares; kg = numel / (M (N + 1)).
+Tensor gemm_partials(const Tensor& a, const Tensor& w, double rms_eps) {
+  check_rows(a, "a");
+  check_rows(w, "w");
+  SHAI_CHECK(a.dim() == 2 && w.dim() == 2 && a.size(1) == w.size(1) && rms_eps >= 0, "gemm_partials: a [M, K], w [N, K]");
+  shai::GemmArgs g{};
+  g.A = cptr(a);
+  g.W = cptr(w);
+  g.M = a.size(0);
+  g.K = a.size(1);
+  g.N = w.size(0);
+  g.lda = a.stride(0);
+  g.ldw = w.stride(0);
+  g.ldc = g.N;
+  g.batch = 1;
+  g.alpha = 1.0;
+  g.res_alpha = 1.0;
+  g.rms = 1;
+  g.rms_eps = (float)rms_eps;
+  SHAI_CHECK(g.K % 8 == 0 && shai::skinny_supported(g), "gemm_partials: problem not supported by the skinny kernel");
+  Choice c{-1, 1};
+  int kg = (lookup_choice(g, gemm_key(g), &c) && (c.cfg == kSkinnyCfg || c.cfg == kSkinnyFixCfg)) ? c.splits
+                                                                                                : shai::skinny_kgroups(g);
+  kg = std::min(std::max(kg, 2), shai::skinny_max_kgroups(g));
+  SHAI_CHECK(kg >= 2, "gemm_partials: K too small for split-K");
+  Tensor ws = at::empty({(long)kg * g.M * (g.N + 1)}, a.options().dtype(at::kFloat));
+  g.C = nullptr;  // partials only: nothing is written to C
+  shai::launch_skinny_kg(g, ws.data_ptr<float>(), kg, stream(), false, false);
+  return ws;
+}
+
 void decode_attn_rope(const Tensor& qkv, const Tensor& k_cache, const Tensor& v_cache, const Tensor& o,
                       const Tensor& block_table, const Tensor& ctx_lens, const Tensor& positions, const Tensor& cos,
                       const Tensor& sin, const Tensor& slots, const Tensor& ws, int64_t h, int64_t hk,
-                      int64_t num_splits, double scale) {
+                      int64_t num_splits, double scale, const optional<Tensor>& qkv_ws, int64_t qkv_kg,
+                      int64_t qkv_k, double qkv_eps) {
   check_bf16(qkv, "qkv");
+  const bool part = qkv_ws.has_value();
   check_rows(o, "o");
   check_bf16(k_cache, "k_cache");
   check_bf16(v_cache, "v_cache");
@@ -1009,12 +1044,25 @@ void decode_attn_rope(const Tensor& qkv, const Tensor& k_cache, const Tensor& v_
   SHAI_CHECK(k_cache.dim() == 4 && k_cache.size(2) == 64 && k_cache.size(1) == hk, "decode_attn_rope cache shape");
   shai::DecodeAttnArgs a{};
   a.D = k_cache.size(3);
-  a.B = qkv.size(0);
+  a.B = part ? o.size(0) : qkv.size(0);
   a.Hq = h;
   a.Hkv = hk;
   SHAI_CHECK(a.D == 64 || a.D == 128, "decode_attn head dim 64/128");
   SHAI_CHECK(a.Hq % a.Hkv == 0 && a.Hq / a.Hkv <= 8, "decode_attn GQA group must be <= 8");
-  SHAI_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) >= (h + 2 * hk) * a.D, "qkv rows");
+  if (part) {  // q / k / v come from the QKV GEMM's split-K partials (gemm_partials); qkv is not read
+    check_f32(*qkv_ws, "qkv_ws");
+    const long n = (h + 2 * hk) * a.D;
+    SHAI_CHECK(qkv_kg >= 2 && qkv_k > 0 && qkv_eps >= 0 &&
+                   qkv_ws->numel() == qkv_kg * (long)a.B * (n + 1),
+               "qkv_ws must be the [kg][B][(h + 2 hk) D] partials + [kg][B] row sums of gemm_partials");
+    a.qkv_ws = qkv_ws->data_ptr<float>();
+    a.qkv_kg = qkv_kg;
+    a.qkv_n = n;
+    a.qkv_k = qkv_k;
+    a.qkv_eps = qkv_eps;
+  } else {
+    SHAI_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) >= (h + 2 * hk) * a.D, "qkv rows");
+  }
   SHAI_CHECK(o.dim() == 2 && o.size(0) == a.B && o.size(1) == h * a.D && o.stride(1) == 1, "o [B, h D]");
   SHAI_CHECK(cos.size(1) == a.D / 2 && sin.sizes() == cos.sizes(), "rope tables [max_pos, D / 2]");
   SHAI_CHECK(positions.numel() >= a.B && slots.numel() >= a.B && ctx_lens.numel() >= a.B, "per-row inputs");
@@ -1320,7 +1368,8 @@ TORCH_LIBRARY(shai, m) {
   m.def("token_feedback(Tensor(a!) ids, Tensor rowmap, Tensor prev) -> ()");
   m.def("decode_attn_rope(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor(c!) o, Tensor block_table, "
         "Tensor ctx_lens, Tensor positions, Tensor cos, Tensor sin, Tensor slots, Tensor(d!) ws, int h, int hk, "
-        "int num_splits, float scale) -> ()");
+        "int num_splits, float scale, Tensor? qkv_ws=None, int qkv_kg=0, int qkv_k=0, float qkv_eps=-1.0) -> ()");
+  m.def("gemm_partials(Tensor a, Tensor w, float rms_eps) -> Tensor");
   m.def("gemm_tuning() -> str[]", &gemm_tuning);
   m.def("gemm_tuning_export() -> str[]", &gemm_tuning_export);
   m.def("gemm_tuning_import(str[] entries) -> int", &gemm_tuning_import);
@@ -1354,4 +1403,5 @@ TORCH_LIBRARY_IMPL(shai, CUDA, m) {
   m.impl("embedding", &embedding);
   m.impl("token_feedback", &token_feedback);
   m.impl("decode_attn_rope", &decode_attn_rope);
+  m.impl("gemm_partials", &gemm_partials);
 }

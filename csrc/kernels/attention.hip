@@ -617,6 +617,39 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
   const int rpos = fused ? p.positions[b] : 0;
   // this step's k / v (fused path, last split) loaded now and consumed after the loop, so their latency is hidden
   const bool new_tok = fused && split == p.num_splits - 1 && p.slots[b] >= 0;
+  // QKV fold fused in: element col of this row = bf16(sum of the kg partial slabs (in slab order, as the fold
+  // adds them) x the folded RMSNorm scale)
+  // This lane's six elements (q halves, k halves, two v) and the row's sum of squares, four slabs per round with
+  // every load issued before the first add (a dependent load-add chain per slab costs ~5 us per layer).
+  const bool part = p.qkv_ws != nullptr;
+  float pv[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (part) {
+    const long pslab = (long)p.B * p.qkv_n;
+    const int lq = lane & (D / 2 - 1), kcol = (p.Hq + hk) * D, vcol = (p.Hq + p.Hkv + hk) * D;
+    const int col[6] = {hq * D + lq, hq * D + lq + D / 2, kcol + lq, kcol + lq + D / 2,
+                        D == 128 ? vcol + 2 * lane : vcol + lane, D == 128 ? vcol + 2 * lane + 1 : vcol + lane};
+    const float* row = p.qkv_ws + (long)b * p.qkv_n;
+    const float* ssr = p.qkv_ws + (long)p.qkv_kg * pslab + b;
+    for (int s0 = 0; s0 < p.qkv_kg; s0 += 4) {
+      float t[4][7];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int sl = min(s0 + u, p.qkv_kg - 1);  // past the last slab: re-read it, dropped below
+#pragma unroll
+        for (int e = 0; e < 6; ++e) t[u][e] = row[(long)sl * pslab + col[e]];
+        t[u][6] = ssr[(long)sl * p.B];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (s0 + u < p.qkv_kg) {
+#pragma unroll
+          for (int e = 0; e < 7; ++e) pv[e] += t[u][e];
+        }
+    }
+    const float rstd = rsqrtf(pv[6] / p.qkv_k + p.qkv_eps);
+#pragma unroll
+    for (int e = 0; e < 6; ++e) pv[e] = bf2f(f2bf(pv[e] * rstd));
+  }
   float kn0 = 0.f, kn1 = 0.f, kc0 = 0.f, ks0 = 0.f;
   uint32_t vn_pair = 0u;
   float vn_one = 0.f;
@@ -624,20 +657,26 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
     const bf16_t* kn = p.knew + (long)b * p.new_bs + (long)hk * D;
     const bf16_t* vn = p.vnew + (long)b * p.new_bs + (long)hk * D;
     if (lane < D / 2) {
-      kn0 = bf2f(kn[lane]);
-      kn1 = bf2f(kn[lane + D / 2]);
+      kn0 = part ? pv[2] : bf2f(kn[lane]);
+      kn1 = part ? pv[3] : bf2f(kn[lane + D / 2]);
       kc0 = p.rope_cos[(long)rpos * (D / 2) + lane];
       ks0 = p.rope_sin[(long)rpos * (D / 2) + lane];
     }
-    if constexpr (D == 128) vn_pair = *reinterpret_cast<const uint32_t*>(vn + 2 * lane);
-    else vn_one = bf2f(vn[lane]);
+    if constexpr (D == 128) {
+      vn_pair = part ? pack2(pv[4], pv[5])
+                     : *reinterpret_cast<const uint32_t*>(vn + 2 * lane);
+    } else {
+      vn_one = part ? pv[4] : bf2f(vn[lane]);
+    }
   }
   if (fused) {  // NeoX RoPE on q (f32 math, bf16 result: what rope_qkv_cache would have stored)
     const bf16_t* qs = p.q + (long)b * p.q_bs + (long)hq * D;
     const float* cp = p.rope_cos + (long)rpos * (D / 2);
     const float* sp = p.rope_sin + (long)rpos * (D / 2);
     for (int i = lane; i < D / 2; i += 64) {
-      const float x0 = bf2f(qs[i]), x1 = bf2f(qs[i + D / 2]), c = cp[i], sn = sp[i];
+      const float x0 = part ? pv[0] : bf2f(qs[i]);  // (i == lane: one pass)
+      const float x1 = part ? pv[1] : bf2f(qs[i + D / 2]);
+      const float c = cp[i], sn = sp[i];
       sQb[w * D + i] = f2bf(x0 * c - x1 * sn);
       sQb[w * D + i + D / 2] = f2bf(x1 * c + x0 * sn);
     }
@@ -759,8 +798,9 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
         kc[dst + lane] = f2bf(kr0);
         kc[dst + lane + D / 2] = f2bf(kr1);
       }
-      const bf16_t* vn = p.vnew + (long)b * p.new_bs + (long)hk * D;
-      for (int i = lane; i < D; i += 64) vc[dst + i] = vn[i];
+      // v from registers (the values attended above; bf16-exact)
+      if constexpr (D == 128) *reinterpret_cast<uint32_t*>(vc + dst + 2 * lane) = vn_pair;
+      else vc[dst + lane] = f2bf(vn_one);
     }
   }
   if (p.num_splits == 1) {  // no split-K: normalise and write the output here (no combine launch)

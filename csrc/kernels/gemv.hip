@@ -553,7 +553,7 @@ static void launch_skinny_mb(const GemmArgs& a, float* ws, int kg, unsigned* cnt
 }
 
 // kg K groups (split-K over workgroups; needs ws of skinny_workspace_bytes_kg, else kg = 1)
-void launch_skinny_kg(const GemmArgs& a_in, float* ws, int kg, hipStream_t s, bool fixup) {
+void launch_skinny_kg(const GemmArgs& a_in, float* ws, int kg, hipStream_t s, bool fixup, bool fold) {
   static const int nt = [] {
     const char* e = getenv("SHAI_SKINNY_NT");
     return e ? atoi(e) : 1;
@@ -573,7 +573,7 @@ void launch_skinny_kg(const GemmArgs& a_in, float* ws, int kg, hipStream_t s, bo
     if (a.M <= 32) launch_skinny_mb<32, false>(a, ws, kg, cnt, s);
     else launch_skinny_mb<64, false>(a, ws, kg, cnt, s);
   }
-  if (kg > 1 && cnt == nullptr) launch_splitk_epilogue(a, ws, kg, s);
+  if (kg > 1 && cnt == nullptr && fold) launch_splitk_epilogue(a, ws, kg, s);
 }
 
 void launch_skinny(const GemmArgs& a, float* ws, hipStream_t s) {

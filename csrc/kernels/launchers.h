@@ -154,7 +154,8 @@ int skinny_max_kgroups(const GemmArgs& a);    // largest K-group count worth try
 size_t skinny_workspace_bytes(const GemmArgs& a);
 size_t skinny_workspace_bytes_kg(const GemmArgs& a, int kg);
 void launch_skinny(const GemmArgs& a, float* ws, hipStream_t s);
-void launch_skinny_kg(const GemmArgs& a, float* ws, int kg, hipStream_t s, bool fixup = false);
+// fold = false (kg > 1, no fixup): leave the fp32 partials in ws for a consumer kernel (no fold launch)
+void launch_skinny_kg(const GemmArgs& a, float* ws, int kg, hipStream_t s, bool fixup = false, bool fold = true);
 // this launch's slice of the in-kernel split-K arrival tickets (nullptr: none available -> no fixup)
 unsigned* skinny_ticket_slice(hipStream_t s, int ntiles);
 // skinny2 (gemv2.hip): 128-row W tiles, whole K-step per wave, M <= 64, bf16 weights; split-K always fixed up
@@ -214,6 +215,12 @@ struct DecodeAttnArgs {
   const float* rope_cos;    // [max_pos, D / 2] NeoX halves
   const float* rope_sin;
   const int* slots;
+  // QKV GEMM fold fused in (qkv_ws != nullptr): q / k / v are read as the sum of qkv_kg fp32 split-K partial slabs
+  // [kg][B][qkv_n] of the skinny kernel, times the folded-RMSNorm row scale from the [kg][B] row sums of squares
+  // (qkv_k = the GEMM's K, qkv_eps its epsilon), rounded to bf16 -- what the separate fold would have stored
+  const float* qkv_ws;
+  int qkv_kg, qkv_n, qkv_k;
+  float qkv_eps;
 };
 void launch_decode_attn(const DecodeAttnArgs& a, hipStream_t s);
 size_t decode_attn_workspace(int B, int Hq, int D, int num_splits);

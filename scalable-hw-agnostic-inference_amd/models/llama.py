@@ -33,6 +33,9 @@ from .layers import GLULinear, RMSNorm
 # decode steps run RoPE + the KV-cache write inside the paged decode-attention kernel (one launch per layer
 # instead of two); SHAI_FUSED_DECODE=0 keeps the separate rope_qkv_cache launch
 FUSED_DECODE = os.environ.get("SHAI_FUSED_DECODE", "1") != "0"
+# decode with the norm folded into qkv_proj: the QKV GEMM's split-K fold runs inside the attention kernel
+# (one launch fewer per layer); SHAI_QKV_FOLD_IN_ATTN=0 keeps the GEMM's own fold launch
+QKV_FOLD_IN_ATTN = os.environ.get("SHAI_QKV_FOLD_IN_ATTN", "1") != "0"
 
 KV_BLOCK = 64
 
@@ -159,8 +162,16 @@ class LlamaAttention(nn.Module):
 
     def forward(self, x, batch: Batch, k_cache, v_cache, cos, sin, residual=None, rms_eps=None):
         T = x.shape[0]
-        qkv = self.qkv_proj(x, rms_eps=rms_eps)  # [T, (h + 2hk) * hd]
         h, hk, hd = self.h, self.hk, self.hd
+        qp = self.qkv_proj
+        if (not batch.is_prefill and FUSED_DECODE and QKV_FOLD_IN_ATTN and rms_eps is not None and x.is_cuda
+                and T <= 64 and qp.bias is None and qp.w_scale is None and qp.weight.dtype == torch.bfloat16
+                and x.is_contiguous() and x.shape[1] >= 2048):
+            o = ops.decode_attention_rope_qkv(x, qp.weight, rms_eps, k_cache, v_cache, batch.block_table,
+                                              batch.ctx_lens, batch.positions, cos, sin, batch.slots, h, hk,
+                                              self.scale, num_splits=batch.num_splits)
+            return self.o_proj(o, residual=residual)
+        qkv = qp(x, rms_eps=rms_eps)  # [T, (h + 2hk) * hd]
         if not batch.is_prefill and FUSED_DECODE:  # RoPE + KV-cache write inside the decode attention kernel
             o = ops.decode_attention_rope(qkv, k_cache, v_cache, batch.block_table, batch.ctx_lens, batch.positions,
                                           cos, sin, batch.slots, h, hk, self.scale, num_splits=batch.num_splits)

@@ -24,7 +24,7 @@ from .reference import (ACT_GELU, ACT_GELU_TANH, ACT_NONE, ACT_QUICK_GELU, ACT_R
 __all__ = [
     "rmsnorm", "layernorm", "groupnorm_stats", "groupnorm_apply", "groupnorm", "linear", "conv2d", "attention",
     "paged_attention", "decode_attention", "kv_write", "rope", "rope_pairs", "gated_act", "bias_act", "sched_step",
-    "softmax_", "embedding", "token_feedback", "decode_attention_rope", "quantize_fp8_rows", "dequant_fp8", "quant_rows_fp8", "gemm_f8", "pack_conv_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
+    "softmax_", "embedding", "token_feedback", "decode_attention_rope", "decode_attention_rope_qkv", "gemm_partials", "quantize_fp8_rows", "dequant_fp8", "quant_rows_fp8", "gemm_f8", "pack_conv_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
     "ACT_GELU_TANH", "ACT_QUICK_GELU", "ACT_RELU", "decode_splits",
 ]
 
@@ -400,6 +400,37 @@ def decode_attention_rope(qkv, k_cache, v_cache, block_table, ctx_lens, position
     o = out if out is not None else torch.empty(B, h * D, dtype=qkv.dtype, device=qkv.device)
     _K().decode_attn_rope(qkv, k_cache, v_cache, o, _i32(block_table), _i32(ctx_lens), _i32(positions), cos, sin,
                           _i32(slots), ws, int(h), int(hk), int(num_splits), float(scale))
+    return o
+
+
+def gemm_partials(x, w, rms_eps: float) -> torch.Tensor:
+    """Decode-shaped x [M <= 64, K] times w [N, K]^T with the folded RMSNorm of x, left UNFOLDED: the skinny
+    kernel's split-K fp32 partials [kg][M][N] followed by the [kg][M] row sums of squares (kg = numel / (M (N + 1)),
+    at least 2).  decode_attention_rope_qkv folds them (no separate reduce launch)."""
+    return _K().gemm_partials(x, w, float(rms_eps))
+
+
+def decode_attention_rope_qkv(x, w_qkv, rms_eps: float, k_cache, v_cache, block_table, ctx_lens, positions, cos, sin,
+                              slots, h: int, hk: int, scale=None, num_splits: Optional[int] = None, out=None):
+    """decode_attention_rope on qkv = linear(rmsnorm(x), w_qkv) (norm gain folded into w_qkv) with the QKV GEMM's
+    split-K fold done inside the attention kernel.  Same values as the two-step form: the kernel adds the partial
+    slabs in the fold's order and rounds q / k / v to bf16 as the fold's epilogue does.  Returns [B, h D]."""
+    if not _gpu(x):
+        return decode_attention_rope(linear(x, w_qkv, rms_eps=rms_eps), k_cache, v_cache, block_table, ctx_lens,
+                                     positions, cos, sin, slots, h, hk, scale, num_splits, out=out)
+    D = k_cache.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    B, K = x.shape
+    N = w_qkv.shape[0]
+    if num_splits is None:
+        num_splits = decode_splits(B, hk, block_table.shape[1] * 64)
+    part = gemm_partials(x, w_qkv, rms_eps)
+    kg = part.numel() // (B * (N + 1))
+    ws = torch.empty(B * h * num_splits * (D + 2), dtype=torch.float32, device=x.device)
+    o = out if out is not None else torch.empty(B, h * D, dtype=x.dtype, device=x.device)
+    _K().decode_attn_rope(o, k_cache, v_cache, o, _i32(block_table), _i32(ctx_lens), _i32(positions), cos, sin,
+                          _i32(slots), ws, int(h), int(hk), int(num_splits), float(scale), part, int(kg), int(K),
+                          float(rms_eps))
     return o
 
 

@@ -259,6 +259,49 @@ def test_fused_decode_rope_attention(cuda, D, H, Hk, splits):
     assert _rel(o[:-1], want.reshape(B, H * D)[:-1]) < 1e-2
 
 
+@pytest.mark.parametrize("D,H,Hk", [(128, 32, 8), (64, 8, 2)])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_decode_attention_with_qkv_fold_in_kernel(cuda, D, H, Hk, splits):
+    """decode_attention_rope_qkv (QKV GEMM left as split-K partials, folded with the RMSNorm scale inside the decode
+    attention kernel) equals the two-step form -- skinny GEMM with the same K-group count and its fold launch, then
+    decode_attention_rope -- bit for bit: same output, same KV-cache contents, padding row writes nothing."""
+    torch.manual_seed(7 * D + splits)
+    ctx = [1, 2, 64, 65, 300, 1000, 1]
+    B, nb, K, eps = len(ctx), 40, 2048, 1e-5
+    N = (H + 2 * Hk) * D
+    x = torch.randn(B, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
+    ang = torch.rand(1024, D // 2, device=cuda) * 3
+    cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
+    kc = torch.randn(nb, Hk, 64, D, device=cuda).bfloat16()
+    vc = torch.randn(nb, Hk, 64, D, device=cuda).bfloat16()
+    perm = torch.randperm(nb, device=cuda).int()
+    bt = torch.zeros(B, 16, dtype=torch.int32, device=cuda)
+    i = 0
+    for b, c in enumerate(ctx):
+        n = (c + 63) // 64
+        bt[b, :n] = perm[i:i + n]
+        i += n
+    lens = torch.tensor(ctx, dtype=torch.int32, device=cuda)
+    pos = lens - 1
+    slots = torch.stack([bt[b, (c - 1) // 64] * 64 + (c - 1) % 64 for b, c in enumerate(ctx)]).int()
+    slots[-1] = -1
+    part = ops.gemm_partials(x, w, eps)
+    kg = part.numel() // (B * (N + 1))
+    assert kg >= 2 and part.numel() == kg * B * (N + 1)
+    qkv = torch.empty(B, N, device=cuda, dtype=torch.bfloat16)
+    ops.gemm_into(x, w, qkv, force_cfg=SKINNY + kg, rms_eps=eps)
+    # the partials themselves: fp32 reference fold of the slabs
+    slabs = part[:kg * B * N].view(kg, B, N).sum(0)
+    rstd = torch.rsqrt(part[kg * B * N:].view(kg, B).sum(0) / K + eps)
+    assert _rel((slabs * rstd[:, None]).bfloat16(), qkv) < 1e-3
+    kc2, vc2 = kc.clone(), vc.clone()
+    o = ops.decode_attention_rope_qkv(x, w, eps, kc, vc, bt, lens, pos, cos, sin, slots, H, Hk, num_splits=splits)
+    want = ops.decode_attention_rope(qkv, kc2, vc2, bt, lens, pos, cos, sin, slots, H, Hk, num_splits=splits)
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    assert torch.equal(o[:-1], want[:-1])
+
+
 def test_skinny_fixup_concurrent_streams_and_many_tiles(cuda):
     """In-kernel split-K fixups running at the same time on two streams (each stream owns its ticket slice),
     many back-to-back launches with tiles * K groups large (448 tiles x 16 groups), and a graph replayed
