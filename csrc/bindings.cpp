@@ -1016,6 +1016,11 @@ Tensor gemm_partials(const Tensor& a, const Tensor& w, double rms_eps) {
   Choice c{-1, 1};
   int kg = (lookup_choice(g, gemm_key(g), &c) && (c.cfg == kSkinnyCfg || c.cfg == kSkinnyFixCfg)) ? c.splits
                                                                                                 : shai::skinny_kgroups(g);
+  static const int env_kg = [] {  // A/B knob: pin the K-group count of the partials
+    const char* e = getenv("SHAI_QKV_PART_KG");
+    return e ? atoi(e) : 0;
+  }();
+  if (env_kg > 0) kg = env_kg;
   kg = std::min(std::max(kg, 2), shai::skinny_max_kgroups(g));
   SHAI_CHECK(kg >= 2, "gemm_partials: K too small for split-K");
   Tensor ws = at::empty({(long)kg * g.M * (g.N + 1)}, a.options().dtype(at::kFloat));
