@@ -243,3 +243,28 @@ def test_sampled_async_matches_sync_with_stops_and_seeds():
     e = mk(True)
     together = e.generate([prompts[0], prompts[1], prompts[3]], seeded)
     assert together[1].output == alone
+
+
+def test_decode_attention_rope_qkv_cpu_fallback_matches_two_step():
+    """CPU path of ops.decode_attention_rope_qkv (the fused QKV-fold decode op) = linear with the folded RMSNorm
+    followed by decode_attention_rope: same output, same KV-cache writes."""
+    import torch
+    from shai_amd import ops
+    torch.manual_seed(0)
+    B, K, H, Hk, D, nb = 3, 64, 4, 2, 16, 8
+    x = torch.randn(B, K).bfloat16()
+    w = (torch.randn((H + 2 * Hk) * D, K) / K ** 0.5).bfloat16()
+    ang = torch.rand(256, D // 2) * 3
+    cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
+    kc = torch.randn(nb, Hk, 64, D).bfloat16()
+    vc = torch.randn(nb, Hk, 64, D).bfloat16()
+    bt = torch.tensor([[0, 1], [2, 3], [4, 5]], dtype=torch.int32)
+    lens = torch.tensor([5, 70, 1], dtype=torch.int32)
+    pos = lens - 1
+    slots = torch.stack([bt[b, (int(c) - 1) // 64] * 64 + (int(c) - 1) % 64 for b, c in enumerate(lens)]).int()
+    kc2, vc2 = kc.clone(), vc.clone()
+    o = ops.decode_attention_rope_qkv(x, w, 1e-5, kc, vc, bt, lens, pos, cos, sin, slots, H, Hk)
+    qkv = ops.linear(x, w, rms_eps=1e-5)
+    want = ops.decode_attention_rope(qkv, kc2, vc2, bt, lens, pos, cos, sin, slots, H, Hk)
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    assert torch.allclose(o.float(), want.float(), atol=1e-2, rtol=1e-2)
