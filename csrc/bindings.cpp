@@ -1034,8 +1034,8 @@ void decode_attn_rope(const Tensor& qkv, const Tensor& k_cache, const Tensor& v_
                       const Tensor& sin, const Tensor& slots, const Tensor& ws, int64_t h, int64_t hk,
                       int64_t num_splits, double scale, const optional<Tensor>& qkv_ws, int64_t qkv_kg,
                       int64_t qkv_k, double qkv_eps) {
-  check_bf16(qkv, "qkv");
   const bool part = qkv_ws.has_value();
+  if (!part) check_bf16(qkv, "qkv");  // partials path: qkv is a placeholder (the partials), never read
   check_rows(o, "o");
   check_bf16(k_cache, "k_cache");
   check_bf16(v_cache, "v_cache");
@@ -1071,11 +1071,18 @@ void decode_attn_rope(const Tensor& qkv, const Tensor& k_cache, const Tensor& v_
   SHAI_CHECK(o.dim() == 2 && o.size(0) == a.B && o.size(1) == h * a.D && o.stride(1) == 1, "o [B, h D]");
   SHAI_CHECK(cos.size(1) == a.D / 2 && sin.sizes() == cos.sizes(), "rope tables [max_pos, D / 2]");
   SHAI_CHECK(positions.numel() >= a.B && slots.numel() >= a.B && ctx_lens.numel() >= a.B, "per-row inputs");
-  const shai::bf16_t* base = cptr(qkv);
-  a.q = base;
-  a.knew = base + h * a.D;
-  a.vnew = base + (h + hk) * a.D;
-  a.q_bs = a.new_bs = qkv.stride(0);
+  if (part) {
+    // q / k / v come from the partials; knew != nullptr only selects the fused RoPE / KV-write path
+    const shai::bf16_t* flag = reinterpret_cast<const shai::bf16_t*>(a.qkv_ws);
+    a.q = a.knew = a.vnew = flag;
+    a.q_bs = a.new_bs = 0;
+  } else {
+    const shai::bf16_t* base = cptr(qkv);
+    a.q = base;
+    a.knew = base + h * a.D;
+    a.vnew = base + (h + hk) * a.D;
+    a.q_bs = a.new_bs = qkv.stride(0);
+  }
   a.o = mptr(o);
   a.o_bs = o.stride(0);
   a.k_cache = cptr(k_cache);

@@ -63,14 +63,21 @@ def write_ninja(path: str) -> dict:
         f"kflags = {kflags}",
         f"bflags = {bflags}",
         f"rflags = {rflags}",
+        # compiler depfiles (-MD -MF): an edit to ANY included header (gemm_epilogue.h, ...) rebuilds its users
         "rule hip",
-        "  command = $hipcc $kflags -c $in -o $out",
+        "  command = $hipcc $kflags -MD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
         "  description = HIP $in",
         "rule cxx",
-        "  command = c++ $bflags -c $in -o $out",
+        "  command = c++ $bflags -MD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
         "  description = CXX $in",
         "rule rcxx",
-        "  command = c++ $rflags -c $in -o $out",
+        "  command = c++ $rflags -MD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
         "  description = CXX $in",
         "rule link_kernels",
         f"  command = $hipcc --offload-arch={ARCH} -shared -fPIC $in -o $out -L{tlib} -Wl,-rpath,{tlib} "
@@ -113,6 +120,9 @@ def write_ninja(path: str) -> dict:
     return targets
 
 
+LAST_BUILD: dict = {}
+
+
 def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -> dict:
     if clean and os.path.isdir(BUILD):
         shutil.rmtree(BUILD)
@@ -129,8 +139,28 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
         cmd += ["-j", str(jobs)]
     if verbose:
         cmd.append("-v")
-    subprocess.run(cmd, check=True, cwd=BUILD)
+    r = subprocess.run(cmd, cwd=BUILD, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    sys.stdout.write(r.stdout)
+    if r.returncode != 0:
+        raise subprocess.CalledProcessError(r.returncode, cmd, r.stdout)
+    # what ninja actually did: "[i/n] HIP <src>" per compiled object, "no work to do" when all were reused
+    compiled = [ln.split("] ", 1)[1].split(" ", 1)[1] for ln in r.stdout.splitlines()
+                if ln.startswith("[") and ("] HIP " in ln or "] CXX " in ln)]
+    LAST_BUILD.clear()
+    LAST_BUILD.update(compiled=compiled, linked=sum("] LINK " in ln for ln in r.stdout.splitlines()),
+                      up_to_date="no work to do" in r.stdout)
     return targets
+
+
+def summary() -> str:
+    """One line: whether the last build() compiled objects or reused every one of them."""
+    if not LAST_BUILD:
+        return "native build: not run"
+    if LAST_BUILD["up_to_date"]:
+        return "native build: up to date (all objects reused)"
+    return (f"native build: compiled {len(LAST_BUILD['compiled'])} object(s), relinked {LAST_BUILD['linked']} "
+            f"librar{'y' if LAST_BUILD['linked'] == 1 else 'ies'}: " + ", ".join(
+                os.path.relpath(c, CSRC) if os.path.isabs(c) else c for c in LAST_BUILD["compiled"]))
 
 
 def main():
@@ -142,6 +172,7 @@ def main():
     t = build(a.clean, a.j, a.v)
     for k, v in t.items():
         print(f"{k}: {v}")
+    print(summary())
 
 
 if __name__ == "__main__":

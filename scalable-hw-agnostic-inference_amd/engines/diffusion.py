@@ -191,6 +191,22 @@ class DiffusionRequest:
     finish_time: Optional[float] = None
 
 
+MAX_INFERENCE_STEPS = 1000   # the DDIM training schedule length: more steps than timesteps is meaningless
+
+
+def validate_request(prompt, num_inference_steps) -> None:
+    """Reject a request that cannot run before it touches shared batch state: a non-string prompt would fail the
+    text encoder for every request regrouped with it, and a step count < 1 divides by zero in the schedule."""
+    if not isinstance(prompt, str):
+        raise ValueError(f"prompt must be a string, got {type(prompt).__name__}")
+    try:
+        n = int(num_inference_steps)
+    except (TypeError, ValueError):
+        raise ValueError(f"num_inference_steps must be an integer, got {num_inference_steps!r}") from None
+    if not 1 <= n <= MAX_INFERENCE_STEPS:
+        raise ValueError(f"num_inference_steps must be in [1, {MAX_INFERENCE_STEPS}], got {n}")
+
+
 class StepBatcher:
     """Step-level (continuous) batching for SD2.1: a request joins the running batch at the NEXT denoising-step
     boundary instead of waiting for the whole current batch (50 steps) to finish, and leaves it as soon as its
@@ -224,6 +240,7 @@ class StepBatcher:
     # ------------------------------------------------------------------ requests
     def add(self, prompt: str, num_inference_steps: int = 50, seed: Optional[int] = None,
             negative: str = "") -> DiffusionRequest:
+        validate_request(prompt, num_inference_steps)
         seed = int(seed) if seed is not None else int(time.time_ns() % (2 ** 31))
         r = DiffusionRequest(prompt, self.eng.scheduler.steps(num_inference_steps), seed, negative,
                              arrival=time.perf_counter())

@@ -428,7 +428,8 @@ def decode_attention_rope_qkv(x, w_qkv, rms_eps: float, k_cache, v_cache, block_
     kg = part.numel() // (B * (N + 1))
     ws = torch.empty(B * h * num_splits * (D + 2), dtype=torch.float32, device=x.device)
     o = out if out is not None else torch.empty(B, h * D, dtype=x.dtype, device=x.device)
-    _K().decode_attn_rope(o, k_cache, v_cache, o, _i32(block_table), _i32(ctx_lens), _i32(positions), cos, sin,
+    # qkv slot: the (read-only) partials stand in -- never an alias of the mutated output o
+    _K().decode_attn_rope(part, k_cache, v_cache, o, _i32(block_table), _i32(ctx_lens), _i32(positions), cos, sin,
                           _i32(slots), ws, int(h), int(hk), int(num_splits), float(scale), part, int(kg), int(K),
                           float(rms_eps))
     return o

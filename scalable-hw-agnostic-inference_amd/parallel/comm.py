@@ -48,7 +48,12 @@ def raise_if_p2p_error() -> None:
     """Raise if an xGMI peer collective timed out (a peer never arrived): its output is a partial sum.
     Reads a host-mapped word -- no device synchronisation -- so the engines call it after every step."""
     if _P2P is not None and _P2P.error():
-        raise RuntimeError("xGMI P2P collective timed out waiting for a peer rank: TP group broken")
+        # the error word is never cleared (the peer buffers may hold a half-finished round): the process is
+        # done serving -- /health turns 503 for good and the supervisor restarts the TP group
+        from ..utils.liveness import mark_broken
+        msg = "xGMI P2P collective timed out waiting for a peer rank: TP group broken"
+        mark_broken(msg)
+        raise RuntimeError(msg)
 
 
 def all_reduce(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:

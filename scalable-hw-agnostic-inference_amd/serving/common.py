@@ -308,6 +308,10 @@ def base_app(env: ServerEnv, title: str, spaced: bool, cors: bool = False):
         # liveness, not just "the HTTP server answers": 503 once an engine has had work pending without
         # progress for longer than its hang timeout (utils/liveness.py), so the router drains this replica
         # and the supervisor's watchdog restarts it
+        why = _liveness.broken()
+        if why is not None:
+            from fastapi import HTTPException
+            raise HTTPException(status_code=503, detail=f"replica broken: {why}")
         live = _liveness.worst()
         if live is not None and not live.healthy:
             from fastapi import HTTPException

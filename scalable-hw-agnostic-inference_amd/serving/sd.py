@@ -25,6 +25,7 @@ import time
 from concurrent.futures import Future
 from typing import Optional
 
+from ..engines.diffusion import validate_request
 from .common import METRICS, EngineWorker, ServerEnv, base_app, benchmark, mount_ui, png_b64, run
 
 LOAD_PROMPT = "a photo of an astronaut riding a horse on mars"
@@ -53,6 +54,7 @@ class StepBatchingWorker:
         self.t.start()
 
     def submit(self, prompt: str, steps: int, seed: Optional[int] = None) -> Future:
+        validate_request(prompt, steps)
         f: Future = Future()
         self.live.work_pending()
         self.q.put((prompt, int(steps), seed, f))
@@ -84,7 +86,10 @@ class StepBatchingWorker:
                     except BaseException as e:  # noqa: BLE001
                         f.set_exception(e)
                     continue
-                self._futs[id(b.add(a, steps, seed))] = f
+                try:
+                    self._futs[id(b.add(a, steps, seed))] = f
+                except BaseException as e:  # noqa: BLE001 -- a bad request fails alone, before it joins the batch
+                    f.set_exception(e)
             if not b.has_work():
                 continue
             try:
@@ -104,6 +109,15 @@ class StepBatchingWorker:
             self.live.progress(still_pending=b.has_work() or not self.q.empty())
 
 
+def _check(prompt, steps) -> None:
+    """Route-level validation: a malformed request is a 422 for its caller, never an engine-thread failure."""
+    from fastapi import HTTPException
+    try:
+        validate_request(prompt, steps)
+    except ValueError as e:
+        raise HTTPException(status_code=422, detail=str(e)) from None
+
+
 def create_app(engine=None, env: Optional[ServerEnv] = None, max_batch: Optional[int] = None, title_suffix: str = ""):
     env = env or ServerEnv.from_env(app="sd21", num_inference_steps=50)
     engine = engine or build_engine(env)
@@ -121,6 +135,7 @@ def create_app(engine=None, env: Optional[ServerEnv] = None, max_batch: Optional
     worker = EngineWorker("sd-engine", batch_fn=batch_fn, max_batch=max_batch, max_wait_ms=10.0)
 
     def text2img(prompt: str, steps: Optional[int] = None):
+        validate_request(prompt, steps or env.num_inference_steps)
         t0 = time.time()
         img = worker.submit_batched(int(steps or env.num_inference_steps), prompt).result()
         return img, str(time.time() - t0)
@@ -145,6 +160,7 @@ def create_app(engine=None, env: Optional[ServerEnv] = None, max_batch: Optional
 
     @app.get("/load/{n_runs}/infer/{n_inf}")
     def load(n_runs: int, n_inf: int):
+        _check(LOAD_PROMPT, n_inf)
         t0 = time.time()
         report = benchmark(n_runs, "stable_diffusion_512",
                            lambda: worker.submit_batched(n_inf, LOAD_PROMPT).result(), env.pod_name)
@@ -154,6 +170,7 @@ def create_app(engine=None, env: Optional[ServerEnv] = None, max_batch: Optional
     @app.post("/genimage")
     def generate_image_post(request: dict):
         prompt = request.get("prompt")
+        _check(prompt, env.num_inference_steps)
         img, latency = text2img(prompt)
         METRICS.request_done(env, float(latency))
         return {"prompt": prompt, "response": png_b64(img), "latency": latency}
@@ -170,6 +187,7 @@ def _routes(app, env, text2img, run_load):
 
     @app.get("/load/{n_runs}/infer/{n_inf}")
     def load(n_runs: int, n_inf: int):
+        _check(LOAD_PROMPT, n_inf)
         t0 = time.time()
         report = benchmark(n_runs, "stable_diffusion_512", lambda: run_load(n_inf), env.pod_name)
         METRICS.request_done(env, time.time() - t0)
@@ -178,6 +196,7 @@ def _routes(app, env, text2img, run_load):
     @app.post("/genimage")
     def generate_image_post(request: dict):
         prompt = request.get("prompt")
+        _check(prompt, env.num_inference_steps)
         img, latency = text2img(prompt)
         METRICS.request_done(env, float(latency))
         return {"prompt": prompt, "response": png_b64(img), "latency": latency}

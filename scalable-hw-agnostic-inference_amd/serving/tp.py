@@ -19,7 +19,19 @@ SPMD protocol:
 
 Control messages travel on a separate **gloo** group (host sockets), never on the RCCL
 communicator: an idle follower blocks in a CPU receive, not in a GPU collective, and the leader sends
-a heartbeat every ``HEARTBEAT_S`` seconds so the gloo timeout only fires when the leader is gone.
+a heartbeat every ``HEARTBEAT_S`` seconds.
+
+Failure handling (a TP group is one unit: it serves or it is restarted whole):
+
+* a follower whose call fails with anything but a mirrored input error (``MIRRORED``: the leader raises the
+  same exception on the same inputs and reports it to its client) reports the failure to the leader on a
+  second gloo group and exits non-zero; ``torch.distributed.run`` then stops the other ranks and the
+  supervisor relaunches the group.  The leader's status listener marks the process broken
+  (``utils.liveness.mark_broken``: ``/health`` 503) the moment the report -- or the lost connection of a
+  killed follower -- arrives, so the router drains the replica before the launcher has torn it down;
+* a follower that hears nothing from the leader (no call, no heartbeat) for ``LEADER_TIMEOUT_S``
+  (default 2 x ``HEARTBEAT_S`` + 5 s) while idle takes the leader for dead and exits non-zero (a killed
+  leader's closed socket fails the pending receive at once).
 """
 from __future__ import annotations
 
@@ -27,6 +39,7 @@ import datetime
 import os
 import pickle
 import threading
+import time
 from dataclasses import dataclass
 from typing import Any, Iterable, Optional
 
@@ -39,6 +52,11 @@ _log = get_logger("tp-serving")
 
 CALL, STEP, NOOP, STOP = 1, 2, 3, 4
 HEARTBEAT_S = float(os.environ.get("SHAI_TP_HEARTBEAT_S", "20"))
+LEADER_TIMEOUT_S = float(os.environ.get("SHAI_TP_LEADER_TIMEOUT_S", str(2 * HEARTBEAT_S + 5)))
+# exceptions a follower treats as mirrored on the leader (same inputs, same code -> the leader's client gets
+# the error); anything else is rank-local (OOM, device fault, shard-specific shape) and breaks the group
+MIRRORED = (ValueError, TypeError, KeyError)
+FOLLOWER_FAILED_EXIT = 70
 
 
 class TPChannel:
@@ -49,8 +67,11 @@ class TPChannel:
         self.rank = dist.get_rank()
         self.world = dist.get_world_size()
         self.group = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=timeout_s))
+        # followers -> leader failure reports (point to point, leader receives from any rank)
+        self.status_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(days=7))
         self._lock = threading.Lock()
         self.sent = 0
+        self.stopping = False
 
     @property
     def is_leader(self) -> bool:
@@ -64,6 +85,40 @@ class TPChannel:
             if data:
                 dist.broadcast(torch.frombuffer(bytearray(data), dtype=torch.uint8), 0, group=self.group)
             self.sent += 1
+
+    def report_failure(self, detail: str) -> None:
+        """Follower: tell the leader this rank is failing (best effort; the exit that follows is what counts)."""
+        data = detail.encode()[:4000]
+        dist.send(torch.tensor([self.rank, len(data)], dtype=torch.int64), 0, group=self.status_group)
+        if data:
+            dist.send(torch.frombuffer(bytearray(data), dtype=torch.uint8), 0, group=self.status_group)
+
+    def listen_for_failures(self, on_failure) -> threading.Thread:
+        """Leader: a daemon thread that waits for a follower's failure report (or the loss of its connection,
+        e.g. a killed follower) and calls ``on_failure(detail)`` once."""
+        def loop():
+            while True:
+                hdr = torch.zeros(2, dtype=torch.int64)
+                try:
+                    src = dist.recv(hdr, None, group=self.status_group)
+                    rank, n = (int(v) for v in hdr.tolist())
+                    detail = f"rank {rank}"
+                    if n:
+                        buf = torch.empty(n, dtype=torch.uint8)
+                        dist.recv(buf, src, group=self.status_group)
+                        detail += ": " + buf.numpy().tobytes().decode(errors="replace")
+                except Exception as e:  # noqa: BLE001 -- a peer's socket closed (killed rank) or teardown
+                    if self.stopping:
+                        return
+                    if "imed out" in str(e):
+                        continue
+                    detail = f"lost a TP rank ({type(e).__name__}: {str(e)[:200]})"
+                if not self.stopping:
+                    on_failure(detail)
+                return
+        t = threading.Thread(target=loop, daemon=True, name="tp-status")
+        t.start()
+        return t
 
     def recv(self):
         hdr = torch.zeros(2, dtype=torch.int64)
@@ -98,29 +153,87 @@ class SPMDProxy:
         return call
 
 
-def follow(target, channel: TPChannel, step_fn=None) -> int:
+def _die(code: int) -> None:
+    """Leave NOW: a broken TP rank must not linger in a destructor or a collective that never completes."""
+    import logging
+    import sys
+    logging.shutdown()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(code)
+
+
+class _LeaderWatchdog:
+    """Follower: exits the process when no control message (call, step or heartbeat) arrived for ``timeout_s``
+    while the follower sat idle in its receive (the time a call runs does not count)."""
+
+    def __init__(self, timeout_s: float, on_dead=None):
+        self.timeout_s = timeout_s
+        self.on_dead = on_dead or (lambda: _die(FOLLOWER_FAILED_EXIT))
+        self.idle_since: Optional[float] = None
+        self._stop = threading.Event()
+        if timeout_s > 0:
+            threading.Thread(target=self._loop, daemon=True, name="tp-leader-watchdog").start()
+
+    def _loop(self):
+        while not self._stop.wait(min(1.0, self.timeout_s / 4)):
+            t0 = self.idle_since
+            if t0 is not None and time.monotonic() - t0 > self.timeout_s:
+                _log.error("leader silent: exiting", extra={"event": "leader_lost",
+                                                            "detail": f"{self.timeout_s:.0f}s without a message"})
+                self.on_dead()
+                return
+
+    def stop(self):
+        self._stop.set()
+
+
+def follow(target, channel: TPChannel, step_fn=None, leader_timeout_s: Optional[float] = None) -> int:
     """Follower main loop: execute the leader's calls until STOP.  ``step_fn(payload)`` handles STEP
-    messages (the LLM engine loop).  A call that raises is logged and skipped -- the leader hits the same
-    exception (same inputs, same code) and reports it to its client.  Returns the number of calls run."""
+    messages (the LLM engine loop).  A CALL that raises a ``MIRRORED`` (input) error is logged and skipped --
+    the leader hits the same exception on the same inputs and reports it to its client.  Any other failure is
+    rank-local: it is reported to the leader and the process exits non-zero, so the group is restarted whole
+    instead of running on with mismatched collectives.  Returns the number of calls run."""
     n = 0
-    while True:
-        kind, payload = channel.recv()
-        if kind == STOP:
-            return n
-        if kind == NOOP:
-            continue
-        try:
-            with torch.inference_mode():
-                if kind == CALL:
-                    from ..parallel.comm import raise_if_p2p_error
-                    name, args, kwargs = payload
-                    getattr(target, name)(*args, **kwargs)
-                    raise_if_p2p_error()
-                elif kind == STEP and step_fn is not None:
-                    step_fn(payload)
-        except Exception as e:  # noqa: BLE001 -- mirrored on the leader
-            _log.warning("follower call failed", extra={"event": "follower_error", "detail": repr(e)[:300]})
-        n += 1
+    dog = _LeaderWatchdog(LEADER_TIMEOUT_S if leader_timeout_s is None else leader_timeout_s)
+    try:
+        while True:
+            dog.idle_since = time.monotonic()
+            kind, payload = channel.recv()
+            dog.idle_since = None
+            if kind == STOP:
+                return n
+            if kind == NOOP:
+                continue
+            try:
+                with torch.inference_mode():
+                    if kind == CALL:
+                        from ..parallel.comm import raise_if_p2p_error
+                        name, args, kwargs = payload
+                        getattr(target, name)(*args, **kwargs)
+                        raise_if_p2p_error()
+                    elif kind == STEP and step_fn is not None:
+                        step_fn(payload)
+            except MIRRORED as e:
+                if kind != CALL:
+                    _fail(channel, e)
+                _log.warning("follower call failed (mirrored on the leader)",
+                             extra={"event": "follower_error", "detail": repr(e)[:300]})
+            except Exception as e:  # noqa: BLE001 -- rank-local: the group cannot continue
+                _fail(channel, e)
+            n += 1
+    finally:
+        dog.stop()
+
+
+def _fail(channel: TPChannel, e: BaseException) -> None:
+    detail = f"{type(e).__name__}: {str(e)[:500]}"
+    _log.error("follower failed: leaving the TP group", extra={"event": "follower_fatal", "detail": detail})
+    try:
+        channel.report_failure(detail)
+    except Exception:  # noqa: BLE001
+        pass
+    _die(FOLLOWER_FAILED_EXIT)
 
 
 def heartbeat(channel: TPChannel, stop: threading.Event) -> threading.Thread:
@@ -227,12 +340,19 @@ def setup(tensor_parallel_size: Optional[int] = None) -> TPContext:
     backend = "gloo" if on_cpu else (os.environ.get("SHAI_TP_BACKEND") or None)
     init_distributed(backend=backend, tp_size=tp, device=None if on_cpu else "cuda")
     ctx = TPContext(dist.get_rank(), world, TPChannel())
+    if ctx.is_leader:
+        from ..utils.liveness import mark_broken
+        ctx.channel.listen_for_failures(lambda why: mark_broken(f"TP group broken: {why}"))
+        # heartbeats from the start: a follower that is ready first must not take a leader still loading its
+        # shard for dead
+        ctx.start_heartbeat()
     _log.info("tp worker up", extra={"event": "tp_up", "detail": f"rank {ctx.rank}/{world}"})
     return ctx
 
 
 def shutdown(ctx: TPContext) -> None:
     if ctx.enabled and ctx.is_leader and ctx.channel is not None:
+        ctx.channel.stopping = True
         if ctx._hb is not None:
             ctx._hb.set()
         try:

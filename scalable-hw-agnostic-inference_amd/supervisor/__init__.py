@@ -265,6 +265,36 @@ class Supervisor:
             os.killpg(p.pid, sig)
             self.log("inject_kill", name)
 
+    def rank_pids(self, name: str) -> Dict[int, int]:
+        """{rank: pid} of the worker processes of a TP group (the children ``torch.distributed.run`` started,
+        identified by their RANK environment variable); {} for a TP1 worker."""
+        p = self.procs.get(name)
+        if p is None:
+            return {}
+        import psutil
+        out = {}
+        try:
+            for c in psutil.Process(p.pid).children(recursive=True):
+                try:
+                    r = c.environ().get("RANK")
+                except (psutil.Error, OSError):
+                    continue
+                if r is not None:
+                    out[int(r)] = c.pid
+        except psutil.Error:
+            pass
+        return out
+
+    def kill_rank(self, name: str, rank: int, sig: int = 9) -> bool:
+        """Fault injection: hard-kill ONE rank of a TP group (by its exact PID).  The launcher then stops the
+        other ranks and the group is restarted whole (if its spec allows)."""
+        pid = self.rank_pids(name).get(rank)
+        if pid is None:
+            return False
+        os.kill(pid, sig)
+        self.log("inject_kill_rank", f"{name} rank={rank} pid={pid}")
+        return True
+
     def fail_gpu(self, gpu: int):
         """Fault injection: take a GPU out of the inventory and kill the replica using it."""
         self.inv.fail(gpu)

@@ -56,6 +56,31 @@ class Liveness:
 
 
 _REGISTRY: list = []
+_BROKEN: "str | None" = None
+
+
+def mark_broken(reason: str) -> None:
+    """A fault this process cannot recover from in place (a TP peer collective timed out, a TP rank died):
+    ``/health`` answers 503 from now on, so the router drains the replica and the supervisor restarts the
+    whole group.  The first reason is kept."""
+    global _BROKEN
+    if _BROKEN is None:
+        _BROKEN = str(reason)
+        try:
+            from .logging import get_logger
+            get_logger("liveness").error("process marked broken", extra={"event": "broken", "detail": _BROKEN})
+        except Exception:  # noqa: BLE001 -- never let reporting mask the fault
+            pass
+
+
+def broken() -> "str | None":
+    """The reason this process was marked broken, or None."""
+    return _BROKEN
+
+
+def _reset_broken_for_tests() -> None:
+    global _BROKEN
+    _BROKEN = None
 
 
 def register(live: "Liveness") -> "Liveness":

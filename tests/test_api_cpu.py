@@ -53,6 +53,53 @@ def test_sd_server():
     assert c.get("/serve").status_code == 200
 
 
+def test_sd_server_rejects_bad_requests_alone():
+    """A malformed request is a 422 for its own caller and never reaches the step-batching engine thread
+    (steps < 1 would divide by zero in the schedule, a non-string prompt would fail the text encoder for every
+    request regrouped with it); the server keeps serving."""
+    from shai_amd.serving import sd
+    c = TestClient(sd.create_app(env=env(app="sd21")))
+    assert c.get("/load/1/infer/0").status_code == 422
+    assert c.get("/load/1/infer/-3").status_code == 422
+    assert c.post("/genimage", json={}).status_code == 422
+    assert c.post("/genimage", json={"prompt": 5}).status_code == 422
+    worker = c.app.state.worker
+    import pytest as _pt
+    with _pt.raises(ValueError):
+        worker.submit("x", 0)
+    assert worker.t.is_alive()
+    assert c.post("/genimage", json={"prompt": "a cat"}).status_code == 200
+    assert c.get("/health").status_code == 200
+
+
+def test_broken_replica_health_is_503():
+    """A fault the process cannot recover from in place (an xGMI peer collective that timed out, a dead TP
+    rank) marks it broken for good: /health answers 503 so the router drains it and the supervisor restarts
+    it, even though the engine loop itself keeps making 'progress' by failing requests."""
+    from shai_amd.serving import bert
+    from shai_amd.utils import liveness
+    from shai_amd.parallel import comm
+    c = TestClient(bert.create_app(env=env(app="bert", device="cpu")))
+    assert c.get("/health").status_code == 200
+
+    class _Err:
+        def error(self):
+            return True
+    old = comm.p2p()
+    comm.enable_p2p(_Err())
+    try:
+        import pytest as _pt
+        with _pt.raises(RuntimeError, match="TP group broken"):
+            comm.raise_if_p2p_error()
+        r = c.get("/health")
+        assert r.status_code == 503 and "broken" in r.text
+        assert c.get("/health").status_code == 503     # permanent, not a one-off
+    finally:
+        comm.enable_p2p(old)
+        liveness._reset_broken_for_tests()
+    assert c.get("/health").status_code == 200
+
+
 def test_llm_api_server():
     from shai_amd.serving import llm_api
     c = TestClient(llm_api.create_app(env=env(app="mistral")))

@@ -28,3 +28,21 @@ def test_wheel_installs_and_imports(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env,
                        cwd=str(tmp_path))
     assert r.returncode == 0 and r.stdout.strip() == "2", r.stderr[-2000:]
+
+
+def test_native_build_tracks_every_header(tmp_path):
+    """csrc/build.py compiles with compiler depfiles (deps = gcc), so an edit to any included header
+    (gemm_epilogue.h, ...) rebuilds every object that includes it -- not only common.h / launchers.h users."""
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("shai_native_build", os.path.join(root, "csrc", "build.py"))
+    nb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(nb)
+    f = tmp_path / "build.ninja"
+    nb.write_ninja(str(f))
+    text = f.read_text()
+    for rule in ("hip", "cxx", "rcxx"):
+        block = text.split(f"rule {rule}\n", 1)[1].split("rule ", 1)[0]
+        assert "-MD -MF $out.d" in block and "depfile = $out.d" in block and "deps = gcc" in block, rule
+    assert nb.summary() in ("native build: not run",) or nb.summary().startswith("native build:")

@@ -14,14 +14,14 @@ import pytest
 pytestmark = pytest.mark.slow
 
 
-def _fleet(tmp_path, module, extra_env, tps=(1, 2)):
+def _fleet(tmp_path, module, extra_env, tps=(1, 2), restart=False):
     from shai_amd.supervisor import GPUInventory, Supervisor, WorkerSpec
     sup = Supervisor(None, GPUInventory(list(range(2 * len(tps)))), log_dir=str(tmp_path))  # slots, not GPUs
     env = {"DEVICE": "cpu", "SHAI_MODEL_CONFIG": "tiny", "OMP_NUM_THREADS": "2", "SHAI_TP_HEARTBEAT_S": "1"}
     env.update(extra_env)
     names = []
     for tp in tps:
-        spec = WorkerSpec(f"{module.rsplit('.', 1)[-1]}-tp{tp}", module, tp=tp, env=dict(env), restart=False)
+        spec = WorkerSpec(f"{module.rsplit('.', 1)[-1]}-tp{tp}", module, tp=tp, env=dict(env), restart=restart)
         assert sup.start(spec)
         names.append(spec.name)
     for n in names:
@@ -99,5 +99,44 @@ def test_t5_api_tp2_matches_tp1(tmp_path):
         a, b = embs[n1], embs[n2]
         assert a.shape == b.shape and a.size > 0
         assert np.linalg.norm(a - b) / (np.linalg.norm(a) + 1e-6) < 3e-2
+    finally:
+        sup.shutdown()
+
+
+def test_llm_api_tp2_rank_failure_restarts_group(tmp_path):
+    """Kill rank 1 of a supervisor-launched TP2 LLM server: rank 0 turns unhealthy (503, or gone) within the ALB
+    check budget (sd21-weighted-routing-ing.yaml:9-14: 10 s interval x 10 failures), the launcher tears the group
+    down, and the supervisor relaunches it whole; the relaunched group serves again."""
+    import time
+    sup, (n2,) = _fleet(tmp_path, "shai_amd.serving.llm_api", {"SHAI_TEMPERATURE": "0"}, tps=(2,), restart=True)
+    sup.monitor(0.5)
+    try:
+        first = base64.b64decode(_post(sup, n2, "/generate", {"prompt": "hello", "max_new_tokens": 4})["text"])
+        pids = sup.rank_pids(n2)
+        assert set(pids) == {0, 1}, pids
+        t0 = time.time()
+        assert sup.kill_rank(n2, 1)
+
+        def health():
+            try:
+                return _get(sup, n2, "/health").status_code
+            except Exception:  # noqa: BLE001 -- the leader is gone
+                return None
+        while health() == 200:
+            assert time.time() - t0 < 100, "rank 0 still healthy after its follower died"
+            time.sleep(0.2)
+        t_unhealthy = time.time() - t0
+        # relaunched as a group: new PIDs for both ranks, healthy again, same answer
+        deadline = time.time() + 600
+        while True:
+            new = sup.rank_pids(n2)
+            if set(new) == {0, 1} and all(new[r] != pids[r] for r in (0, 1)) and health() == 200:
+                break
+            assert time.time() < deadline, open(os.path.join(tmp_path, f"{n2}.log")).read()[-4000:]
+            time.sleep(0.5)
+        again = base64.b64decode(_post(sup, n2, "/generate", {"prompt": "hello", "max_new_tokens": 4})["text"])
+        assert again == first
+        assert sup.restarts.get(n2, 0) >= 1
+        assert t_unhealthy < 100, t_unhealthy
     finally:
         sup.shutdown()
