@@ -1126,6 +1126,15 @@ void gated_act(const Tensor& x, const Tensor& out, int64_t act, bool gate_first)
   shai::launch_gated_act(cptr(x), mptr(out), rows, F, xs, act, gate_first, stream());
 }
 
+// A non-owning device tensor over memory this library did not allocate through torch (the xGMI P2P staging slot:
+// IPC-exported uncached memory a row-parallel GEMM writes its partial product into).  The caller keeps the
+// memory alive for the tensor's lifetime.
+Tensor from_ptr(int64_t ptr, at::IntArrayRef size, at::ScalarType dtype, int64_t device) {
+  SHAI_CHECK(ptr != 0 && (ptr & 15) == 0, "from_ptr: null or misaligned pointer");
+  return at::from_blob(reinterpret_cast<void*>(ptr), size,
+                       at::TensorOptions().dtype(dtype).device(at::kCUDA, (c10::DeviceIndex)device));
+}
+
 void bias_act(const Tensor& x, const optional<Tensor>& bias, const optional<Tensor>& residual, const Tensor& out,
               int64_t act, double alpha) {
   check_bf16(x, "x");
@@ -1352,6 +1361,7 @@ void quant_rows_fp8(const Tensor& x, const Tensor& out, const Tensor& scale, dou
 }
 
 TORCH_LIBRARY(shai, m) {
+  m.def("from_ptr(int ptr, int[] size, ScalarType dtype, int device) -> Tensor", &from_ptr);
   m.def("gemm_f8(Tensor a8, Tensor w8, Tensor a_scale, Tensor w_scale, Tensor(a!) c, Tensor? bias, Tensor? residual, float res_alpha, int act, bool glu, int cfg=-1) -> ()");
   m.def("quant_rows_fp8(Tensor x, Tensor(a!) out, Tensor(b!) scale, float rms_eps) -> ()");
   m.def("rmsnorm(Tensor x, Tensor? w, Tensor(a!) out, Tensor? residual, Tensor(b!)? residual_out, float eps, float w_offset) -> ()");

@@ -81,8 +81,51 @@ __device__ __forceinline__ void barrier_phase(const Peers& P, Layout* me, int ph
   __syncthreads();
 }
 
+// Fused output stage of a row-parallel layer on the reduced row-major [rows, ncols] bf16 message:
+//   out = residual + gate[row / rows_per_gate] * (sum + bias)
+// bias (per column, added once after the reduction), gate (AdaLN-Zero: one row of ncols per image, row stride
+// gate_ld8 16-B groups) and residual ([rows, ncols], may be the output itself) are each optional.  16-B group i
+// holds columns (8 i) % ncols .. + 7 of row i / (ncols / 8) (ncols % 8 == 0).
+struct Epi {
+  const uint4* bias;      // [ncols] bf16 or nullptr
+  const uint4* residual;  // [rows, ncols] bf16 or nullptr
+  int ncols8;             // ncols / 8
+  const uint4* gate = nullptr;
+  int gate_ld8 = 0;
+  int rows_per_gate = 1;
+};
+
+__device__ __forceinline__ void add_bf16x8(float acc[8], uint4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    acc[2 * e] += __uint_as_float(w[e] << 16);
+    acc[2 * e + 1] += __uint_as_float(w[e] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ void apply_epi(const Epi& E, long i, float acc[8]) {
+  const int row = (int)i / E.ncols8, c8 = (int)i - row * E.ncols8;  // i < 2^31: the slot is <= 16 MiB
+  if (E.bias) add_bf16x8(acc, E.bias[c8]);
+  if (E.gate) {
+    const uint4 g = E.gate[(long)(row / E.rows_per_gate) * E.gate_ld8 + c8];
+    const uint32_t w[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc[2 * e] *= __uint_as_float(w[e] << 16);
+      acc[2 * e + 1] *= __uint_as_float(w[e] & 0xffff0000u);
+    }
+  }
+  if (E.residual) add_bf16x8(acc, E.residual[i]);
+}
+
+__device__ __forceinline__ uint4 pack_bf16x8(const float acc[8]);
+
+// STAGED: the input already sits in this rank's slot A (the row-parallel GEMM wrote its partial there), so the
+// copy of step 1 is skipped; the slot is never rewritten before every peer is past this call's end barrier.
+template <bool STAGED>
 __global__ void __launch_bounds__(512) p2p_one_shot(Peers P, int rank, int world, const uint4* in,
-                                                    uint4* out, long n16) {
+                                                    uint4* out, long n16, Epi E) {
   __shared__ uint32_t s_epoch;
   Layout* me = reinterpret_cast<Layout*>(P.base[rank]);
   if (threadIdx.x == 0) {
@@ -94,31 +137,20 @@ __global__ void __launch_bounds__(512) p2p_one_shot(Peers P, int rank, int world
   const uint32_t epoch = s_epoch;
   uint4* mine = reinterpret_cast<uint4*>(P.base[rank] + kDataOff);
   const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) mine[i] = in[i];
-  __threadfence_system();
+  if (!STAGED) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) mine[i] = in[i];
+    __threadfence_system();
+  }
   __syncthreads();
   barrier_phase(P, me, 0, rank, world, epoch);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int r = 0; r < world; ++r) {
       const uint4 v = r == rank ? mine[i] : peer_load16(peer_rsrc(P.base[r] + kDataOff, n16 * 16), i);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        acc[2 * e] += __uint_as_float(w[e] << 16);
-        acc[2 * e + 1] += __uint_as_float(w[e] & 0xffff0000u);
-      }
+      add_bf16x8(acc, v);
     }
-    uint32_t o[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      // round-to-nearest-even to bf16
-      uint32_t lo = __float_as_uint(acc[2 * e]), hi = __float_as_uint(acc[2 * e + 1]);
-      lo = (lo + 0x7fffu + ((lo >> 16) & 1u)) >> 16;
-      hi = (hi + 0x7fffu + ((hi >> 16) & 1u)) >> 16;
-      o[e] = lo | (hi << 16);
-    }
-    out[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    apply_epi(E, i, acc);
+    out[i] = pack_bf16x8(acc);
   }
   __syncthreads();
   barrier_phase(P, me, 1, rank, world, epoch);
@@ -137,7 +169,7 @@ __device__ __forceinline__ uint4 pack_bf16x8(const float acc[8]) {
 }
 
 // Two-shot (reduce-scatter + all-gather) all-reduce for mid-size messages (Flux / prefill row-parallel
-// outputs, 0.5-64 MiB).  The message is cut into `world` segments; rank r owns segment r.
+// outputs, 256 KiB - 16 MiB: the default routing in parallel/comm.py).  The message is cut into `world` segments; rank r owns segment r.
 //   phase 0: copy the input into the local staging slot A (only the positions this block will hand out),
 //   barrier, phase 1: sum segment r over every rank's slot A (world-1 remote reads of M/world each, all xGMI
 //   links busy at once) into the local slot B, barrier, phase 2: gather every segment s from rank s's slot B
@@ -145,8 +177,11 @@ __device__ __forceinline__ uint4 pack_bf16x8(const float acc[8]) {
 //   ONE link per direction for a single ring.  Block b of every rank touches the same positions in every
 //   phase, so the per-block flag barriers order all the hand-offs (no grid-wide barrier); the next call's
 //   first barrier protects slot B from being overwritten while a peer still gathers it.
+// STAGED as for the one-shot kernel (no phase-0 copy); the fused epilogue (bias, residual) is applied by the
+// segment's owner in phase 1, so every element gets it exactly once and phase 2 gathers final values.
+template <bool STAGED>
 __global__ void __launch_bounds__(512) p2p_two_shot(Peers P, int rank, int world, const uint4* in, uint4* out,
-                                                    long n16, size_t slot_bytes) {
+                                                    long n16, size_t slot_bytes, Epi E) {
   __shared__ uint32_t s_epoch;
   Layout* me = reinterpret_cast<Layout*>(P.base[rank]);
   if (threadIdx.x == 0) {
@@ -161,11 +196,13 @@ __global__ void __launch_bounds__(512) p2p_two_shot(Peers P, int rank, int world
   const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
   uint4* slotA = reinterpret_cast<uint4*>(P.base[rank] + kDataOff);
   uint4* slotB = reinterpret_cast<uint4*>(P.base[rank] + kDataOff + slot_bytes);
-  for (int s = 0; s < world; ++s) {
-    const long beg = s * seg, end = min(n16, beg + seg);
-    for (long i = beg + t0; i < end; i += stride) slotA[i] = in[i];
+  if (!STAGED) {
+    for (int s = 0; s < world; ++s) {
+      const long beg = s * seg, end = min(n16, beg + seg);
+      for (long i = beg + t0; i < end; i += stride) slotA[i] = in[i];
+    }
+    __threadfence_system();
   }
-  __threadfence_system();
   __syncthreads();
   barrier_phase(P, me, 0, rank, world, epoch);
   {
@@ -175,13 +212,9 @@ __global__ void __launch_bounds__(512) p2p_two_shot(Peers P, int rank, int world
       for (int r = 0; r < world; ++r) {
         const int src = (rank + r) % world;  // stagger the peers so the links are loaded evenly
         const uint4 v = src == rank ? slotA[i] : peer_load16(peer_rsrc(P.base[src] + kDataOff, n16 * 16), i);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          acc[2 * e] += __uint_as_float(w[e] << 16);
-          acc[2 * e + 1] += __uint_as_float(w[e] & 0xffff0000u);
-        }
+        add_bf16x8(acc, v);
       }
+      apply_epi(E, i, acc);
       slotB[i] = pack_bf16x8(acc);
     }
   }
@@ -242,6 +275,7 @@ struct Ctx {
   uint32_t* host_err;  // pinned, mapped into the device address space (Peers::host_err)
   Peers peers;
   bool opened[kMaxRanks];
+  long long launches[5];  // one-shot, two-shot, staged one-shot, staged two-shot, all-gather (host-side count)
 };
 
 }  // namespace
@@ -323,8 +357,9 @@ int shai_p2p_allreduce_bf16(void* ctx, const void* in, void* out, size_t bytes, 
   if (blocks > c->max_blocks) blocks = c->max_blocks;
   if (blocks < 1) blocks = 1;
   // every rank must use the same grid: it is a function of bytes only
-  hipLaunchKernelGGL(p2p_one_shot, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world,
-                     static_cast<const uint4*>(in), static_cast<uint4*>(out), n16);
+  hipLaunchKernelGGL(p2p_one_shot<false>, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world,
+                     static_cast<const uint4*>(in), static_cast<uint4*>(out), n16, Epi{nullptr, nullptr, 1});
+  ++c->launches[0];
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -337,9 +372,66 @@ int shai_p2p_allreduce2_bf16(void* ctx, const void* in, void* out, size_t bytes,
   int blocks = (int)((per_rank + 511) / 512);
   if (blocks > c->max_blocks) blocks = c->max_blocks;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(p2p_two_shot, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world,
-                     static_cast<const uint4*>(in), static_cast<uint4*>(out), n16, c->max_bytes);
+  hipLaunchKernelGGL(p2p_two_shot<false>, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world,
+                     static_cast<const uint4*>(in), static_cast<uint4*>(out), n16, c->max_bytes,
+                     Epi{nullptr, nullptr, 1});
+  ++c->launches[1];
   return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// This rank's staging slot (slot A): a row-parallel GEMM writes its partial product straight into it and
+// shai_p2p_allreduce_staged reduces from there (no staging copy).  Returns the device pointer; *bytes = capacity.
+void* shai_p2p_staging(void* ctx, size_t* bytes) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (bytes) *bytes = c->max_bytes;
+  return c->local + kDataOff;
+}
+
+// out[rows, ncols] = residual + gate[row / rows_per_gate] * (sum over ranks of every rank's staged partial + bias)
+// (bytes = rows * ncols * 2 at the start of slot A; bias / residual / gate optional, gate row stride gate_ld
+// elements; out may be the residual itself), bf16, fp32 accumulation.  two_shot selects
+// reduce-scatter + all-gather (mid-size messages) over one-shot.  Every rank must pass the same bytes / ncols /
+// two_shot.  0 on success.
+int shai_p2p_allreduce_staged(void* ctx, void* out, size_t bytes, int ncols, const void* bias, const void* residual,
+                              const void* gate, int gate_ld, int rows_per_gate, int two_shot, hipStream_t stream) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (bytes % 16 != 0 || bytes > c->max_bytes || ncols <= 0 || ncols % 8 != 0 || (bytes / 2) % ncols != 0)
+    return -1;
+  if ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(residual) |
+       reinterpret_cast<uintptr_t>(gate)) & 15)
+    return -3;
+  if (gate && (gate_ld % 8 != 0 || gate_ld < ncols || rows_per_gate < 1)) return -4;
+  const long n16 = (long)(bytes / 16);
+  Epi E{static_cast<const uint4*>(bias), static_cast<const uint4*>(residual), ncols / 8};
+  E.gate = static_cast<const uint4*>(gate);
+  E.gate_ld8 = gate_ld / 8;
+  E.rows_per_gate = rows_per_gate;
+  const uint4* in = reinterpret_cast<const uint4*>(c->local + kDataOff);
+  int blocks;
+  if (two_shot) {
+    blocks = (int)(((n16 + c->world - 1) / c->world + 511) / 512);
+  } else {
+    blocks = (int)((n16 + 511) / 512);
+  }
+  if (blocks > c->max_blocks) blocks = c->max_blocks;
+  if (blocks < 1) blocks = 1;
+  if (two_shot) {
+    hipLaunchKernelGGL(p2p_two_shot<true>, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world, in,
+                       static_cast<uint4*>(out), n16, c->max_bytes, E);
+    ++c->launches[3];
+  } else {
+    hipLaunchKernelGGL(p2p_one_shot<true>, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world, in,
+                       static_cast<uint4*>(out), n16, E);
+    ++c->launches[2];
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// Host-side launch counts (captured launches count once): [one-shot, two-shot, staged one-shot, staged two-shot,
+// all-gather].
+void shai_p2p_launch_counts(void* ctx, long long* out5) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  for (int i = 0; i < 5; ++i) out5[i] = c->launches[i];
 }
 
 // Rank-major all-gather of `bytes` (multiple of 16, <= max_bytes) per rank: out holds world * bytes.
@@ -352,6 +444,7 @@ int shai_p2p_allgather(void* ctx, const void* in, void* out, size_t bytes, hipSt
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(p2p_all_gather, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world,
                      static_cast<const uint4*>(in), static_cast<uint4*>(out), n16);
+  ++c->launches[4];
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -26,12 +26,16 @@ def main(argv=None):
     ap.add_argument("--background", type=int, default=16)
     ap.add_argument("--gen", type=int, default=128)
     ap.add_argument("--no-mix", action="store_true", help="alternate prefill chunks and decode steps instead")
-    ap.add_argument("--model", default="mistral", choices=["mistral", "llama3_8b"])
+    ap.add_argument("--model", default="mistral", choices=["mistral", "llama3_8b", "llama31_8b"],
+                    help="llama31_8b: 128k context (64k / 128k lines: --prompt-len 65536 / 127744)")
     a = ap.parse_args(argv)
     from ..engines.llm import LLMEngine, SamplingParams
     from ..models.llama import LlamaConfig
-    cfg = LlamaConfig.mistral_7b() if a.model == "mistral" else LlamaConfig.llama3_8b()
+    cfg = {"mistral": LlamaConfig.mistral_7b, "llama3_8b": LlamaConfig.llama3_8b,
+           "llama31_8b": LlamaConfig.llama31_8b}[a.model]()
     P, G = a.prompt_len, a.gen
+    if P + G + 64 > cfg.max_position_embeddings:
+        raise SystemExit(f"{a.model}: prompt {P} + {G} generated exceeds its {cfg.max_position_embeddings} positions")
     eng = LLMEngine(cfg, device="cuda:0", max_num_seqs=a.background + 1, max_model_len=P + G + 64,
                     enable_prefix_caching=False, prefill_chunk=a.chunk, prefill_token_budget=max(a.chunk, 2048),
                     mixed_steps=not a.no_mix)

@@ -162,6 +162,9 @@ def _gated_out(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], resi
     if tp().size == 1:
         ops.gemm_into(x, w, residual, b, residual=residual, gate=gate, rows_per_gate=rows)
         return
+    # xGMI P2P: GEMM into the IPC staging slot, then one kernel reduces and applies the gated residual in place
+    if comm.row_parallel_reduce(x, w, b, residual, gate=gate, rows_per_gate=rows, out=residual) is not None:
+        return
     y = ops.linear(x, w, None)
     comm.all_reduce(y)
     yb = y.float() + (b.float() if b is not None else 0.0)

@@ -67,6 +67,16 @@ class LlamaConfig:
                            eos_token_id=128001)
 
     @staticmethod
+    def llama31_8b():
+        """Llama-3.1-8B: the 128k-context text model (and the Llama-3.2-11B-Vision text tower's shape), llama3
+        RoPE scaling."""
+        c = LlamaConfig.llama3_8b()
+        c.max_position_embeddings = 131072
+        c.rope_scaling = {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                          "original_max_position_embeddings": 8192}
+        return c
+
+    @staticmethod
     def llama3_70b():
         return LlamaConfig(vocab_size=128256, hidden_size=8192, intermediate_size=28672, num_hidden_layers=80,
                            num_attention_heads=64, num_key_value_heads=8, rope_theta=5e5,

@@ -187,20 +187,25 @@ def _attn_any_head_dim(q, k, v, scale):
 
 
 class VisionAttention(nn.Module):
+    """Head-sharded at TP > 1 (the reference serves the whole model at TP32, cova/mllama-32-11b-vllm-trn1-
+    config.yaml:9): fused QKV column-parallel by heads, o_proj row-parallel with the residual added after the
+    reduction -- each rank runs attention for its own heads over all tiles."""
+
     def __init__(self, c: MllamaVisionConfig):
         super().__init__()
-        self.h = c.attention_heads
         self.hd = c.hidden_size // c.attention_heads
-        self.qkv = Linear(c.hidden_size, 3 * c.hidden_size, bias=False)
-        self.o_proj = Linear(c.hidden_size, c.hidden_size, bias=False)
+        self.qkv = QKVParallelLinear(c.hidden_size, c.attention_heads, c.attention_heads, self.hd, bias=False)
+        self.h = self.qkv.h_local
+        self.o_proj = RowParallelLinear(c.hidden_size, c.hidden_size, bias=False)
 
     def forward(self, x, valid_idx: List[torch.Tensor], pad_idx: List[Optional[torch.Tensor]], residual):
         N, T, d = x.shape
         h, hd = self.h, self.hd
+        dl = h * hd                      # this rank's heads
         qkv = self.qkv(x)
-        q = qkv[..., :d].view(N, T, h, hd)
-        k = qkv[..., d:2 * d].view(N, T, h, hd)
-        v = qkv[..., 2 * d:].view(N, T, h, hd)
+        q = qkv[..., :dl].view(N, T, h, hd)
+        k = qkv[..., dl:2 * dl].view(N, T, h, hd)
+        v = qkv[..., 2 * dl:].view(N, T, h, hd)
         scale = hd ** -0.5
         o = _attn_any_head_dim(q, k, v, scale).contiguous()
         for n in range(N):
@@ -211,7 +216,7 @@ class VisionAttention(nn.Module):
             op = _attn_any_head_dim(q[n:n + 1].index_select(1, pi), k[n:n + 1].index_select(1, vi),
                                     v[n:n + 1].index_select(1, vi), scale)
             o[n].index_copy_(0, pi, op[0])
-        return self.o_proj(o.view(N, T, d), residual=residual)
+        return self.o_proj(o.view(N, T, dl), residual=residual)
 
 
 class VisionLayer(nn.Module):
@@ -221,8 +226,8 @@ class VisionLayer(nn.Module):
         self.input_layernorm = LayerNorm(c.hidden_size, c.norm_eps)
         self.self_attn = VisionAttention(c)
         self.post_attention_layernorm = LayerNorm(c.hidden_size, c.norm_eps)
-        self.fc1 = Linear(c.hidden_size, c.intermediate_size)
-        self.fc2 = Linear(c.intermediate_size, c.hidden_size)
+        self.fc1 = ColumnParallelLinear(c.hidden_size, c.intermediate_size)      # MLP sharded by the hidden dim
+        self.fc2 = RowParallelLinear(c.intermediate_size, c.hidden_size)
         if gated:
             self.gate_attn = nn.Parameter(torch.zeros(1), requires_grad=False)
             self.gate_ffn = nn.Parameter(torch.zeros(1), requires_grad=False)

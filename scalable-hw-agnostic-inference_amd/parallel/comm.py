@@ -6,14 +6,19 @@ and capturable in HIP graphs.  Two transports:
 * RCCL (``torch.distributed`` backend "nccl" on ROCm) -- default for every size;
   also the sequence-parallel all-gather / reduce-scatter pair (:func:`all_gather_seq`,
   :func:`reduce_scatter_seq`) used by the Flux single-stream blocks at SP > 1.
-* ``P2PAllReduce`` (``csrc/comm/p2p_allreduce.hip``) -- one-shot all-reduce for
-  small, latency-bound messages (LLM decode: B x 4096 bf16 per layer), reading
-  every peer's IPC-mapped buffer directly over xGMI in one kernel, and a one-shot
-  all-gather (vocab-parallel logits).  ON by default for every TP > 1 group on
-  GPUs (``SHAI_P2P_ALLREDUCE=0`` disables it): all-reduces up to
-  ``SHAI_P2P_MAX_BYTES`` (default 512 KiB) and all-gather shards up to the buffer
-  capacity go through it; everything else goes to RCCL.  A peer that never arrives
-  sets an error word the engines poll after every step (:func:`raise_if_p2p_error`).
+* ``P2PAllReduce`` (``csrc/comm/p2p_allreduce.hip``) -- xGMI peer-memory kernels
+  over IPC-mapped buffers, ON by default for every TP > 1 group on GPUs
+  (``SHAI_P2P_ALLREDUCE=0`` disables it).  Routing by message size:
+  one-shot (every rank reads every peer's whole message; latency-bound LLM decode,
+  B x 4096 bf16) up to ``SHAI_P2P_ONE_SHOT_MAX`` (256 KiB), two-shot
+  (reduce-scatter + all-gather over all 7 links at once; Flux / prefill
+  row-parallel outputs, 27 MiB per call for Flux 1024^2 at TP8) up to
+  ``SHAI_P2P_MAX_BYTES`` (32 MiB, the staging capacity), RCCL above; a one-shot all-gather for vocab-parallel logits.
+  A row-parallel layer (:func:`row_parallel_reduce`) writes its GEMM partial
+  straight into this rank's IPC staging slot and one fused kernel reduces it and
+  adds the bias and the residual (no staging copy, no separate residual launch).
+  A peer that never arrives sets an error word the engines poll after every step
+  (:func:`raise_if_p2p_error`).
 
 On a fully connected 8x MI355X node each GPU has 7 xGMI links; RCCL's
 multi-channel rings / direct algorithms use them for the large Flux/prefill
@@ -30,9 +35,11 @@ import torch.distributed as dist
 from .state import tp
 
 _P2P = None
-P2P_ONE_SHOT_MAX = int(os.environ.get("SHAI_P2P_ONE_SHOT_MAX", str(512 * 1024)))
-P2P_MAX_BYTES = int(os.environ.get("SHAI_P2P_MAX_BYTES", str(512 * 1024)))
-P2P_CAPACITY = int(os.environ.get("SHAI_P2P_CAPACITY", str(16 << 20)))
+P2P_ONE_SHOT_MAX = int(os.environ.get("SHAI_P2P_ONE_SHOT_MAX", str(256 * 1024)))
+P2P_CAPACITY = int(os.environ.get("SHAI_P2P_CAPACITY", str(32 << 20)))   # Flux 1024^2 TP8 messages: 27 MiB
+P2P_MAX_BYTES = int(os.environ.get("SHAI_P2P_MAX_BYTES", str(P2P_CAPACITY)))
+# SHAI_P2P_STAGED=0: row-parallel layers all-reduce a separate GEMM output (staging copy + residual launch)
+P2P_STAGED = os.environ.get("SHAI_P2P_STAGED", "1") != "0"
 
 
 def enable_p2p(p2p) -> None:
@@ -116,6 +123,39 @@ def all_reduce_overlapped(x2d: torch.Tensor, gemm_chunk, out: torch.Tensor, chun
         with torch.cuda.stream(side):
             all_reduce(out[r0:r1], group)
     cur.wait_stream(side)
+    return out
+
+
+def row_parallel_reduce(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+                        residual: Optional[torch.Tensor], w_scale: Optional[torch.Tensor] = None,
+                        gate: Optional[torch.Tensor] = None, rows_per_gate: int = 1,
+                        out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """Fused output stage of a row-parallel layer on the xGMI P2P path: the GEMM writes this rank's partial
+    product ([..., N], x's leading shape) straight into the IPC staging slot, then ONE kernel sums every rank's
+    slot (one-shot or two-shot by size) and applies ``residual + gate * (sum + bias)`` -- the TP=1 epilogue
+    fusion kept at TP > 1 (``out`` may be ``residual``: the in-place gated update of the Flux blocks).
+    Returns None when the message does not qualify (no P2P, too large, fp8 prefill, odd widths, strided
+    tensors); the caller then takes the generic GEMM -> all_reduce -> epilogue path."""
+    p = _P2P
+    if p is None or not P2P_STAGED or not x.is_cuda or x.dtype != torch.bfloat16:
+        return None
+    n = weight.shape[0]
+    rows = x.numel() // x.shape[-1]
+    nbytes = rows * n * 2
+    if n % 8 or nbytes > p.max_bytes or (w_scale is not None and rows > 64):
+        return None
+    for t in (residual, out):
+        if t is not None and (t.dtype != torch.bfloat16 or t.numel() != rows * n or not t.is_contiguous()):
+            return None
+    if gate is not None and (gate.dtype != torch.bfloat16 or gate.stride(-1) != 1 or gate.shape[-1] < n):
+        return None
+    from .. import ops
+    stage = p.staging(rows, n, x.device).view(*x.shape[:-1], n)
+    ops.gemm_into(x, weight, stage, w_scale=w_scale)
+    if out is None:
+        out = torch.empty(*x.shape[:-1], n, dtype=x.dtype, device=x.device)
+    p.reduce_staged(out, n, bias, residual, gate.reshape(-1, gate.shape[-1]) if gate is not None else None,
+                    rows_per_gate)
     return out
 
 
@@ -213,6 +253,12 @@ class P2PAllReduce:
         for fn in (self.lib.shai_p2p_allreduce_bf16, self.lib.shai_p2p_allreduce2_bf16, self.lib.shai_p2p_allgather):
             fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         self.one_shot_max = one_shot_max
+        self.lib.shai_p2p_staging.restype = ctypes.c_void_p
+        self.lib.shai_p2p_staging.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]
+        self.lib.shai_p2p_allreduce_staged.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                                       ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        self.lib.shai_p2p_launch_counts.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong)]
         self.lib.shai_p2p_error.argtypes = [ctypes.c_void_p]
         self.lib.shai_p2p_set_max_blocks.argtypes = [ctypes.c_void_p, ctypes.c_int]
         self.lib.shai_p2p_destroy.argtypes = [ctypes.c_void_p]
@@ -247,6 +293,46 @@ class P2PAllReduce:
         if rc != 0:
             raise RuntimeError(f"p2p all-reduce launch failed ({rc})")
         return x
+
+    def staging(self, rows: int, cols: int, device) -> torch.Tensor:
+        """A bf16 [rows, cols] view of this rank's IPC staging slot (the GEMM output of :meth:`reduce_staged`).
+        One slot per group: valid until the next collective of this group."""
+        import ctypes
+        cap = ctypes.c_size_t(0)
+        ptr = self.lib.shai_p2p_staging(self.ctx, ctypes.byref(cap))
+        assert rows * cols * 2 <= cap.value
+        idx = device.index if getattr(device, "index", None) is not None else torch.cuda.current_device()
+        return torch.ops.shai.from_ptr(int(ptr), [rows, cols], torch.bfloat16, int(idx))
+
+    def reduce_staged(self, out: torch.Tensor, ncols: int, bias: Optional[torch.Tensor] = None,
+                      residual: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None,
+                      rows_per_gate: int = 1) -> torch.Tensor:
+        """out = residual + gate[row // rows_per_gate] * (sum over ranks of the staged partials + bias)
+        (contiguous bf16, ``out.numel()`` elements: the first ``out.numel()`` of the staging slot; ``out`` may
+        be ``residual``; ``gate`` [G, >= ncols] with rows of stride ``gate.stride(0)``)."""
+        nbytes = out.numel() * 2
+        two = nbytes > self.one_shot_max
+        for t in (bias, residual):
+            assert t is None or (t.dtype == torch.bfloat16 and t.is_contiguous())
+        if gate is not None:
+            assert gate.dtype == torch.bfloat16 and gate.dim() == 2 and gate.stride(1) == 1
+        st = torch.cuda.current_stream(out.device).cuda_stream
+        rc = self.lib.shai_p2p_allreduce_staged(self.ctx, out.data_ptr(), nbytes, int(ncols),
+                                                bias.data_ptr() if bias is not None else None,
+                                                residual.data_ptr() if residual is not None else None,
+                                                gate.data_ptr() if gate is not None else None,
+                                                int(gate.stride(0)) if gate is not None else 0, int(rows_per_gate),
+                                                int(two), st)
+        if rc != 0:
+            raise RuntimeError(f"p2p staged all-reduce launch failed ({rc})")
+        return out
+
+    def launch_counts(self) -> dict:
+        """Kernel launches per algorithm so far (a captured launch counts once)."""
+        import ctypes
+        buf = (ctypes.c_longlong * 5)()
+        self.lib.shai_p2p_launch_counts(self.ctx, buf)
+        return dict(zip(("one_shot", "two_shot", "staged_one_shot", "staged_two_shot", "all_gather"), list(buf)))
 
     def can_gather(self, shard_bytes: int) -> bool:
         return shard_bytes % 16 == 0 and shard_bytes <= self.capacity

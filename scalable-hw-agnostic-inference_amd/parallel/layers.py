@@ -120,6 +120,10 @@ class RowParallelLinear(_ShardLoadMixin, nn.Module):
             comm.all_reduce_overlapped(x2, gemm_chunk, y, nch)
             y = y.view(*x.shape[:-1], self.out_features)
         else:
+            # xGMI P2P: the GEMM writes into the IPC staging slot and one kernel reduces + adds bias / residual
+            y = comm.row_parallel_reduce(x, self.weight, self.bias, residual, self.w_scale)
+            if y is not None:
+                return y.view(*x.shape[:-1], self.out_features)
             y = ops.linear(x, self.weight, None, w_scale=self.w_scale)
             comm.all_reduce(y)
         if self.bias is not None or residual is not None:

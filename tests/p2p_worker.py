@@ -1,5 +1,7 @@
 """world ranks (2, 4 or 8) on ONE GPU (gloo for the handle exchange): the IPC-mapped one-shot and two-shot
-all-reduces must equal the sum of every rank's tensor, and the one-shot all-gather the rank-major
+all-reduces -- both reached through the DEFAULT size routing (one-shot <= 256 KiB < two-shot <= capacity) --
+must equal the sum of every rank's tensor, the staged (GEMM-into-the-slot) reduce with its fused
+bias / AdaLN gate / residual epilogue the fp32 reference, and the one-shot all-gather the rank-major
 concatenation, repeatedly, at mixed sizes and inside a HIP graph."""
 import os
 
@@ -15,8 +17,11 @@ def run(rank, world, port):
     import torch.distributed as dist
     dist.init_process_group("gloo")
     torch.cuda.set_device(0)
+    from shai_amd.parallel import comm
     from shai_amd.parallel.comm import P2PAllReduce
-    ar = P2PAllReduce(None, max_bytes=8 << 20, one_shot_max=512 << 10)
+    ar = P2PAllReduce(None)                      # default routing thresholds
+    assert ar.one_shot_max == 256 << 10 and ar.max_bytes >= 16 << 20, (ar.one_shot_max, ar.max_bytes)
+    c0 = ar.launch_counts()
     # one-shot sizes, then two-shot (reduce-scatter + all-gather) sizes incl. an uneven segmentation
     for n in (8, 4096 * 32, 1 << 18, 1 << 19, (3 << 20) + 8, 4 << 20):
         for it in range(3):
@@ -29,6 +34,31 @@ def run(rank, world, port):
             err = ((x.float() - want).abs().max() / want.abs().max()).item()
             assert err < 2e-2, (n, it, err)
             dist.barrier()
+    c1 = ar.launch_counts()
+    assert c1["one_shot"] - c0["one_shot"] == 3 * 2 and c1["two_shot"] - c0["two_shot"] == 3 * 4, (c0, c1)
+    # staged reduce: each rank's partial is written INTO the staging slot (as the row-parallel GEMM does), then
+    # one kernel sums the slots and applies residual + gate[row // rpg] * (sum + bias); one-shot and two-shot
+    # sizes, the residual updated in place (Flux's gated residual)
+    for rows, cols, rpg, inplace in ((64, 4096, 64, False), (1000, 3072, 250, True), (8, 64, 1, False)):
+        torch.manual_seed(rows + cols)
+        parts = [torch.randn(rows, cols, device="cuda").bfloat16() for _ in range(world)]
+        bias = torch.randn(cols, device="cuda").bfloat16()
+        res = torch.randn(rows, cols, device="cuda").bfloat16()
+        gfull = torch.randn(rows // rpg, 6 * cols, device="cuda").bfloat16()
+        gate = gfull[:, 2 * cols:3 * cols]         # a strided chunk of the AdaLN modulation, as in models/flux.py
+        want = res.float() + gate.float().repeat_interleave(rpg, 0) * (sum(p.float() for p in parts) + bias.float())
+        stage = ar.staging(rows, cols, torch.device("cuda", 0))
+        stage.copy_(parts[rank])
+        out = res if inplace else torch.empty_like(res)
+        before = ar.launch_counts()
+        ar.reduce_staged(out, cols, bias, res, gate, rpg)
+        torch.cuda.synchronize()
+        err = ((out.float() - want).abs().max() / want.abs().max()).item()
+        assert err < 2e-2, (rows, cols, err)
+        after = ar.launch_counts()
+        key = "staged_two_shot" if rows * cols * 2 > ar.one_shot_max else "staged_one_shot"
+        assert after[key] == before[key] + 1, (key, before, after)
+        dist.barrier()
     # all-gather (vocab-parallel logits: [B, V / world] shards -> [world * B, V / world] rank-major)
     for rows, cols in ((1, 8), (64, 4096), (3, 1000), (64, 16032)):
         torch.manual_seed(rows * 7 + cols)

@@ -328,6 +328,32 @@ def test_decode_attn(cuda, D, Hq, Hkv, long_ctx):
         close(o, ref.decode_attention(q, kc, vc, bt, lens, 1 / math.sqrt(D)), 2e-2)
 
 
+@pytest.mark.parametrize("ctx", [[65536 + 17], [127744, 65600]])
+def test_decode_attn_long_context_64k_128k(cuda, ctx):
+    """Split-K paged decode attention at the reference's configured context (max_model_len 128000,
+    cova/mllama-32-11b-vllm-trn1-config.yaml:12-16), Llama-3 GQA shape (32 q / 8 kv heads, D 128): the tuned
+    split count (decode_splits), the cap (64) and an uneven one against the fp32 reference.  A "needle" key
+    aligned with q far into the context (and one near the start) dominates each row's softmax, so a split that
+    drops, double-counts or mis-rescales its partial shows up as a wrong output, not as averaged noise."""
+    torch.manual_seed(21)
+    D, Hq, Hkv = 128, 32, 8
+    B = len(ctx)
+    nblocks = sum((c + 63) // 64 for c in ctx) + 4
+    kc, vc, bt = _paged_setup(B, Hkv, D, ctx, nblocks=nblocks)
+    q = rnd(B, Hq, D)
+    G = Hq // Hkv
+    for b, c in enumerate(ctx):
+        for pos in (5, c - 1000):
+            blk, off = int(bt[b, pos // 64]), pos % 64
+            for h in range(Hkv):   # key aligned with the group's first q head: score ~ 0.35 |q|^2 / sqrt(D)
+                kc[blk, h, off] = (q[b, h * G].float() * 0.35).to(torch.bfloat16)
+    lens = torch.tensor(ctx, dtype=torch.int32, device="cuda")
+    want = ref.decode_attention(q, kc, vc, bt, lens, 1 / math.sqrt(D))
+    for splits in (None, 64, 37):
+        o = ops.decode_attention(q, kc, vc, bt, lens, num_splits=splits, max_ctx=max(ctx))
+        close(o, want, 2e-2)
+
+
 def test_paged_prefill_attn(cuda):
     torch.manual_seed(13)
     D, Hq, Hkv = 128, 8, 2

@@ -84,16 +84,18 @@ def run(rank, world, port):
 def run_flux(rank, world, port):
     """Flux pipeline (CLIP + T5 + MMDiT + VAE) at TP=2 on one GPU with HIP-graph steps vs TP=1 from the same
     seeds: every row-parallel all-reduce inside the captured step goes through the P2P kernels."""
+    # one-shot only below 4 KiB: the tiny model's row-parallel messages then take the two-shot kernel through
+    # the default routing (the path Flux's 6-27 MiB TP8 messages take)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), SHAI_P2P_MAX_BLOCKS="128", SHAI_P2P_TIMEOUT_S="10",
-                      SHAI_P2P_MAX_BYTES=str(8 << 20))
+                      SHAI_P2P_ONE_SHOT_MAX=str(4096))
     import torch.distributed as dist
     from shai_amd.engines.flux import FluxEngine, FluxPipelineConfig
     from shai_amd.parallel import comm
     from shai_amd.parallel.state import TPState, init_distributed, set_tp
     from shai_amd.models.flux import FluxConfig
     torch.cuda.set_device(0)
-    comm.P2P_MAX_BYTES = 8 << 20
+    comm.P2P_ONE_SHOT_MAX = 4096
 
     def cfg():  # head dims the GPU flash kernel takes (64 / 128), heads divisible by the TP degree
         c = FluxPipelineConfig.tiny()
@@ -118,6 +120,9 @@ def run_flux(rank, world, port):
             assert rel < 5e-2 and rel < 0.1 * rel_seed, (rel, rel_seed)
         torch.cuda.synchronize()
         assert not comm.p2p().error()
+        n = comm.p2p().launch_counts()
+        # the gated row-parallel outputs ran as GEMM-into-the-slot + the fused two-shot reduce
+        assert n["staged_two_shot"] > 0, n
     dist.barrier()
     comm.p2p().close()
     comm.enable_p2p(None)

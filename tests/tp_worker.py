@@ -122,6 +122,27 @@ def run(rank, world, port, which):
         load_into(m2, dict(sd), strict=True)
         with torch.no_grad():
             _close(m2(lat, t5, pooled, t, g, img_hw=(4, 6)), ref, 3e-2)
+    elif which == "mllama_vision":
+        # the Llama-3.2-Vision tower head-sharded (QKV column-parallel by heads, o_proj / fc2 row-parallel, fc1
+        # column-parallel) vs TP1, 3 valid tiles of 4 (padding queries take the exact masked path), gates folded
+        from shai_amd.models.mllama import MllamaConfig, MllamaVisionModel
+        vc = MllamaConfig.tiny().vision
+        vc.attention_heads = 4
+        _tp1()
+        m1 = MllamaVisionModel(vc)
+        init_random_(m1, 5)
+        for lyr in m1.global_layers:   # non-trivial tanh gates
+            lyr.gate_attn.fill_(0.7)
+            lyr.gate_ffn.fill_(-0.4)
+        sd = {k: v.clone() for k, v in m1.state_dict().items()}
+        px = torch.randn(2, vc.max_num_tiles, vc.image_size, vc.image_size, 3).to(torch.bfloat16)
+        ar = torch.tensor([3, 6])
+        ref = m1(px, ar, [3, 4])
+        init_distributed("gloo", tp_size=world)
+        m2 = MllamaVisionModel(vc)
+        assert m2.layers[0].self_attn.h == 4 // world
+        load_into(m2, dict(sd), strict=True)
+        _close(m2(px, ar, [3, 4]), ref, 3e-2)
     elif which == "row_overlap":
         # chunked row-parallel GEMM + all-reduce (compute / communication overlap path) vs the dense product
         from shai_amd.parallel import comm
