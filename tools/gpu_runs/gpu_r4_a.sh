@@ -1,10 +1,14 @@
 #!/bin/bash
-# Round 4, first GPU call: the P2P / decode tests touched this round (staged fused reduce, default two-shot
-# routing, partials placeholder), then the whole GPU suite, smoke, a short SD2.1 bench line.
+# Round 4, first GPU call: GEMM lab (v4 vs the new 4-wave 128x128-per-wave kernel, plain GEMMs), the P2P /
+# decode tests touched this round (staged fused reduce, default two-shot routing, partials placeholder,
+# 64k / 128k decode attention), then the whole GPU suite, smoke, a short SD2.1 bench line.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+timeout -k 10 300 ./tools/gemm_lab/bin/gemm_lab full --plain > gpurun_out/r4a_lab.log 2>&1 || { tail -30 gpurun_out/r4a_lab.log; exit 1; }
+grep -E "==|w4_256|v4_256w |MISMATCH" gpurun_out/r4a_lab.log | grep -v max_abs | head -60
+grep -c MISMATCH gpurun_out/r4a_lab.log
 timeout -k 10 400 python -u -m pytest tests/test_p2p_gpu.py tests/test_skinny_gpu.py -x -v --timeout 120 \
   --timeout-method thread > gpurun_out/r4a_pytest_p2p.log 2>&1 || { tail -40 gpurun_out/r4a_pytest_p2p.log; exit 1; }
 tail -3 gpurun_out/r4a_pytest_p2p.log
