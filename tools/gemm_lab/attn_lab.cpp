@@ -16,6 +16,7 @@
 namespace shai {
 void launch_flash2_exp(const AttnArgs& a, int exp, hipStream_t s);
 void flash2_read_stamps(unsigned long long* host);
+void launch_flash64_dma(const AttnArgs& a, int occ, hipStream_t s);
 }  // namespace shai
 using shai::bf16_t;
 
@@ -88,9 +89,13 @@ int main() {
       const int rows = 64;
       float* ref;
       CK(hipMalloc(&ref, rows * c.D * 4));
-      if (c.D == 64) shai::launch_flash64(a, 0);  // production d64 kernel
-      else shai::launch_flash2_exp(a, 0, 0);
       ref_rows<<<1, 64>>>(q, k, v, ref, c.S, c.H, c.D, rows, a.scale);
+      CK(hipDeviceSynchronize());
+      for (int kv = 0; kv < (c.D == 64 ? 3 : 1); ++kv) {
+      if (c.D == 64) {
+        if (kv == 0) shai::launch_flash64(a, 0);  // production d64 kernel
+        else shai::launch_flash64_dma(a, kv == 1 ? 2 : 4, 0);
+      } else shai::launch_flash2_exp(a, 0, 0);
       CK(hipDeviceSynchronize());
       std::vector<float> hr(rows * c.D);
       std::vector<bf16_t> ho(rows * ts);
@@ -105,16 +110,22 @@ int main() {
           err = fmax(err, fabs(f - hr[i * c.D + d]));
           mx = fmax(mx, fabs(hr[i * c.D + d]));
         }
-      printf("  %s max_abs_err %.4f (max |ref| %.3f) %s\n", c.D == 64 ? "flash64" : "flash2", err, mx, err < 0.02 * mx + 0.01 ? "OK" : "MISMATCH");
+      printf("  %s max_abs_err %.4f (max |ref| %.3f) %s\n", c.D == 64 ? (kv == 0 ? "flash64" : kv == 1 ? "f64dma-occ2" : "f64dma-occ4") : "flash2", err, mx, err < 0.02 * mx + 0.01 ? "OK" : "MISMATCH");
+      }
       CK(hipFree(ref));
     }
     struct V { const char* name; int exp; };  // exp < 0: v1
-    const V vars[] = {{"v1", -1}, {"flash2", 0}, {"flash64", -2}, {"f2-prev", 48}};
-    float best[4] = {1e30f, 1e30f, 1e30f, 1e30f};
+    const V vars[] = {{"v1", -1}, {"flash2", 0}, {"flash64", -2}, {"f64dma-occ2", -3}, {"f64dma-occ4", -4}};
+    constexpr int NV = sizeof(vars) / sizeof(vars[0]);
+    float best[NV];
+    for (int vi = 0; vi < NV; ++vi) best[vi] = 1e30f;
     for (int r = 0; r < 5; ++r)
-      for (int vi = 0; vi < 4; ++vi) {
+      for (int vi = 0; vi < NV; ++vi) {
+        if (vars[vi].exp <= -3 && c.D != 64) continue;
         auto run = [&]() {
           if (vars[vi].exp == -2) { if (c.D == 64) shai::launch_flash64(a, 0); }
+          else if (vars[vi].exp == -3) shai::launch_flash64_dma(a, 2, 0);
+          else if (vars[vi].exp == -4) shai::launch_flash64_dma(a, 4, 0);
           else if (vars[vi].exp < 0) shai::launch_flash_attn(a, 0);
           else shai::launch_flash2_exp(a, vars[vi].exp, 0);
         };
@@ -127,8 +138,9 @@ int main() {
         CK(hipEventElapsedTime(&ms, e0, e1));
         best[vi] = fminf(best[vi], ms / 10);
       }
-    for (int vi = 0; vi < 4; ++vi)
-      printf("  %-13s %8.1f us  %7.1f TF/s\n", vars[vi].name, best[vi] * 1e3, flop / (best[vi] * 1e-3) / 1e12);
+    for (int vi = 0; vi < NV; ++vi)
+      if (best[vi] < 1e29f)
+        printf("  %-13s %8.1f us  %7.1f TF/s\n", vars[vi].name, best[vi] * 1e3, flop / (best[vi] * 1e-3) / 1e12);
     // stamps: 4 per tile per wave (M start, M end, V start, V end); print mean durations over tiles 2..nt-2
     for (int exp : {4, 12}) {
       shai::launch_flash2_exp(a, exp, 0);

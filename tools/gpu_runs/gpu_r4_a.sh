@@ -9,6 +9,8 @@ mkdir -p gpurun_out
 timeout -k 10 300 ./tools/gemm_lab/bin/gemm_lab full --plain > gpurun_out/r4a_lab.log 2>&1 || { tail -30 gpurun_out/r4a_lab.log; exit 1; }
 grep -E "==|w4_256|v4_256w |MISMATCH" gpurun_out/r4a_lab.log | grep -v max_abs | head -60
 grep -c MISMATCH gpurun_out/r4a_lab.log
+timeout -k 10 300 ./tools/gemm_lab/bin/attn_lab > gpurun_out/r4a_attn_lab.log 2>&1 || { tail -30 gpurun_out/r4a_attn_lab.log; exit 1; }
+grep -v stamps gpurun_out/r4a_attn_lab.log
 timeout -k 10 400 python -u -m pytest tests/test_p2p_gpu.py tests/test_skinny_gpu.py -x -v --timeout 120 \
   --timeout-method thread > gpurun_out/r4a_pytest_p2p.log 2>&1 || { tail -40 gpurun_out/r4a_pytest_p2p.log; exit 1; }
 tail -3 gpurun_out/r4a_pytest_p2p.log
