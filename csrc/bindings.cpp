@@ -280,7 +280,7 @@ Choice tune(const shai::GemmArgs& g_real, const Tensor& like, bool skinny_only =
     const int ms = max_splits_for(g);
     for (int c = 0; c < shai::gemm2_num_cfgs(); ++c) {
       if (!shai::gemm2_cfg_supported(g, c)) continue;
-      for (int s = 1; s <= ms; s *= 2) cands.push_back({c, s});
+      for (int s = 1; s <= (shai::gemm2_cfg_splittable(c) ? ms : 1); s *= 2) cands.push_back({c, s});
     }
   }
   if (shai::skinny_supported(g))

@@ -366,6 +366,9 @@ constexpr int kNumCfgs = 5;
 // (gemm_pipe.hip); kNumCfgs + 4 / + 5 the 8-phase ping-pong v4 kernel (gemm_8ph.hip) with 256 / 320 wide tiles,
 // kNumCfgs + 6 / + 7 the same in its persistent form (next tile's operands prefetched under the epilogue).
 constexpr int kV4Cfg = kNumCfgs + 4;
+// kV4Cfg + 4: the four-wave 256 x 256 kernel with 128 x 128 wave tiles (gemm_w4.hip; plain / GLU GEMMs, no
+// split-K, no conv).
+constexpr int kW4Cfg = kV4Cfg + 4;
 
 
 template <bool CONV, bool FAST, bool GLU, int ACT>
@@ -475,6 +478,10 @@ static void launch_all(const GemmArgs& a, float* ws, int cfg, int splits, hipStr
 }
 
 void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStream_t s) {
+  if (cfg == kW4Cfg) {  // whole K per tile: a split-K choice is run unsplit
+    launch_gemm_w4(a, s);
+    return;
+  }
   if (cfg >= kV4Cfg) {
     const int v = cfg - kV4Cfg;
     launch_gemm4(a, ws, splits, (v & 1) ? 320 : 256, s, v >= 2);
@@ -512,9 +519,12 @@ void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipS
   }
 }
 
-int gemm2_num_cfgs() { return kV4Cfg + 4; }
+int gemm2_num_cfgs() { return kW4Cfg + 1; }
+
+bool gemm2_cfg_splittable(int cfg) { return cfg != kW4Cfg; }
 
 bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
+  if (cfg == kW4Cfg) return gemm_w4_supported(a);
   if (cfg >= kV4Cfg) return cfg < kV4Cfg + 4 && gemm4_supported(a);
   if (cfg >= kNumCfgs) return gemm3_supported(a);
   if (a.in_scale != nullptr) return false;
@@ -523,6 +533,11 @@ bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
 }
 
 void gemm2_cfg_info(int cfg, int* bm, int* bn) {
+  if (cfg == kW4Cfg) {  // four-wave kernel: reported as "4x-256"
+    *bm = 4;
+    *bn = -256;
+    return;
+  }
   if (cfg >= kV4Cfg) {  // 8-phase v4 kernel: reported as "8x-<BN>" ("9x-<BN>" persistent)
     *bm = cfg >= kV4Cfg + 2 ? 9 : 8;
     *bn = ((cfg - kV4Cfg) & 1) ? -320 : -256;

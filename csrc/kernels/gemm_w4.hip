@@ -51,7 +51,7 @@ __device__ __forceinline__ int w4_wperm(int r) {
   return g * 128 + (jb >> 1) * 32 + (nn >> 2) * 8 + (jb & 1) * 4 + (nn & 3);
 }
 
-template <int ACT>
+template <int ACT, bool GLU>
 __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) bf16_t w4_smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const GemmArgs p) {
     for (int i = 0; i < 8; ++i) {
       const long m = m0 + wr * 128 + 16 * i + fr;
       uint4_ rr[4];
-      if (R) {
+      if (!GLU && R) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           rr[q] = *reinterpret_cast<const uint4_*>(R + m * p.ldr + n0 + wc * 128 + q * 32 + 8 * fq);
@@ -242,16 +242,33 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const GemmArgs p) {
         float v[8];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = apply_act<ACT>(acc[i][2 * q][e] * p.alpha + bq[q][e]);
-          v[4 + e] = apply_act<ACT>(acc[i][2 * q + 1][e] * p.alpha + bq[q][4 + e]);
+          v[e] = acc[i][2 * q][e] * p.alpha + bq[q][e];
+          v[4 + e] = acc[i][2 * q + 1][e] * p.alpha + bq[q][4 + e];
         }
-        if (R) {
-          float r8[8];
-          unpack8(rr[q], r8);
+        if constexpr (GLU) {  // (value, gate) column pairs: the lane's 8 columns give 4 consecutive outputs
+          float o[4];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += r8[e] * p.res_alpha;
+          for (int e = 0; e < 4; ++e) o[e] = v[2 * e] * apply_act<ACT>(v[2 * e + 1]);
+          if (R) {
+            const uint2_ r2 = *reinterpret_cast<const uint2_*>(R + m * p.ldr + ((n0 + wc * 128 + q * 32 + 8 * fq) >> 1));
+            o[0] += bf2f(r2[0] & 0xffff) * p.res_alpha; o[1] += bf2f(r2[0] >> 16) * p.res_alpha;
+            o[2] += bf2f(r2[1] & 0xffff) * p.res_alpha; o[3] += bf2f(r2[1] >> 16) * p.res_alpha;
+          }
+          uint2_ w;
+          w[0] = pack2(o[0], o[1]);
+          w[1] = pack2(o[2], o[3]);
+          *reinterpret_cast<uint2_*>(C + m * p.ldc + ((n0 + wc * 128 + q * 32 + 8 * fq) >> 1)) = w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = apply_act<ACT>(v[e]);
+          if (R) {
+            float r8[8];
+            unpack8(rr[q], r8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += r8[e] * p.res_alpha;
+          }
+          *reinterpret_cast<uint4_*>(C + m * p.ldc + n0 + wc * 128 + q * 32 + 8 * fq) = pack8(v);
         }
-        *reinterpret_cast<uint4_*>(C + m * p.ldc + n0 + wc * 128 + q * 32 + 8 * fq) = pack8(v);
       }
     }
   } else {
@@ -261,12 +278,26 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const GemmArgs p) {
 #pragma unroll
       for (int jb = 0; jb < 8; ++jb) {
         const int n = n0 + wc * 128 + (jb >> 1) * 32 + 8 * fq + 4 * (jb & 1);
+        if constexpr (GLU) {  // edge tiles: guarded (value, gate) pairs
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {   // edge tiles: element-wise, guarded (no array indexed at run time)
-          if (m < p.M && n + e < p.N) {
-            float v = apply_act<ACT>(acc[i][jb][e] * p.alpha + (p.bias ? bf2f(p.bias[n + e]) : 0.f));
-            if (R) v += bf2f(R[(long)m * p.ldr + n + e]) * p.res_alpha;
-            C[(long)m * p.ldc + n + e] = f2bf(v);
+          for (int e = 0; e < 4; e += 2) {
+            if (m < p.M && n + e + 1 < p.N) {
+              const float a = acc[i][jb][e] * p.alpha + (p.bias ? bf2f(p.bias[n + e]) : 0.f);
+              const float gt = acc[i][jb][e + 1] * p.alpha + (p.bias ? bf2f(p.bias[n + e + 1]) : 0.f);
+              float v = a * apply_act<ACT>(gt);
+              const int nc = (n + e) >> 1;
+              if (R) v += bf2f(R[(long)m * p.ldr + nc]) * p.res_alpha;
+              C[(long)m * p.ldc + nc] = f2bf(v);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {   // edge tiles: element-wise, guarded (no array indexed at run time)
+            if (m < p.M && n + e < p.N) {
+              float v = apply_act<ACT>(acc[i][jb][e] * p.alpha + (p.bias ? bf2f(p.bias[n + e]) : 0.f));
+              if (R) v += bf2f(R[(long)m * p.ldr + n + e]) * p.res_alpha;
+              C[(long)m * p.ldc + n + e] = f2bf(v);
+            }
           }
         }
       }
@@ -275,7 +306,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const GemmArgs p) {
 }
 
 bool gemm_w4_supported(const GemmArgs& a) {
-  return a.conv == 0 && !a.glu && a.batch <= 1 && a.in_scale == nullptr && a.bias2d == nullptr &&
+  return a.conv == 0 && (!a.glu || a.N % 8 == 0) && a.batch <= 1 && a.in_scale == nullptr && a.bias2d == nullptr &&
          a.gate == nullptr && !a.rms && a.w_scale == nullptr && a.A2 == nullptr && a.K % 8 == 0 &&
          a.lda % 8 == 0 && a.ldw % 8 == 0 && (long)a.M * a.lda * 2 < 0x7fffffffL &&
          (long)a.N * a.ldw * 2 < 0x7fffffffL;
@@ -284,11 +315,21 @@ bool gemm_w4_supported(const GemmArgs& a) {
 void launch_gemm_w4(const GemmArgs& a, hipStream_t s) {
   const int tiles = ((a.M + W4_BM - 1) / W4_BM) * ((a.N + W4_BN - 1) / W4_BN);
   const size_t lds = (size_t)2 * W4_STAGE * sizeof(bf16_t);
+  if (a.glu) {
+    switch (a.act) {
+      case ACT_SILU: gemm_w4_kernel<ACT_SILU, true><<<tiles, 256, lds, s>>>(a); break;
+      case ACT_GELU_TANH: gemm_w4_kernel<ACT_GELU_TANH, true><<<tiles, 256, lds, s>>>(a); break;
+      default: gemm_w4_kernel<ACT_GELU, true><<<tiles, 256, lds, s>>>(a); break;
+    }
+    return;
+  }
   switch (a.act) {
-    case ACT_SILU: gemm_w4_kernel<ACT_SILU><<<tiles, 256, lds, s>>>(a); break;
-    case ACT_GELU: gemm_w4_kernel<ACT_GELU><<<tiles, 256, lds, s>>>(a); break;
-    case ACT_GELU_TANH: gemm_w4_kernel<ACT_GELU_TANH><<<tiles, 256, lds, s>>>(a); break;
-    default: gemm_w4_kernel<ACT_NONE><<<tiles, 256, lds, s>>>(a); break;
+    case ACT_SILU: gemm_w4_kernel<ACT_SILU, false><<<tiles, 256, lds, s>>>(a); break;
+    case ACT_GELU: gemm_w4_kernel<ACT_GELU, false><<<tiles, 256, lds, s>>>(a); break;
+    case ACT_GELU_TANH: gemm_w4_kernel<ACT_GELU_TANH, false><<<tiles, 256, lds, s>>>(a); break;
+    case ACT_QUICK_GELU: gemm_w4_kernel<ACT_QUICK_GELU, false><<<tiles, 256, lds, s>>>(a); break;
+    case ACT_RELU: gemm_w4_kernel<ACT_RELU, false><<<tiles, 256, lds, s>>>(a); break;
+    default: gemm_w4_kernel<ACT_NONE, false><<<tiles, 256, lds, s>>>(a); break;
   }
 }
 

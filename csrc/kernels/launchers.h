@@ -139,6 +139,10 @@ void gemm2_plan(const GemmArgs& a, int* cfg, int* splits);
 void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStream_t s);
 int gemm2_num_cfgs();
 bool gemm2_cfg_supported(const GemmArgs& a, int cfg);
+bool gemm2_cfg_splittable(int cfg);  // false: the config always runs the whole K (split-K choices are moot)
+// v5: four-wave 256 x 256 GEMM with 128 x 128 wave tiles (gemm_w4.hip): plain / bias / act / GLU / residual
+bool gemm_w4_supported(const GemmArgs& a);
+void launch_gemm_w4(const GemmArgs& a, hipStream_t s);
 // v3: pipelined 256x256 LDS-DMA GEMM / conv (gemm_pipe.hip); config index gemm2_num_cfgs() - 1
 bool gemm3_supported(const GemmArgs& a);
 void launch_gemm3(const GemmArgs& a, float* ws, int splits, int stages, hipStream_t s, int bn = 256);
