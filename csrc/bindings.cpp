@@ -853,7 +853,8 @@ void flash_attn(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor&
   a.Sq = q.size(1);
   a.Hq = q.size(2);
   a.D = q.size(3);
-  SHAI_CHECK(a.D == 64 || a.D == 128, "flash_attn supports head dim 64 / 128, got ", a.D);
+  SHAI_CHECK(a.D == 64 || a.D == 128 || (a.D == 512 && a.Hq == 1),
+             "flash_attn supports head dim 64 / 128 (and 512 with one head: the VAE mid-block), got ", a.D);
   SHAI_CHECK(q.stride(2) == a.D && o.stride(2) == a.D, "heads must be packed (head stride == D)");
   if (block_table) {
     // k/v are caches [num_blocks, Hkv, 64, D]
@@ -901,6 +902,12 @@ void flash_attn(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor&
     check_bf16(*bias, "bias");
     SHAI_CHECK(bias->is_contiguous() && bias->numel() == (long)a.Hq * a.Sq * a.Skv, "bias must be [Hq, Sq, Skv]");
     a.bias = cptr(*bias);
+  }
+  if (a.D == 512) {
+    SHAI_CHECK(shai::attn512_supported(a), "D = 512 attention: one head, no mask / bias / causal / paged K/V, "
+                                           "8-element aligned strides");
+    shai::launch_attn512(a, stream());
+    return;
   }
   shai::launch_flash_attn(a, stream());
 }

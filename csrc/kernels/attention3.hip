@@ -233,3 +233,184 @@ void launch_flash64_dma(const AttnArgs& a, int occ, hipStream_t s) {
 }
 
 }  // namespace shai
+
+namespace shai {
+
+// ----------------------------------------------------------------------------------------------------------
+// attn512: single-head attention with D = 512 -- the VAE mid-block self-attention (SD2.1 / Flux decoders:
+// 512 channels, one head, S = (H/8) x (W/8) latent pixels: 4096 at 512^2, 9216 at 768^2).  Fused flash
+// form instead of score GEMM -> softmax -> value GEMM: no S x S scores in HBM (the unfused path wrote up to
+// 512 MiB of score chunks per call).
+//
+// * Workgroup = 8 waves x 16 queries; each wave keeps its Q^T fragments (16 x 512, pre-scaled by
+//   scale * log2 e, 64 VGPRs) and O^T (512 x 16 fp32, 128 accumulators) in registers.
+// * K / V tiles of 32 keys x 512 (32 KB each) staged by LDS-DMA (one 1-KB row per wave-instruction),
+//   2-stage ring (128 KB); 16-B chunks XOR-swizzled on the source address: K by (key & 15) -> the
+//   ds_read_b128 A fragments are conflict-free; V by 2 (key & 3) + 8 ((key >> 2) & 1) -> the
+//   ds_read_b64_tr_b16 transposed reads (V^T fragments) are conflict-free per 32-lane half.
+// * S^T = K Q^T on v_mfma_f32_16x16x32_bf16: lane (query fq, group g) holds keys 4g..4g+3 of both 16-key
+//   blocks, which is exactly the B fragment P^T of the PV MFMA under the key order k' = 8g + j ->
+//   {4g + j, 16 + 4g + j - 4}: P feeds the PV MFMA from registers, no shuffles; the V^T fragment reads use
+//   the same key order.
+// * Online softmax in the exp2 domain with a deferred max: O / l are rescaled only when a query's tile max
+//   exceeds the running max by more than 2^8 (P <= 256 in bf16 otherwise).
+constexpr int A5_D = 512, A5_KT = 32, A5_WAVES = 8;
+constexpr int A5_STAGE = 2 * A5_KT * A5_D;  // bf16 elements: K tile then V tile
+
+__device__ __forceinline__ int a5_vswz(int r) { return 2 * (r & 3) + 8 * ((r >> 2) & 1); }
+
+__global__ void __launch_bounds__(512, 1) attn512_kernel(const AttnArgs p) {
+  constexpr float kThr = 8.f, kL2e = 1.4426950408889634f;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fq = lane & 15, g = lane >> 4;
+  const int b = blockIdx.y;
+  const int S = p.Skv;
+  const int qi = blockIdx.x * 128 + wid * 16 + fq;
+  const int nt = (S + A5_KT - 1) / A5_KT;
+
+  const bf16_t* kb_ = p.k + (long)b * p.k_bs;
+  const bf16_t* vb_ = p.v + (long)b * p.v_bs;
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(kb_), (short)0,
+                                                                      0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(vb_), (short)0,
+                                                                      0x7fffffff, 0x00020000);
+  // DMA: wave w moves K rows 4w .. 4w+3 and V rows 4w .. 4w+3 of each tile (one 1-KB row per instruction)
+  auto dma = [&](int stage, int t) {
+    bf16_t* ks = smem + stage * A5_STAGE;
+    bf16_t* vs = ks + A5_KT * A5_D;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = wid * 4 + i, key = t * A5_KT + r;
+      const uint32_t oob = key < S ? 0u : 0x80000000u;
+      const uint32_t ko = (uint32_t)(((long)key * p.k_ts + ((lane ^ (r & 15)) << 3)) * 2) | oob;
+      const uint32_t vo = (uint32_t)(((long)key * p.v_ts + ((lane ^ a5_vswz(r)) << 3)) * 2) | oob;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (f3_lds_void*)(ks + r * A5_D), 16, ko, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (f3_lds_void*)(vs + r * A5_D), 16, vo, 0, 0, 0);
+    }
+  };
+  if (nt > 0) dma(0, 0);
+
+  // Q^T fragments: lane (fq, g) holds q[qi][32 ds + 8 g .. + 8] * scale * log2 e
+  f3bf16x8 qf[16];
+  {
+    const float sl2 = p.scale * kL2e;
+    const bf16_t* qp = p.q + (long)b * p.q_bs + (long)min(qi, p.Sq - 1) * p.q_ts + 8 * g;
+#pragma unroll
+    for (int ds = 0; ds < 16; ++ds) {
+      uint4_ v = *reinterpret_cast<const uint4_*>(qp + 32 * ds);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= sl2;
+      qf[ds] = __builtin_bit_cast(f3bf16x8, pack8(f));
+    }
+  }
+  // per-lane LDS byte offsets: K fragment (row fq, chunk (4 ds + g) ^ fq) = koff[ds & 3] + 256 (ds >> 2);
+  // V^T fragment of d-block db (rows 4g + q (+16), chunk (2 db + (p >> 1)) ^ vswz) = voff[db & 3] + 128 (db >> 2)
+  const int fh = fq >> 2, tq = fq >> 2, tp = lane & 3;
+  int koff[4], voff[4];
+#pragma unroll
+  for (int bb = 0; bb < 4; ++bb) {
+    koff[bb] = fq * A5_D * 2 + ((((bb ^ fh) << 2) | ((g ^ fq) & 3)) << 4);
+    const int r = 4 * g + tq;
+    voff[bb] = r * A5_D * 2 + ((2 * bb + (tp >> 1)) ^ a5_vswz(r)) * 16 + (tp & 1) * 8;
+  }
+
+  float4_ o[32];
+  float m_run = -INFINITY, l_lane = 0.f;
+  bool first = true;
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < nt) dma(cur ^ 1, t + 1);
+    const char* ks = reinterpret_cast<const char*>(smem + cur * A5_STAGE);
+    const char* vs = ks + A5_KT * A5_D * 2;
+    float4_ s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const float4_ z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < 16; ++ds) {
+        const f3bf16x8 kf = *reinterpret_cast<const f3bf16x8*>(ks + koff[ds & 3] + 256 * (ds >> 2) + kb * 16 * A5_D * 2);
+        s[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ds], ds == 0 ? z : s[kb], 0, 0, 0);
+      }
+    }
+    const int key0 = t * A5_KT;
+    if (key0 + A5_KT > S) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[kb][r] = key0 + kb * 16 + 4 * g + r < S ? s[kb][r] : -INFINITY;
+    }
+    float mt = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
+                     fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    if (__any(mt > m_run + kThr)) {  // deferred max: rescale only on a large jump (or the first tile)
+      const float m_new = fmaxf(m_run, mt);
+      const float alpha = m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_run - m_new);
+      if (!first) {
+#pragma unroll
+        for (int db = 0; db < 32; ++db) o[db] *= alpha;
+      }
+      l_lane *= alpha;
+      m_run = m_new;
+    }
+    const float mu = m_run == -INFINITY ? 0.f : m_run;
+    f3bf16x8 pf;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = __builtin_amdgcn_exp2f(s[kb][r] - mu);
+        l_lane += e;
+        pf[4 * kb + r] = (__bf16)e;
+      }
+#pragma unroll
+    for (int db = 0; db < 32; ++db) {
+      const char* a0 = vs + voff[db & 3] + 128 * (db >> 2);
+      const f3s4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) f3s4v*)(a0));
+      const f3s4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) f3s4v*)(a0 + 16 * A5_D * 2));
+      short8 vv;
+      vv[0] = t0[0]; vv[1] = t0[1]; vv[2] = t0[2]; vv[3] = t0[3];
+      vv[4] = t1[0]; vv[5] = t1[1]; vv[6] = t1[2]; vv[7] = t1[3];
+      const float4_ z = {0.f, 0.f, 0.f, 0.f};
+      o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(f3bf16x8, vv), pf, first ? z : o[db], 0, 0, 0);
+    }
+    first = false;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this stage's reads done before it is restaged
+  }
+
+  float l = l_lane + __shfl_xor(l_lane, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  if (qi < p.Sq && nt > 0) {
+    bf16_t* op = p.o + (long)b * p.o_bs + (long)qi * p.o_ts + 4 * g;
+#pragma unroll
+    for (int db = 0; db < 32; ++db) {
+      uint2_ w;
+      w[0] = pack2(o[db][0] * inv, o[db][1] * inv);
+      w[1] = pack2(o[db][2] * inv, o[db][3] * inv);
+      *reinterpret_cast<uint2_*>(op + 16 * db) = w;
+    }
+  }
+}
+
+bool attn512_supported(const AttnArgs& a) {
+  return a.D == 512 && a.Hq == 1 && a.Hkv == 1 && a.Sq == a.Skv && a.bias == nullptr && a.block_table == nullptr &&
+         !a.causal && a.kv_lens == nullptr && a.q_lens == nullptr && a.q_start == nullptr &&
+         ((a.k_ts | a.v_ts | a.q_ts | a.o_ts) & 7) == 0 && (long)a.Skv * a.k_ts * 2 < 0x7fffffffL &&
+         (long)a.Skv * a.v_ts * 2 < 0x7fffffffL;
+}
+
+void launch_attn512(const AttnArgs& a, hipStream_t s) {
+  dim3 grid((a.Sq + 127) / 128, a.B);
+  attn512_kernel<<<grid, 512, (size_t)2 * A5_STAGE * sizeof(bf16_t), s>>>(a);
+}
+
+}  // namespace shai

@@ -197,6 +197,9 @@ bool flash2_supported(const AttnArgs& a);
 bool flash64_supported(const AttnArgs& a);
 void launch_flash64(const AttnArgs& a, hipStream_t s);
 void launch_flash2(const AttnArgs& a, hipStream_t s);
+// D = 512 single-head fused attention (attention3.hip; the VAE mid-block)
+bool attn512_supported(const AttnArgs& a);
+void launch_attn512(const AttnArgs& a, hipStream_t s);
 
 struct DecodeAttnArgs {
   const bf16_t* q;          // [B, Hq, D]

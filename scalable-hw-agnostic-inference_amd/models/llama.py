@@ -36,6 +36,9 @@ FUSED_DECODE = os.environ.get("SHAI_FUSED_DECODE", "1") != "0"
 # decode with the norm folded into qkv_proj: the QKV GEMM's split-K fold runs inside the attention kernel
 # (one launch fewer per layer); SHAI_QKV_FOLD_IN_ATTN=0 keeps the GEMM's own fold launch
 QKV_FOLD_IN_ATTN = os.environ.get("SHAI_QKV_FOLD_IN_ATTN", "1") != "0"
+# ... only up to this many decode-attention splits: every split workgroup of a (row, KV head) re-reads all the
+# partial slabs, so at long contexts (decode_splits raises the count to 16-64) the separate fold is cheaper
+QKV_FOLD_MAX_SPLITS = int(os.environ.get("SHAI_QKV_FOLD_MAX_SPLITS", "8"))
 
 KV_BLOCK = 64
 
@@ -175,7 +178,7 @@ class LlamaAttention(nn.Module):
         h, hk, hd = self.h, self.hk, self.hd
         qp = self.qkv_proj
         if (not batch.is_prefill and FUSED_DECODE and QKV_FOLD_IN_ATTN and rms_eps is not None and x.is_cuda
-                and T <= 64 and qp.bias is None and qp.w_scale is None and qp.weight.dtype == torch.bfloat16
+                and (batch.num_splits or 1) <= QKV_FOLD_MAX_SPLITS and T <= 64 and qp.bias is None and qp.w_scale is None and qp.weight.dtype == torch.bfloat16
                 and x.is_contiguous() and x.shape[1] >= 2048):
             o = ops.decode_attention_rope_qkv(x, qp.weight, rms_eps, k_cache, v_cache, batch.block_table,
                                               batch.ctx_lens, batch.positions, cos, sin, batch.slots, h, hk,

@@ -11,6 +11,7 @@ register tile).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Tuple
 
@@ -47,6 +48,10 @@ class VAEConfig:
         return VAEConfig(latent_channels=latent_channels, block_out_channels=(32, 32, 32, 64), layers_per_block=1)
 
 
+# SHAI_VAE_FUSED_ATTN=0: the unfused score GEMM -> softmax -> value GEMM path (chunked scores)
+VAE_FUSED_ATTN = os.environ.get("SHAI_VAE_FUSED_ATTN", "1") != "0"
+
+
 class VAEAttention(nn.Module):
     SCORE_BYTES = 512 << 20
 
@@ -63,6 +68,11 @@ class VAEAttention(nn.Module):
         qkv = self.qkv(h)
         q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
         S = H * W
+        if x.is_cuda and C in (64, 128, 512) and VAE_FUSED_ATTN:
+            # fused flash attention on the strided q / k / v views of the qkv rows (one head; D = 512 is the
+            # dedicated attention3.hip kernel): no S x S scores in HBM
+            o = ops.attention(q.view(B, S, 1, C), k.view(B, S, 1, C), v.view(B, S, 1, C), scale=1.0 / math.sqrt(C))
+            return self.out(o.view(B, S, C), residual=x.view(B, H * W, C)).view(B, H, W, C)
         k, vt = k.contiguous(), v.transpose(1, 2).contiguous()
         # single head, d = 512: score GEMM -> row softmax -> value GEMM, over query-row chunks so the bf16
         # score buffer stays <= SCORE_BYTES whatever the batch and resolution (768^2: S = 9216 -> 170 MB of

@@ -298,6 +298,24 @@ def test_flash_attn_bias_d64_long(cuda):
     close(ops.attention(q, k, v, scale=1.0, bias=bias), ref.attention(q, k, v, 1.0, bias=bias), 3e-2)
 
 
+@pytest.mark.parametrize("S", [1000, 4096])
+def test_attention_d512_vae(cuda, S):
+    """The VAE mid-block attention (one head, D = 512) on the fused attention3.hip kernel against the fp32
+    reference: q / k / v are strided views of one [B, S, 3 * 512] qkv tensor (as models/vae.py passes them),
+    S = 1000 exercises the key / query tails (tiles of 32 keys, workgroups of 128 queries)."""
+    torch.manual_seed(31)
+    B, C = 2, 512
+    qkv = rnd(B, S, 3 * C)
+    q, k, v = (qkv[..., i * C:(i + 1) * C].view(B, S, 1, C) for i in range(3))
+    sc = 1.0 / math.sqrt(C)
+    o = ops.attention(q, k, v, scale=sc)
+    close(o, ref.attention(q, k, v, sc), 2e-2)
+    # a query row aligned with one key: the softmax is dominated by it (exercises the deferred-max rescale)
+    k2 = k.clone()
+    k2[0, S // 2, 0] = (q[0, 7, 0].float() * 3.0).to(torch.bfloat16)
+    close(ops.attention(q, k2, v, scale=sc), ref.attention(q, k2, v, sc), 2e-2)
+
+
 def _paged_setup(B, Hkv, D, ctx, nblocks=64):
     kc = rnd(nblocks, Hkv, 64, D)
     vc = rnd(nblocks, Hkv, 64, D)

@@ -11,7 +11,7 @@ grep -E "==|w4_256|v4_256w |MISMATCH" gpurun_out/r4a_lab.log | grep -v max_abs |
 grep -c MISMATCH gpurun_out/r4a_lab.log
 timeout -k 10 300 ./tools/gemm_lab/bin/attn_lab > gpurun_out/r4a_attn_lab.log 2>&1 || { tail -30 gpurun_out/r4a_attn_lab.log; exit 1; }
 grep -v stamps gpurun_out/r4a_attn_lab.log
-timeout -k 10 400 python -u -m pytest tests/test_p2p_gpu.py tests/test_skinny_gpu.py -x -v --timeout 120 \
+timeout -k 10 400 python -u -m pytest tests/test_p2p_gpu.py tests/test_skinny_gpu.py tests/test_kernels_gpu.py -k "p2p or tp2 or skinny or qkv or d512 or long_context or decode" -x -v --timeout 120 \
   --timeout-method thread > gpurun_out/r4a_pytest_p2p.log 2>&1 || { tail -40 gpurun_out/r4a_pytest_p2p.log; exit 1; }
 tail -3 gpurun_out/r4a_pytest_p2p.log
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
