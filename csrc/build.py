@@ -35,6 +35,9 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 KERNEL_SRCS = ["kernels/norm.hip", "kernels/gemm.hip", "kernels/gemm_lds.hip", "kernels/gemm_pipe.hip", "kernels/gemm_8ph.hip", "kernels/gemm_w4.hip", "kernels/attention.hip", "kernels/attention2.hip", "kernels/attention3.hip", "kernels/elementwise.hip", "kernels/dit.hip",
                "kernels/sampling.hip", "kernels/gemv.hip", "kernels/gemv2.hip",
                "kernels/gemm_f8.hip"]
+# per-source extra hipcc flags: gemm_w4's epilogue (256 accumulators x an activation) is larger than LLVM's
+# default pragma-unroll budget; partially unrolled it would index the accumulators at run time (scratch)
+EXTRA_KFLAGS = {"kernels/gemm_w4.hip": "-mllvm -pragma-unroll-threshold=100000"}
 BINDING_SRCS = ["bindings.cpp"]
 RUNTIME_SRCS = ["runtime/block_manager.cpp", "runtime/scheduler.cpp"]
 COMM_SRCS = ["comm/p2p_allreduce.hip"]
@@ -100,6 +103,8 @@ def write_ninja(path: str) -> dict:
             o = os.path.join(BUILD, s.replace("/", "_") + ".o")
             lines.append(f"build {o}: {rule} {os.path.join(CSRC, s)} | {os.path.join(CSRC, 'kernels', 'common.h')} "
                          f"{os.path.join(CSRC, 'kernels', 'launchers.h')}")
+            if s in EXTRA_KFLAGS:
+                lines.append(f"  kflags = $kflags {EXTRA_KFLAGS[s]}")
             out.append(o)
         return out
 

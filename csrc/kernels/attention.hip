@@ -517,6 +517,14 @@ bool flash64_supported(const AttnArgs& a) {
 }
 
 void launch_flash64(const AttnArgs& a, hipStream_t s) {
+  static const bool dma = [] {  // SHAI_FLASH64_DMA=0: the register-staged kernel below (A/B)
+    const char* e = getenv("SHAI_FLASH64_DMA");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  if (dma && flash64_dma_supported(a)) {
+    launch_flash64_dma(a, 2, s);
+    return;
+  }
   dim3 grid((a.Sq + 127) / 128, a.Hq, a.B);
   const size_t lds = (size_t)4 * 64 * 64 * sizeof(bf16_t);
   if (a.causal) flash64_kernel<true><<<grid, 256, lds, s>>>(a);

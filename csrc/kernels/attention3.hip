@@ -1,9 +1,11 @@
-// flash64 with LDS-DMA K/V staging (lab variant, `launch_flash64_dma`): the register-staged K/V pipeline of
+// flash64 with LDS-DMA K/V staging (`launch_flash64_dma`, production for D = 64): the register-staged K/V pipeline of
 // flash64 (attention.hip) holds 16 VGPRs of next-tile K/V plus the ds_write pass; staging the tiles with
 // `buffer_load ... lds` (source-side swizzle, lane-linear LDS image) frees them, and the softmax computes P in
 // chunks of 8 exponentials instead of a 32-float buffer, so the kernel can aim at 4 waves per SIMD (128 VGPRs)
 // instead of 3 (168): more co-resident waves to overlap one wave's MFMAs with another's softmax, which is what
-// bounds D = 64 attention (VALU issue + latency, profiles/pmc_round3.md: 37 % MFMA busy).
+// bounds D = 64 attention (VALU issue + latency, profiles/pmc_round3.md: 37 % MFMA busy).  Measured (attention lab,
+// round 4): at 3 waves / SIMD (150 VGPRs) 906 vs 821 TF/s at the SD2.1 64x64 shape, 616 vs 557 at 32x32; forcing 4
+// waves spills (23 VGPRs) and halves the rate, so production runs the 3-wave build.
 #include "common.h"
 #include "launchers.h"
 
@@ -18,7 +20,7 @@ typedef __attribute__((address_space(3))) void f3_lds_void;
 __device__ __forceinline__ int f3_kswz(int row, int ch) { return row * 64 + ((ch ^ ((row >> 1) & 7)) << 3); }
 __device__ __forceinline__ int f3_vswz(int row, int ch) { return row * 64 + ((ch ^ (((row >> 1) & 1) << 2)) << 3); }
 
-template <int OCC>
+template <int OCC, bool CAUSAL>
 __global__ void __launch_bounds__(256, OCC) flash64_dma_kernel(const AttnArgs p) {
   constexpr int D = 64, KT = 64, NS = 4, ND = 2;
   constexpr float kSumThr = 256.f;
@@ -31,7 +33,9 @@ __global__ void __launch_bounds__(256, OCC) flash64_dma_kernel(const AttnArgs p)
   const int fr = lane & 31, fh = lane >> 5;
   const int b = blockIdx.z, hq = blockIdx.y;
   const int hk = hq / (p.Hq / p.Hkv);
-  const int q_len = p.Sq, kv_len = p.Skv;
+  const int q_len = p.q_lens ? p.q_lens[b] : p.Sq;
+  const int kv_len = p.kv_lens ? p.kv_lens[b] : p.Skv;
+  const int c_off = p.q_lens ? kv_len - q_len : p.causal_offset;
   if ((int)blockIdx.x * 128 >= q_len) return;
   const int q0 = blockIdx.x * 128;
   const int qi = q0 + wid * 32 + fr;
@@ -43,7 +47,9 @@ __global__ void __launch_bounds__(256, OCC) flash64_dma_kernel(const AttnArgs p)
       const_cast<bf16_t*>(kbase), (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16_t*>(vbase), (short)0, 0x7fffffff, 0x00020000);
-  const int ntiles = (kv_len + KT - 1) / KT;
+  int kv_end = kv_len;
+  if (CAUSAL) kv_end = min(kv_end, q0 + 127 + c_off + 1);
+  const int ntiles = kv_end > 0 ? (kv_end + KT - 1) / KT : 0;
   // DMA: wave wid moves K rows 16 wid + 8 i + (lane >> 3) (i < 2) and the same V rows; lane position lane & 7
   // of the 128-B row receives source chunk (pos ^ swizzle(row))
   const int drow = wid * 16 + (lane >> 3), dpos = lane & 7;
@@ -65,7 +71,8 @@ __global__ void __launch_bounds__(256, OCC) flash64_dma_kernel(const AttnArgs p)
 
   f3bf16x8 qf[NS];
   {
-    const bf16_t* qp = p.q + (long)b * p.q_bs + (long)min(qi, q_len - 1) * p.q_ts + (long)hq * D;
+    const bf16_t* qp = p.q + (p.q_start ? (long)p.q_start[b] * p.q_ts : (long)b * p.q_bs) +
+                        (long)min(qi, q_len - 1) * p.q_ts + (long)hq * D;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       uint4_ v = *reinterpret_cast<const uint4_*>(qp + 16 * s + 8 * fh);
@@ -142,13 +149,14 @@ __global__ void __launch_bounds__(256, OCC) flash64_dma_kernel(const AttnArgs p)
       }
     }
     const int key0 = t * KT;
-    if (key0 + KT > kv_len) {
+    if ((key0 + KT > kv_len) || (CAUSAL && key0 + KT - 1 > q0 + c_off)) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-          sacc[kb][r] = key >= kv_len ? -INFINITY : sacc[kb][r];
+          const bool bad = key >= kv_len || (CAUSAL && key > qi + c_off);
+          sacc[kb][r] = bad ? -INFINITY : sacc[kb][r];
         }
     }
     float ls = 0.f;
@@ -205,7 +213,8 @@ __global__ void __launch_bounds__(256, OCC) flash64_dma_kernel(const AttnArgs p)
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   if (qi < q_len) {
-    bf16_t* op = p.o + (long)b * p.o_bs + (long)qi * p.o_ts + (long)hq * D;
+    bf16_t* op = p.o + (p.q_start ? (long)p.q_start[b] * p.o_ts : (long)b * p.o_bs) + (long)qi * p.o_ts +
+                 (long)hq * D;
 #pragma unroll
     for (int d = 0; d < ND; ++d)
 #pragma unroll
@@ -219,17 +228,23 @@ __global__ void __launch_bounds__(256, OCC) flash64_dma_kernel(const AttnArgs p)
   }
 }
 
+// Same contract as flash64 (attention.hip): D = 64, causal (+ offset), per-batch q / kv lengths, packed varlen
+// q / o, GQA; K / V rows addressed through 32-bit buffer offsets.
 bool flash64_dma_supported(const AttnArgs& a) {
-  return a.D == 64 && a.bias == nullptr && a.block_table == nullptr && !a.causal && a.kv_lens == nullptr &&
-         a.q_lens == nullptr && a.q_start == nullptr && ((a.k_ts | a.v_ts | a.q_ts) & 7) == 0 &&
+  return a.D == 64 && a.bias == nullptr && a.block_table == nullptr && ((a.k_ts | a.v_ts | a.q_ts) & 7) == 0 &&
          (long)a.Skv * a.k_ts * 2 < 0x7fffffffL && (long)a.Skv * a.v_ts * 2 < 0x7fffffffL;
 }
 
 void launch_flash64_dma(const AttnArgs& a, int occ, hipStream_t s) {
   dim3 grid((a.Sq + 127) / 128, a.Hq, a.B);
   const size_t lds = (size_t)2 * 2 * 64 * 64 * sizeof(bf16_t);
-  if (occ >= 4) flash64_dma_kernel<4><<<grid, 256, lds, s>>>(a);
-  else flash64_dma_kernel<2><<<grid, 256, lds, s>>>(a);
+  if (occ >= 4) {
+    if (a.causal) flash64_dma_kernel<4, true><<<grid, 256, lds, s>>>(a);
+    else flash64_dma_kernel<4, false><<<grid, 256, lds, s>>>(a);
+  } else {
+    if (a.causal) flash64_dma_kernel<2, true><<<grid, 256, lds, s>>>(a);
+    else flash64_dma_kernel<2, false><<<grid, 256, lds, s>>>(a);
+  }
 }
 
 }  // namespace shai

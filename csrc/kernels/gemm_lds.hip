@@ -366,8 +366,8 @@ constexpr int kNumCfgs = 5;
 // (gemm_pipe.hip); kNumCfgs + 4 / + 5 the 8-phase ping-pong v4 kernel (gemm_8ph.hip) with 256 / 320 wide tiles,
 // kNumCfgs + 6 / + 7 the same in its persistent form (next tile's operands prefetched under the epilogue).
 constexpr int kV4Cfg = kNumCfgs + 4;
-// kV4Cfg + 4: the four-wave 256 x 256 kernel with 128 x 128 wave tiles (gemm_w4.hip; plain / GLU GEMMs, no
-// split-K, no conv).
+// kV4Cfg + 4 / + 5: the four-wave kernel (gemm_w4.hip) with 256 x 256 / 192 x 320 tiles (128 x 128 / 96 x 160
+// wave tiles; plain GEMM, GLU, conv; no split-K).
 constexpr int kW4Cfg = kV4Cfg + 4;
 
 
@@ -478,8 +478,8 @@ static void launch_all(const GemmArgs& a, float* ws, int cfg, int splits, hipStr
 }
 
 void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStream_t s) {
-  if (cfg == kW4Cfg) {  // whole K per tile: a split-K choice is run unsplit
-    launch_gemm_w4(a, s);
+  if (cfg == kW4Cfg || cfg == kW4Cfg + 1) {  // whole K per tile: a split-K choice is run unsplit
+    launch_gemm_w4(a, cfg == kW4Cfg ? 256 : 320, s);
     return;
   }
   if (cfg >= kV4Cfg) {
@@ -519,12 +519,12 @@ void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipS
   }
 }
 
-int gemm2_num_cfgs() { return kW4Cfg + 1; }
+int gemm2_num_cfgs() { return kW4Cfg + 2; }
 
-bool gemm2_cfg_splittable(int cfg) { return cfg != kW4Cfg; }
+bool gemm2_cfg_splittable(int cfg) { return cfg != kW4Cfg && cfg != kW4Cfg + 1; }
 
 bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
-  if (cfg == kW4Cfg) return gemm_w4_supported(a);
+  if (cfg == kW4Cfg || cfg == kW4Cfg + 1) return gemm_w4_supported(a);
   if (cfg >= kV4Cfg) return cfg < kV4Cfg + 4 && gemm4_supported(a);
   if (cfg >= kNumCfgs) return gemm3_supported(a);
   if (a.in_scale != nullptr) return false;
@@ -533,9 +533,9 @@ bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
 }
 
 void gemm2_cfg_info(int cfg, int* bm, int* bn) {
-  if (cfg == kW4Cfg) {  // four-wave kernel: reported as "4x-256"
+  if (cfg == kW4Cfg || cfg == kW4Cfg + 1) {  // four-wave kernel: reported as "4x-256" / "4x-320"
     *bm = 4;
-    *bn = -256;
+    *bn = cfg == kW4Cfg ? -256 : -320;
     return;
   }
   if (cfg >= kV4Cfg) {  // 8-phase v4 kernel: reported as "8x-<BN>" ("9x-<BN>" persistent)

@@ -140,9 +140,9 @@ void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStre
 int gemm2_num_cfgs();
 bool gemm2_cfg_supported(const GemmArgs& a, int cfg);
 bool gemm2_cfg_splittable(int cfg);  // false: the config always runs the whole K (split-K choices are moot)
-// v5: four-wave 256 x 256 GEMM with 128 x 128 wave tiles (gemm_w4.hip): plain / bias / act / GLU / residual
+// v5: four-wave GEMM / implicit-GEMM conv (gemm_w4.hip), bn = 256: 256 x 256 tiles, bn = 320: 192 x 320 tiles
 bool gemm_w4_supported(const GemmArgs& a);
-void launch_gemm_w4(const GemmArgs& a, hipStream_t s);
+void launch_gemm_w4(const GemmArgs& a, int bn, hipStream_t s);
 // v3: pipelined 256x256 LDS-DMA GEMM / conv (gemm_pipe.hip); config index gemm2_num_cfgs() - 1
 bool gemm3_supported(const GemmArgs& a);
 void launch_gemm3(const GemmArgs& a, float* ws, int splits, int stages, hipStream_t s, int bn = 256);
@@ -197,6 +197,9 @@ bool flash2_supported(const AttnArgs& a);
 bool flash64_supported(const AttnArgs& a);
 void launch_flash64(const AttnArgs& a, hipStream_t s);
 void launch_flash2(const AttnArgs& a, hipStream_t s);
+// flash64 with LDS-DMA K/V staging (attention3.hip; launch_flash64 routes to it, SHAI_FLASH64_DMA=0 opts out)
+bool flash64_dma_supported(const AttnArgs& a);
+void launch_flash64_dma(const AttnArgs& a, int occ, hipStream_t s);
 // D = 512 single-head fused attention (attention3.hip; the VAE mid-block)
 bool attn512_supported(const AttnArgs& a);
 void launch_attn512(const AttnArgs& a, hipStream_t s);

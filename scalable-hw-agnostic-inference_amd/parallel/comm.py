@@ -302,7 +302,8 @@ class P2PAllReduce:
         ptr = self.lib.shai_p2p_staging(self.ctx, ctypes.byref(cap))
         assert rows * cols * 2 <= cap.value
         idx = device.index if getattr(device, "index", None) is not None else torch.cuda.current_device()
-        return torch.ops.shai.from_ptr(int(ptr), [rows, cols], torch.bfloat16, int(idx))
+        from .. import native
+        return native.ops().from_ptr(int(ptr), [rows, cols], torch.bfloat16, int(idx))
 
     def reduce_staged(self, out: torch.Tensor, ncols: int, bias: Optional[torch.Tensor] = None,
                       residual: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None,

@@ -16,7 +16,6 @@
 namespace shai {
 void launch_flash2_exp(const AttnArgs& a, int exp, hipStream_t s);
 void flash2_read_stamps(unsigned long long* host);
-void launch_flash64_dma(const AttnArgs& a, int occ, hipStream_t s);
 }  // namespace shai
 using shai::bf16_t;
 
@@ -67,6 +66,7 @@ int main() {
   struct Case { int B, H, S, D; };
   const Case cases[] = {{8, 5, 4096, 64}, {8, 10, 1024, 64}, {1, 24, 4608, 128}, {4, 32, 2048, 128}};
   setenv("SHAI_FLASH_V1", "1", 1);  // launch_flash_attn -> v1 kernel
+  setenv("SHAI_FLASH64_DMA", "0", 1);  // launch_flash64 -> the register-staged kernel (the DMA one is its own row)
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));

@@ -8,7 +8,9 @@ FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=fast -I$ROOT/csrc -DSH
 for src in gemm_lds gemm_pipe gemm_8ph gemm_w4 attention attention2 attention3; do
   # incremental: rebuild an object only when its source or a shared header is newer
   if [ ! -f "$OUT/$src.o" ] || [ -n "$(find "$ROOT/csrc/kernels/$src.hip" "$ROOT/csrc/kernels/"*.h -newer "$OUT/$src.o")" ]; then
-    hipcc $FLAGS -c "$ROOT/csrc/kernels/$src.hip" -o "$OUT/$src.o" &
+    extra=""
+    [ "$src" = gemm_w4 ] && extra="-mllvm -pragma-unroll-threshold=100000"   # as csrc/build.py EXTRA_KFLAGS
+    hipcc $FLAGS $extra -c "$ROOT/csrc/kernels/$src.hip" -o "$OUT/$src.o" &
   fi
 done
 hipcc $FLAGS -x hip -c "$ROOT/tools/gemm_lab/gemm_lab.cpp" -o "$OUT/gemm_lab.o" &

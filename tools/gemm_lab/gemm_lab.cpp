@@ -19,7 +19,7 @@ void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t 
 bool gemm4_supported(const GemmArgs& a);
 void launch_gemm4_var(const GemmArgs& a, int var, int bn, hipStream_t s);
 bool gemm_w4_supported(const GemmArgs& a);
-void launch_gemm_w4(const GemmArgs& a, hipStream_t s);
+void launch_gemm_w4(const GemmArgs& a, int bn, hipStream_t s);
 }  // namespace shai
 
 using shai::bf16_t;
@@ -206,14 +206,15 @@ int main(int argc, char** argv) {
     const char* name;
     int kind;  // 0: v3 256 4-stage, 1: v3 256 2-stage, 2: v3 320 2-stage, 10+v: v4 schedule variant v
   };
-  const Var vars[] = {{"v4_256w", 30}, {"v4_256pwn", 70}, {"v4_320w", 130}, {"v4_320pwn", 170}, {"w4_256", 5}};
+  const Var vars[] = {{"v4_256w", 30}, {"v4_256pwn", 70}, {"v4_320w", 130}, {"v4_320pwn", 170}, {"w4_256", 5}, {"w4_320", 6}};
   constexpr int NV = sizeof(vars) / sizeof(vars[0]);
   auto run = [&](const Var& v, const shai::GemmArgs& g) {
     switch (v.kind) {
       case 0: shai::launch_gemm3(g, nullptr, 1, 4, s, 256); break;
       case 1: shai::launch_gemm3(g, nullptr, 1, 2, s, 256); break;
       case 2: shai::launch_gemm3(g, nullptr, 1, 2, s, 320); break;
-      case 5: shai::launch_gemm_w4(g, s); break;
+      case 5: shai::launch_gemm_w4(g, 256, s); break;
+      case 6: shai::launch_gemm_w4(g, 320, s); break;
       default: shai::launch_gemm4_var(g, v.kind % 100 - 10, v.kind >= 100 ? 320 : 256, s); break;
     }
   };
@@ -240,7 +241,7 @@ int main(int argc, char** argv) {
     std::vector<float> best(NV, 1e30f);
     for (int vi = 0; vi < NV; ++vi) {
       if (vars[vi].kind >= 10 && !shai::gemm4_supported(g)) continue;
-      if (vars[vi].kind == 5 && !shai::gemm_w4_supported(g)) continue;
+      if ((vars[vi].kind == 5 || vars[vi].kind == 6) && !shai::gemm_w4_supported(g)) continue;
       CK(hipMemset(C, 0, (size_t)P.M * P.N * 2));
       CK(hipMemset(err, 0, 8));
       run(vars[vi], g);
@@ -257,7 +258,7 @@ int main(int argc, char** argv) {
     for (int r = 0; r < rounds; ++r) {
       for (int vi = 0; vi < NV; ++vi) {
         if (vars[vi].kind >= 10 && !shai::gemm4_supported(g)) continue;
-        if (vars[vi].kind == 5 && !shai::gemm_w4_supported(g)) continue;
+        if ((vars[vi].kind == 5 || vars[vi].kind == 6) && !shai::gemm_w4_supported(g)) continue;
         run(vars[vi], g);
         CK(hipEventRecord(e0, s));
         for (int it = 0; it < iters; ++it) run(vars[vi], g);

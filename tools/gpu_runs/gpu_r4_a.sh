@@ -6,8 +6,8 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 ./tools/gemm_lab/bin/gemm_lab full --plain > gpurun_out/r4a_lab.log 2>&1 || { tail -30 gpurun_out/r4a_lab.log; exit 1; }
-grep -E "==|w4_256|v4_256w |MISMATCH" gpurun_out/r4a_lab.log | grep -v max_abs | head -60
+timeout -k 10 400 ./tools/gemm_lab/bin/gemm_lab full > gpurun_out/r4a_lab.log 2>&1 || { tail -30 gpurun_out/r4a_lab.log; exit 1; }
+grep -E "==|w4_|v4_256w |v4_320pwn |MISMATCH" gpurun_out/r4a_lab.log | grep -v max_abs | head -120
 grep -c MISMATCH gpurun_out/r4a_lab.log
 timeout -k 10 300 ./tools/gemm_lab/bin/attn_lab > gpurun_out/r4a_attn_lab.log 2>&1 || { tail -30 gpurun_out/r4a_attn_lab.log; exit 1; }
 grep -v stamps gpurun_out/r4a_attn_lab.log
@@ -21,3 +21,6 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 tail -1 gpurun_out/r4a_smoke.log | cut -c1-300
 timeout -k 10 400 python -u bench.py --gpus 1 --steps 8 --warmup 2 > gpurun_out/r4a_bench_sd21.log 2>&1 || exit $?
 tail -1 gpurun_out/r4a_bench_sd21.log | cut -c1-400
+# A/B: GroupNorm finalize fused into the stats launch (ticket) at batch 1 latency
+SHAI_GN_FUSED_FINALIZE=1 timeout -k 10 400 python -u bench.py --gpus 1 --steps 1 --warmup 1 --latency-runs 5 > gpurun_out/r4a_bench_gnfused.log 2>&1 || exit $?
+echo "gn fused finalize: $(tail -1 gpurun_out/r4a_bench_gnfused.log | grep -o '"p50_latency_ms_bs1": [0-9.]*')"
