@@ -322,16 +322,17 @@ __global__ void __launch_bounds__(512, 1) attn512_kernel(const AttnArgs p) {
       qf[ds] = __builtin_bit_cast(f3bf16x8, pack8(f));
     }
   }
-  // per-lane LDS byte offsets: K fragment (row fq, chunk (4 ds + g) ^ fq) = koff[ds & 3] + 256 (ds >> 2);
-  // V^T fragment of d-block db (rows 4g + q (+16), chunk (2 db + (p >> 1)) ^ vswz) = voff[db & 3] + 128 (db >> 2)
+  // per-lane LDS byte offsets: K fragment (row fq, chunk (4 ds + g) ^ fq; the XOR reaches chunk bits 0-3, i.e.
+  // ds & 3) = koff[ds & 3] + 256 (ds >> 2); V^T fragment of d-block db (rows 4g + q (+16), chunk
+  // (2 db + (p >> 1)) ^ vswz; vswz reaches chunk bits 1-3, i.e. db & 7) = voff[db & 7] + 256 (db >> 3)
   const int fh = fq >> 2, tq = fq >> 2, tp = lane & 3;
-  int koff[4], voff[4];
+  int koff[4];
 #pragma unroll
-  for (int bb = 0; bb < 4; ++bb) {
-    koff[bb] = fq * A5_D * 2 + ((((bb ^ fh) << 2) | ((g ^ fq) & 3)) << 4);
-    const int r = 4 * g + tq;
-    voff[bb] = r * A5_D * 2 + ((2 * bb + (tp >> 1)) ^ a5_vswz(r)) * 16 + (tp & 1) * 8;
-  }
+  for (int bb = 0; bb < 4; ++bb) koff[bb] = fq * A5_D * 2 + ((((bb ^ fh) << 2) | ((g ^ fq) & 3)) << 4);
+  // V: chunk position (2 db + (p >> 1)) ^ vswz = 2 (db & 7) ^ vx + 16 (db >> 3), vx = (p >> 1) ^ vswz (one XOR
+  // per read instead of 8 more offset registers)
+  const int vrow = (4 * g + tq) * A5_D * 2 + (tp & 1) * 8;
+  const int vx = (tp >> 1) ^ a5_vswz(4 * g + tq);
 
   float4_ o[32];
   float m_run = -INFINITY, l_lane = 0.f;
@@ -344,6 +345,8 @@ __global__ void __launch_bounds__(512, 1) attn512_kernel(const AttnArgs p) {
     if (t + 1 < nt) dma(cur ^ 1, t + 1);
     const char* ks = reinterpret_cast<const char*>(smem + cur * A5_STAGE);
     const char* vs = ks + A5_KT * A5_D * 2;
+    int vxl = vx, vrl = vrow;   // opaque per tile: the 32 V^T read addresses are rebuilt, not hoisted into registers
+    asm volatile("" : "+v"(vxl), "+v"(vrl));
     float4_ s[2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
@@ -387,7 +390,7 @@ __global__ void __launch_bounds__(512, 1) attn512_kernel(const AttnArgs p) {
       }
 #pragma unroll
     for (int db = 0; db < 32; ++db) {
-      const char* a0 = vs + voff[db & 3] + 128 * (db >> 2);
+      const char* a0 = vs + vrl + (((2 * (db & 7)) ^ vxl) << 4) + 256 * (db >> 3);
       const f3s4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) f3s4v*)(a0));
       const f3s4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
           (__attribute__((address_space(3))) f3s4v*)(a0 + 16 * A5_D * 2));

@@ -524,7 +524,8 @@ int gemm2_num_cfgs() { return kW4Cfg + 2; }
 bool gemm2_cfg_splittable(int cfg) { return cfg != kW4Cfg && cfg != kW4Cfg + 1; }
 
 bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
-  if (cfg == kW4Cfg || cfg == kW4Cfg + 1) return gemm_w4_supported(a);
+  if (cfg == kW4Cfg) return gemm_w4_supported(a);
+  if (cfg == kW4Cfg + 1) return false;  // 192 x 320 four-wave tile: lab only (gemm_w4.hip launch_gemm_w4)
   if (cfg >= kV4Cfg) return cfg < kV4Cfg + 4 && gemm4_supported(a);
   if (cfg >= kNumCfgs) return gemm3_supported(a);
   if (a.in_scale != nullptr) return false;

@@ -3,8 +3,8 @@
 //
 //   C[b, m, n] = gate * act(alpha * sum_k A[b, m, k] * W[b, n, k] + bias[n] + bias2d[m / rpb, n]) + res_alpha * R
 //
-// Configs: 256 x 256 tiles (8 x 8 blocks per wave: LLM / Flux / ViT widths, every multiple of 256) and
-// 192 x 320 tiles (6 x 10 blocks per wave: the SD2.1 channel widths 320 / 640 / 1280 / 960).
+// Configs: 256 x 256 tiles (8 x 8 blocks per wave: LLM / Flux / ViT widths, every multiple of 256); a 192 x 320
+// lab config (6 x 10 blocks per wave) for the SD2.1 channel widths lost to v4 (see launch_gemm_w4).
 //
 // Why: the v4 kernel (gemm_8ph.hip) pairs two waves per SIMD that each own a 128 x 64 (or 128 x 80) slice;
 // per 64-deep K-tile a CU then reads 8 x (128 + 80) x 128 B = 213 KB of fragments out of LDS and re-syncs
@@ -449,10 +449,19 @@ static void w4_dispatch(const GemmArgs& a, hipStream_t s) {
   }
 }
 
-// bn = 256: 256 x 256 tiles; bn = 320: 192 x 320 tiles
+// bn = 256: 256 x 256 tiles; bn = 320 (lab builds only): 192 x 320 tiles.  The 192 x 320 config lost to v4's
+// persistent 256 x 320 kernel on every SD2.1 shape in the round-4 lab (unet64_320 conv 949 vs 1135 TF/s: 5.3
+// tile rounds per CU instead of 4, and ~10 % slower per tile), and a 256 x 320 four-wave tile (8 x 10 blocks,
+// 320 accumulators) spills 32-85 VGPRs, so production keeps v4 for the 320-wide problems.
 void launch_gemm_w4(const GemmArgs& a, int bn, hipStream_t s) {
-  if (bn == 320) w4_dispatch<6, 10>(a, s);
-  else w4_dispatch<8, 8>(a, s);
+#ifdef SHAI_GEMM_LAB
+  if (bn == 320) {
+    w4_dispatch<6, 10>(a, s);
+    return;
+  }
+#endif
+  (void)bn;
+  w4_dispatch<8, 8>(a, s);
 }
 
 }  // namespace shai

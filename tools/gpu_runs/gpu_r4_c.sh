@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 4: long-context lines at the reference's configured length (max_model_len 128000,
+# cova/mllama-32-11b-vllm-trn1-config.yaml:12-16): Llama-3.1-8B (128k RoPE), a 64k and a ~128k prompt prefilled in
+# 8k packed chunks beside 16 decoding sequences, then decoded (TTFT, TPOT).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+( while sleep 60; do echo "long-context running $(date +%T)"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+for P in 65536 127744; do
+  timeout -k 10 540 python -u -m shai_amd.bench.long_context --model llama31_8b --prompt-len $P --chunk 8192 \
+    --background 16 --gen 128 > gpurun_out/r4c_long_$P.log 2>&1 || { tail -20 gpurun_out/r4c_long_$P.log; exit 1; }
+  tail -1 gpurun_out/r4c_long_$P.log
+done
