@@ -49,7 +49,7 @@ std::mutex g_tune_mu;
 std::unordered_map<std::string, Choice> g_tuned;
 
 bool lib_supported(const shai::GemmArgs& g) {
-  return g.conv == 0 && g.batch <= 1 && !g.glu && g.act == 0 && !g.bias2d && !g.gate && !g.rms && !g.w_scale &&
+  return g.conv == 0 && !g.row_mr && g.batch <= 1 && !g.glu && g.act == 0 && !g.bias2d && !g.gate && !g.rms && !g.w_scale &&
          !g.A2 && !g.in_scale && g.alpha == 1.f && !(g.bias && g.residual) &&
          (!g.residual || (g.res_alpha == 1.f && g.residual == g.C && g.ldr == g.ldc)) &&
          g.lda >= g.K && g.ldw >= g.K && g.ldc >= g.N;
@@ -136,7 +136,7 @@ bool lib_enabled() {  // SHAI_GEMM_LIB=0 keeps every GEMM on the hand-written ke
 
 int max_splits_for(const shai::GemmArgs& g) {
   const int batch = g.batch > 0 ? g.batch : 1;
-  if (batch != 1) return 1;
+  if (batch != 1 || g.row_mr != nullptr) return 1;  // folded LayerNorm: applied by the unsplit v4 epilogue only
   const long kt = (g.K + 63) / 64;
   int s = 1;
   while (s < 16 && kt / (s * 2) >= 4) s *= 2;
@@ -355,18 +355,63 @@ void run_skinny(const shai::GemmArgs& g, const Tensor& like) {
   launch_choice(g, like, c);
 }
 
-void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_bytes, long a2_bytes) {
+// Statistics of the GEMM output wanted by the next norm: GroupNorm col partials [M / 128, N, 2] and / or LayerNorm
+// row moments [M, 2] = (mean, rstd).  The v4 wide epilogue writes them when the final choice runs it on every tile
+// (gemm4_stats_ok); otherwise a pass over the output produces the same statistics.
+struct OutStats {
+  float* gn_part = nullptr;
+  float* ln_mr = nullptr;
+  float ln_eps = 1e-5f;
+  bool any() const { return gn_part != nullptr || ln_mr != nullptr; }
+};
+
+void launch_final(shai::GemmArgs g, const Tensor& like, const Choice& c, const OutStats* st) {
+  if (st == nullptr || !st->any()) {
+    launch_choice(g, like, c);
+    return;
+  }
+  int bm = 0, bn = 0;
+  bool v4 = c.cfg >= 0 && c.cfg < shai::gemm2_num_cfgs() && c.splits <= 1 && shai::gemm2_cfg_supported(g, c.cfg);
+  if (v4) {
+    shai::gemm2_cfg_info(c.cfg, &bm, &bn);
+    v4 = (bm == 8 || bm == 9) && bn < 0 && shai::gemm4_stats_ok(g, -bn);
+  }
+  Tensor rp;
+  if (v4) {
+    g.col_part = st->gn_part;
+    if (st->ln_mr) {
+      g.row_part_slots = 4 * (g.N / -bn);
+      rp = at::empty({(long)g.M * g.row_part_slots * 2}, like.options().dtype(at::kFloat));
+      g.row_part = rp.data_ptr<float>();
+    }
+  }
+  launch_choice(g, like, c);
+  if (st->gn_part && g.col_part == nullptr) shai::launch_col_partials(g.C, g.M, g.N, g.ldc, st->gn_part, stream());
+  if (st->ln_mr) {
+    if (g.row_part) shai::launch_row_moments_from_partials(g.row_part, g.M, g.row_part_slots, g.N, st->ln_eps,
+                                                           st->ln_mr, stream());
+    else shai::launch_row_moments(g.C, g.M, g.N, g.ldc, st->ln_eps, st->ln_mr, stream());
+  }
+}
+
+void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_bytes, long a2_bytes,
+              const OutStats* st = nullptr) {
   static const int forced = [] {  // tests / tools: pin one config for every supported GEMM/conv
     const char* e = getenv("SHAI_GEMM_FORCE");
     return e ? atoi(e) : -1;
   }();
   if (!use_v2(g, a_bytes, w_bytes, a2_bytes)) {
     SHAI_CHECK(g.gate == nullptr, "gated GEMM epilogue needs the v2 kernel (operands < 2 GiB, SHAI_GEMM_V1 unset)");
+    SHAI_CHECK(g.row_mr == nullptr, "folded LayerNorm needs the v4 kernel (operands < 2 GiB, SHAI_GEMM_V1 unset)");
     shai::launch_gemm(g, stream());
+    if (st && st->any()) {  // v1 writes no statistics
+      if (st->gn_part) shai::launch_col_partials(g.C, g.M, g.N, g.ldc, st->gn_part, stream());
+      if (st->ln_mr) shai::launch_row_moments(g.C, g.M, g.N, g.ldc, st->ln_eps, st->ln_mr, stream());
+    }
     return;
   }
   if (forced >= 0 && forced < shai::gemm2_num_cfgs() && shai::gemm2_cfg_supported(g, forced)) {
-    launch_choice(g, like, Choice{forced, 1});
+    launch_final(g, like, Choice{forced, 1}, st);
     return;
   }
   const std::string key = gemm_key(g);
@@ -387,7 +432,8 @@ void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_
       }
     }
   }
-  launch_choice(g, like, c);
+  if (g.row_mr != nullptr) c.splits = 1;  // a cached choice of the plain problem with this key may be split
+  launch_final(g, like, c, st);
 }
 
 std::vector<std::string> gemm_tuning_table() {
@@ -586,6 +632,47 @@ void groupnorm_stats(const Tensor& x, const optional<Tensor>& x2, const optional
   shai::launch_groupnorm_stats(a, stream());
 }
 
+// GroupNorm (scale, shift) from the col partials a GEMM / conv epilogue wrote ([Nimg * HW / 128, C, 2] per source)
+void groupnorm_from_partials(const Tensor& part1, const optional<Tensor>& part2, int64_t C1, int64_t C2,
+                             int64_t Nimg, int64_t HW, const optional<Tensor>& gamma, const optional<Tensor>& beta,
+                             const Tensor& scale, const Tensor& shift, int64_t G, double eps) {
+  check_f32(part1, "part1");
+  check_f32(scale, "scale");
+  check_f32(shift, "shift");
+  const long C = C1 + C2;
+  SHAI_CHECK(HW % 128 == 0 && C % G == 0 && G <= 128 && C <= 8192, "groupnorm_from_partials: bad HW / C / G");
+  SHAI_CHECK(part1.numel() == Nimg * HW / 128 * C1 * 2, "part1 must be [Nimg * HW / 128, C1, 2]");
+  if (part2.has_value()) {
+    check_f32(*part2, "part2");
+    SHAI_CHECK(part2->numel() == Nimg * HW / 128 * C2 * 2, "part2 must be [Nimg * HW / 128, C2, 2]");
+  } else {
+    SHAI_CHECK(C2 == 0, "C2 > 0 needs part2");
+  }
+  SHAI_CHECK(scale.numel() >= Nimg * C && shift.numel() >= Nimg * C, "scale/shift too small");
+  shai::launch_gn_from_partials(part1.data_ptr<float>(), C1, part2 ? part2->data_ptr<float>() : nullptr, C2, Nimg,
+                                HW, G, optr(gamma), optr(beta), eps, scale.data_ptr<float>(), shift.data_ptr<float>(),
+                                stream());
+}
+
+// the statistics passes on their own (tests, and producers outside the GEMM kernels)
+void col_partials(const Tensor& x, const Tensor& part) {
+  check_rows(x, "x");
+  check_f32(part, "part");
+  SHAI_CHECK(x.dim() == 2, "col_partials: x must be 2D [M, N]");
+  const long M = x.size(0);
+  const int N = x.size(1);
+  SHAI_CHECK(M % 128 == 0 && N % 8 == 0 && N <= 2048 && part.numel() == M / 128 * N * 2,
+             "col_partials: M % 128 == 0, N % 8 == 0, N <= 2048, part [M / 128, N, 2]");
+  shai::launch_col_partials(cptr(x), M, N, x.stride(0), part.data_ptr<float>(), stream());
+}
+
+void row_moments(const Tensor& x, const Tensor& mr, double eps) {
+  check_rows(x, "x");
+  check_f32(mr, "mr");
+  SHAI_CHECK(x.dim() == 2 && x.size(1) % 8 == 0 && mr.numel() == 2 * x.size(0), "row_moments: x [M, N % 8], mr [M, 2]");
+  shai::launch_row_moments(cptr(x), x.size(0), x.size(1), x.stride(0), eps, mr.data_ptr<float>(), stream());
+}
+
 void groupnorm_apply(const Tensor& x, const optional<Tensor>& x2, const Tensor& scale, const Tensor& shift,
                      const Tensor& out, bool silu) {
   check_bf16(out, "out");
@@ -609,11 +696,42 @@ void groupnorm_apply(const Tensor& x, const optional<Tensor>& x2, const Tensor& 
 }
 
 // ---------------------------------------------------------------- GEMM
+// Norm hand-off tensors of a GEMM / conv: ln_mr [M, 2] + ln_s [N] (LayerNorm of A folded in), gn_part
+// [M / 128, N, 2] (GroupNorm partials of the output), ln_stats [M, 2] (LayerNorm moments of the output).
+void attach_norm_io(shai::GemmArgs& g, const optional<Tensor>& ln_mr, const optional<Tensor>& ln_s,
+                    const optional<Tensor>& gn_part, const optional<Tensor>& ln_stats, double ln_eps, OutStats* st) {
+  if (ln_mr.has_value()) {
+    SHAI_CHECK(ln_s.has_value(), "ln_mr needs ln_s");
+    check_f32(*ln_mr, "ln_mr");
+    check_f32(*ln_s, "ln_s");
+    SHAI_CHECK(ln_mr->numel() == 2L * g.M && ln_s->numel() == g.N, "ln_mr must be [M, 2] and ln_s [N]");
+    SHAI_CHECK(reinterpret_cast<uintptr_t>(ln_s->data_ptr()) % 16 == 0, "ln_s must be 16-byte aligned");
+    g.row_mr = ln_mr->data_ptr<float>();
+    g.col_s = ln_s->data_ptr<float>();
+  }
+  const int n_out = g.glu ? g.N / 2 : g.N;
+  if (gn_part.has_value()) {
+    check_f32(*gn_part, "gn_part");
+    SHAI_CHECK(g.M % 128 == 0 && n_out % 8 == 0 && n_out <= 2048 && gn_part->numel() == (long)g.M / 128 * n_out * 2,
+               "gn_part must be [M / 128, N, 2] with M % 128 == 0, N % 8 == 0, N <= 2048");
+    SHAI_CHECK(reinterpret_cast<uintptr_t>(gn_part->data_ptr()) % 16 == 0, "gn_part must be 16-byte aligned");
+    st->gn_part = gn_part->data_ptr<float>();
+  }
+  if (ln_stats.has_value()) {
+    check_f32(*ln_stats, "ln_stats");
+    SHAI_CHECK(ln_stats->numel() == 2L * g.M && n_out % 8 == 0, "ln_stats must be [M, 2] (N % 8 == 0)");
+    st->ln_mr = ln_stats->data_ptr<float>();
+    st->ln_eps = (float)ln_eps;
+  }
+}
+
 // a: [M, K] or [B, M, K]; w: [N, K] or [B, N, K]; c: [M, N'] or [B, M, N'] (N' = N or N/2 for glu)
 void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tensor>& bias,
           const optional<Tensor>& bias2d, int64_t rows_per_bias2d, const optional<Tensor>& residual, double alpha,
           double res_alpha, int64_t act, bool glu, const optional<Tensor>& gate, int64_t rows_per_gate,
-          int64_t force_cfg, double rms_eps, const optional<Tensor>& w_scale) {
+          int64_t force_cfg, double rms_eps, const optional<Tensor>& w_scale, const optional<Tensor>& ln_mr,
+          const optional<Tensor>& ln_s, const optional<Tensor>& gn_part, const optional<Tensor>& ln_stats,
+          double ln_eps) {
   check_rows(a, "a");
   if (w_scale.has_value()) {  // fp8 (e4m3) weights + fp32 per-row scale: skinny (decode-shaped) kernel only
     SHAI_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat8_e4m3fn && w.dim() == 2 && w.stride(1) == 1 &&
@@ -735,6 +853,20 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
     run_gemm(g, xn, (long)g.M * g.K * 2, (long)g.N * g.ldw * 2, 0);
     return;
   }
+  if (ln_mr.has_value() || gn_part.has_value() || ln_stats.has_value()) {
+    SHAI_CHECK(!batched && g.gate == nullptr && (force_cfg < 0 || force_cfg < shai::gemm2_num_cfgs()),
+               "folded LayerNorm / output statistics: 2D, ungated GEMMs on the tile kernels");
+    SHAI_CHECK(!glu || (!gn_part.has_value() && !ln_stats.has_value()), "output statistics of a GLU GEMM");
+    OutStats st;
+    attach_norm_io(g, ln_mr, ln_s, gn_part, ln_stats, ln_eps, &st);
+    if (force_cfg >= 0) {
+      SHAI_CHECK(shai::gemm2_cfg_supported(g, force_cfg), "bad force_cfg");
+      launch_final(g, a, Choice{(int)force_cfg, 1}, &st);
+    } else {
+      run_gemm(g, a, a_bytes, (long)g.N * g.ldw * 2, 0, &st);
+    }
+    return;
+  }
   if (force_cfg == kLibCfg) {  // tests: pin the hipBLASLt path
     SHAI_CHECK(lib_supported(g), "library GEMM path does not support this problem's epilogue");
     launch_lib(g, a);
@@ -759,7 +891,9 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
 void conv2d(const Tensor& x, const optional<Tensor>& x2, const Tensor& w, const Tensor& out,
             const optional<Tensor>& bias, const optional<Tensor>& bias2d, const optional<Tensor>& residual,
             const optional<Tensor>& in_scale, const optional<Tensor>& in_shift, int64_t in_act, int64_t kh,
-            int64_t kw, int64_t stride, int64_t pad, bool upsample, int64_t act, double res_alpha) {
+            int64_t kw, int64_t stride, int64_t pad, bool upsample, int64_t act, double res_alpha,
+            const optional<Tensor>& ln_mr, const optional<Tensor>& ln_s, const optional<Tensor>& gn_part,
+            const optional<Tensor>& ln_stats, double ln_eps) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_bf16(out, "out");
@@ -835,8 +969,10 @@ void conv2d(const Tensor& x, const optional<Tensor>& x2, const Tensor& w, const 
     g.in_shift = in_shift->data_ptr<float>();
     g.in_act = in_act;
   }
+  OutStats st;
+  attach_norm_io(g, ln_mr, ln_s, gn_part, ln_stats, ln_eps, &st);
   run_gemm(g, x, xcat.defined() ? xcat.numel() * 2 : x.numel() * 2, w.numel() * 2,
-           (x2 && !xcat.defined()) ? x2->numel() * 2 : 0);
+           (x2 && !xcat.defined()) ? x2->numel() * 2 : 0, &st);
 }
 
 // ---------------------------------------------------------------- attention
@@ -1375,11 +1511,14 @@ TORCH_LIBRARY(shai, m) {
   m.def("layernorm(Tensor x, Tensor? w, Tensor? b, Tensor(a!) out, Tensor? residual, Tensor(b!)? residual_out, float eps) -> ()");
   m.def("groupnorm_stats(Tensor x, Tensor? x2, Tensor? gamma, Tensor? beta, Tensor(a!) partials, Tensor(b!) scale, Tensor(c!) shift, Tensor(d!)? counters, int G, float eps) -> ()");
   m.def("groupnorm_apply(Tensor x, Tensor? x2, Tensor scale, Tensor shift, Tensor(a!) out, bool silu) -> ()");
-  m.def("gemm(Tensor a, Tensor w, Tensor(a!) c, Tensor? bias, Tensor? bias2d, int rows_per_bias2d, Tensor? residual, float alpha, float res_alpha, int act, bool glu, Tensor? gate=None, int rows_per_gate=1, int force_cfg=-1, float rms_eps=-1.0, Tensor? w_scale=None) -> ()");
+  m.def("groupnorm_from_partials(Tensor part1, Tensor? part2, int C1, int C2, int Nimg, int HW, Tensor? gamma, Tensor? beta, Tensor(a!) scale, Tensor(b!) shift, int G, float eps) -> ()");
+  m.def("col_partials(Tensor x, Tensor(a!) part) -> ()");
+  m.def("row_moments(Tensor x, Tensor(a!) mr, float eps) -> ()");
+  m.def("gemm(Tensor a, Tensor w, Tensor(a!) c, Tensor? bias, Tensor? bias2d, int rows_per_bias2d, Tensor? residual, float alpha, float res_alpha, int act, bool glu, Tensor? gate=None, int rows_per_gate=1, int force_cfg=-1, float rms_eps=-1.0, Tensor? w_scale=None, Tensor? ln_mr=None, Tensor? ln_s=None, Tensor(b!)? gn_part=None, Tensor(c!)? ln_stats=None, float ln_eps=1e-5) -> ()");
   m.def("dequant_fp8(Tensor w8, Tensor scale, Tensor(a!) out) -> ()");
   m.def("layernorm_mod(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, int rows_per_mod, float eps) -> ()");
   m.def("qk_norm_rope(Tensor(a!) x, Tensor? q_w, Tensor? k_w, Tensor? cos, Tensor? sin, int H, int D, int S, float eps) -> ()");
-  m.def("conv2d(Tensor x, Tensor? x2, Tensor w, Tensor(a!) out, Tensor? bias, Tensor? bias2d, Tensor? residual, Tensor? in_scale, Tensor? in_shift, int in_act, int kh, int kw, int stride, int pad, bool upsample, int act, float res_alpha) -> ()");
+  m.def("conv2d(Tensor x, Tensor? x2, Tensor w, Tensor(a!) out, Tensor? bias, Tensor? bias2d, Tensor? residual, Tensor? in_scale, Tensor? in_shift, int in_act, int kh, int kw, int stride, int pad, bool upsample, int act, float res_alpha, Tensor? ln_mr=None, Tensor? ln_s=None, Tensor(b!)? gn_part=None, Tensor(c!)? ln_stats=None, float ln_eps=1e-5) -> ()");
   m.def("flash_attn(Tensor q, Tensor k, Tensor v, Tensor(a!) o, float scale, bool causal, int causal_offset, Tensor? kv_lens, Tensor? q_lens, Tensor? bias, Tensor? block_table) -> ()");
   m.def("paged_attn_varlen(Tensor q, Tensor k_cache, Tensor v_cache, Tensor(a!) o, Tensor block_table, Tensor kv_lens, Tensor q_lens, Tensor q_start, int max_q, float scale, bool causal) -> ()");
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor(a!) o, Tensor block_table, Tensor ctx_lens, Tensor(b!) ws, int num_splits, float scale) -> ()");
@@ -1408,6 +1547,9 @@ TORCH_LIBRARY_IMPL(shai, CUDA, m) {
   m.impl("rmsnorm", &rmsnorm);
   m.impl("layernorm", &layernorm);
   m.impl("groupnorm_stats", &groupnorm_stats);
+  m.impl("groupnorm_from_partials", &groupnorm_from_partials);
+  m.impl("col_partials", &col_partials);
+  m.impl("row_moments", &row_moments);
   m.impl("groupnorm_apply", &groupnorm_apply);
   m.impl("gemm", &gemm);
   m.impl("dequant_fp8", &dequant_fp8);

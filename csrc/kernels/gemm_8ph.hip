@@ -68,6 +68,7 @@ __device__ __forceinline__ void g4_glds(__amdgpu_buffer_rsrc_t r, bf16_t* lds, u
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (g4_lds_void*)lds, 16, off, 0, 0, 0);
 }
 
+
 // Schedule variants (lab A/B; 0 = production):
 //   bit 0: no stagger (both wave groups in lockstep)
 //   bit 1: static priority (waves 4-7 at prio 1 for the whole loop) instead of per-segment setprio
@@ -401,7 +402,39 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
       } else {
         bf16_t* __restrict__ C = p.C + (long)b * p.batch_c;
         const bf16_t* __restrict__ R = p.residual ? p.residual + (long)b * p.batch_r : nullptr;
-        const bool fast = m0 + G4_BM <= p.M && n0 + BN <= p.N && p.bias2d == nullptr && p.gate == nullptr &&
+        if (p.row_mr != nullptr) {
+          // LayerNorm folded in (host: batch 1, unsplit): acc <- rstd[m] * (acc - mean[m] * s[n]), i.e. the GEMM of
+          // the normalised rows with the gain-folded W; the folded shift is in the bias
+          float mean[8], rstd[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int m = min(m0 + wm * 128 + i * 16 + fr, p.M - 1);
+            const float2 v = *reinterpret_cast<const float2*>(p.row_mr + 2 * (long)m);
+            mean[i] = v.x;
+            rstd[i] = v.y;
+          }
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const int n = n0 + wn * WC + g4_col<BN, WIDE>(j, fq);
+            float s[4];
+            if (n + 3 < p.N) {
+              const float4_ sv = *reinterpret_cast<const float4_*>(p.col_s + n);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) s[e] = sv[e];
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) s[e] = n + e < p.N ? p.col_s[n + e] : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc[i][j][e] = rstd[i] * fmaf(-mean[i], s[e], acc[i][j][e]);
+          }
+        }
+        // per-image bias (time embedding) in the wide path: each wave's 128 rows lie inside one image
+        const bool b2ok = p.bias2d == nullptr ||
+                          (WIDE && (p.rows_per_bias2d & 127) == 0 && (p.N & 7) == 0 && ((uintptr_t)p.bias2d & 15) == 0);
+        const bool fast = m0 + G4_BM <= p.M && n0 + BN <= p.N && b2ok && p.gate == nullptr &&
                           (p.ldc & 3) == 0 && (R == nullptr || (p.ldr & 3) == 0);
         if constexpr (WIDE) {
           // 16-byte C / residual / bias accesses: 8-element aligned rows and bases
@@ -426,7 +459,32 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
               bt[0] = bf2f(bb[0] & 0xffff); bt[1] = bf2f(bb[0] >> 16);
               bt[2] = bf2f(bb[1] & 0xffff); bt[3] = bf2f(bb[1] >> 16);
             }
+            if (p.bias2d != nullptr) {  // b2ok: the wave's 128 rows share one bias2d row
+              const bf16_t* b2 = p.bias2d + (long)((m0 + wm * 128) / p.rows_per_bias2d) * p.N;
+#pragma unroll
+              for (int q = 0; q < NP; ++q) {
+                float t8[8];
+                unpack8(*reinterpret_cast<const uint4_*>(b2 + n0 + wn * WC + q * 32 + 8 * fq), t8);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) bq[q][e] += t8[e];
+              }
+              if (TAIL) {
+                const uint2_ bb = *reinterpret_cast<const uint2_*>(b2 + nt4);
+                bt[0] += bf2f(bb[0] & 0xffff); bt[1] += bf2f(bb[0] >> 16);
+                bt[2] += bf2f(bb[1] & 0xffff); bt[3] += bf2f(bb[1] >> 16);
+              }
+            }
+            // statistics of the stored output for the next norm (plain epilogue only; host: gemm4_stats_ok).
+            // Column (GroupNorm) statistics: the accumulator registers leave no room for per-column sums (the
+            // kernel sits at 240-250 VGPRs), so each IG-row-block group of stored values is also written to this
+            // wave's slice of LDS buffer 1 (free during the epilogue: the persistent prefetch targets buffer 0, and
+            // the next tile restages buffer 1 only after the loop-top barrier) and summed down the rows by lanes
+            // owning a column pair: 4 registers per lane.
             constexpr int IG = NJ == 4 ? 4 : 2;
+            float* __restrict__ colp = GLU ? nullptr : p.col_part;
+            float* __restrict__ rowp = GLU ? nullptr : p.row_part;
+            bf16_t* cst = g4_smem + G4_STAGE + wid * (IG * 16 * WC);  // [IG * 16][WC] bf16
+            float c0 = 0.f, c1 = 0.f, d0 = 0.f, d1 = 0.f;              // column pair (2 lane, 2 lane + 1)
 #pragma unroll
             for (int i0 = 0; i0 < 8; i0 += IG) {
               if constexpr (!GLU) {
@@ -445,6 +503,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
                 for (int ii = 0; ii < IG; ++ii) {
                   const int i = i0 + ii;
                   bf16_t* crow = C + (long)(m0 + wm * 128 + i * 16 + fr) * p.ldc + n0 + wn * WC;
+                  float rs = 0.f, rq = 0.f;  // row statistics of this lane's columns
 #pragma unroll
                   for (int q = 0; q < NP; ++q) {
                     float v[8];
@@ -459,7 +518,16 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
 #pragma unroll
                       for (int e = 0; e < 8; ++e) v[e] += r8[e] * p.res_alpha;
                     }
-                    *reinterpret_cast<uint4_*>(crow + q * 32 + 8 * fq) = pack8(v);
+                    const uint4_ pv = pack8(v);
+                    *reinterpret_cast<uint4_*>(crow + q * 32 + 8 * fq) = pv;
+                    if (colp) *reinterpret_cast<uint4_*>(cst + (ii * 16 + fr) * WC + q * 32 + 8 * fq) = pv;
+                    if (rowp) {
+#pragma unroll
+                      for (int e = 0; e < 8; ++e) {
+                        rs += v[e];
+                        rq = fmaf(v[e], v[e], rq);
+                      }
+                    }
                   }
                   if constexpr (TAIL) {
                     float v[4];
@@ -473,7 +541,41 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
                     o[0] = pack2(v[0], v[1]);
                     o[1] = pack2(v[2], v[3]);
                     *reinterpret_cast<uint2_*>(crow + 2 * NP * 16 + 4 * fq) = o;
+                    if (colp) *reinterpret_cast<uint2_*>(cst + (ii * 16 + fr) * WC + 2 * NP * 16 + 4 * fq) = o;
+                    if (rowp) {
+#pragma unroll
+                      for (int e = 0; e < 4; ++e) {
+                        rs += v[e];
+                        rq = fmaf(v[e], v[e], rq);
+                      }
+                    }
                   }
+                  if (rowp) {  // the 4 fq lanes of a row hold its 4 column quarters of this wave's slice
+                    rs += __shfl_xor(rs, 16, 64);
+                    rq += __shfl_xor(rq, 16, 64);
+                    rs += __shfl_xor(rs, 32, 64);
+                    rq += __shfl_xor(rq, 32, 64);
+                    if (fq == 0) {
+                      const long m = m0 + wm * 128 + i * 16 + fr;
+                      const int slot = (n0 / BN) * 4 + wn;
+                      *reinterpret_cast<float2*>(rowp + (m * p.row_part_slots + slot) * 2) = make_float2(rs, rq);
+                    }
+                  }
+                }
+                if (colp) {  // one wave's own LDS slice: its ds ops execute in issue order, no barrier needed
+                  asm volatile("" ::: "memory");
+                  if (lane < WC / 2) {
+#pragma unroll 8
+                    for (int r = 0; r < IG * 16; ++r) {
+                      const uint32_t u = *reinterpret_cast<const uint32_t*>(cst + r * WC + 2 * lane);
+                      const float f0 = bf2f(u & 0xffff), f1 = bf2f(u >> 16);
+                      c0 += f0;
+                      c1 += f1;
+                      d0 = fmaf(f0, f0, d0);
+                      d1 = fmaf(f1, f1, d1);
+                    }
+                  }
+                  asm volatile("" ::: "memory");
                 }
               } else {
                 // GLU: (value, gate) column pairs -> the lane's 8 columns give 4 consecutive outputs
@@ -522,6 +624,9 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
                 }
               }
             }
+            if (colp && lane < WC / 2)  // column totals over the wave's 128 rows -> partial block (m0 + 128 wm) / 128
+              *reinterpret_cast<float4_*>(colp + ((long)((m0 + wm * 128) >> 7) * p.N + n0 + wn * WC + 2 * lane) * 2) =
+                  float4_{c0, d0, c1, d1};
             wide_done = true;
             return;
           }
@@ -636,6 +741,16 @@ bool gemm4_supported(const GemmArgs& a) {
     if (a.Cin % 64 != 0) return false;
     if (a.A2 != nullptr && a.Cin1 % 64 != 0) return false;
   }
+  return true;
+}
+
+bool gemm4_stats_ok(const GemmArgs& a, int bn) {
+  const auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!gemm4_supported(a) || a.glu || a.gate != nullptr || (a.batch > 1)) return false;
+  if (a.M % G4_BM != 0 || a.N % bn != 0 || a.ldc % 8 != 0 || !al16(a.C)) return false;
+  if (a.residual != nullptr && (a.ldr % 8 != 0 || !al16(a.residual))) return false;
+  if (a.bias != nullptr && !al16(a.bias)) return false;
+  if (a.bias2d != nullptr && (a.rows_per_bias2d % 128 != 0 || a.N % 8 != 0 || !al16(a.bias2d))) return false;
   return true;
 }
 

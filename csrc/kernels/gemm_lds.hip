@@ -524,6 +524,8 @@ int gemm2_num_cfgs() { return kW4Cfg + 2; }
 bool gemm2_cfg_splittable(int cfg) { return cfg != kW4Cfg && cfg != kW4Cfg + 1; }
 
 bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
+  // folded LayerNorm (row_mr): only the v4 kernel's epilogue applies it, and only unsplit, batch 1
+  if (a.row_mr != nullptr) return cfg >= kV4Cfg && cfg < kV4Cfg + 4 && a.batch <= 1 && gemm4_supported(a);
   if (cfg == kW4Cfg) return gemm_w4_supported(a);
   if (cfg == kW4Cfg + 1) return false;  // 192 x 320 four-wave tile: lab only (gemm_w4.hip launch_gemm_w4)
   if (cfg >= kV4Cfg) return cfg < kV4Cfg + 4 && gemm4_supported(a);

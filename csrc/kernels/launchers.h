@@ -44,6 +44,17 @@ struct GroupNormArgs {
 int gn_num_blocks(int N, int HW, int C);
 void launch_groupnorm_stats(const GroupNormArgs& a, hipStream_t s);
 void launch_groupnorm_apply(const GroupNormArgs& a, hipStream_t s);
+// Norm statistics produced by a GEMM epilogue (GemmArgs::col_part / row_part) and their fallback passes:
+//   col partials [M / 128, N, 2] (sum, sum of squares per 128-row block and column) of x [M, N] (row stride ldx)
+void launch_col_partials(const bf16_t* x, long M, int N, long ldx, float* part, hipStream_t s);
+//   GroupNorm (scale, shift) [Nimg, C1 + C2] from the col partials of x (C1 channels) and optional x2 (C2)
+void launch_gn_from_partials(const float* part1, int C1, const float* part2, int C2, int Nimg, int HW, int G,
+                             const bf16_t* gamma, const bf16_t* beta, float eps, float* scale, float* shift,
+                             hipStream_t s);
+//   LayerNorm row moments mr [M, 2] = (mean, rstd) from row partials [M, slots, 2], or directly from x
+void launch_row_moments_from_partials(const float* part, long M, int slots, int N, float eps, float* mr,
+                                      hipStream_t s);
+void launch_row_moments(const bf16_t* x, long M, int N, long ldx, float eps, float* mr, hipStream_t s);
 
 // ---------------------------------------------------------------- elementwise
 void launch_cache_flush(const void* buf, size_t bytes, unsigned* sink, hipStream_t s);
@@ -119,6 +130,15 @@ struct GemmArgs {
   // fp8 weights (skinny kernel only): W is e4m3 [N, K] bytes, w_scale[n] fp32 per output row
   const float* w_scale;
   int w_nt;                 // skinny kernel: weight stream with the nt cache policy (set by its launcher)
+  // LayerNorm folded into the GEMM (v4 kernel, unsplit, batch 1): acc <- rstd[m] * (acc - mean[m] * col_s[n])
+  // before the epilogue; the norm gain is pre-multiplied into W's columns and its shift into the bias
+  const float* row_mr;      // [M, 2] (mean, rstd) of the un-normalised A rows
+  const float* col_s;       // [N] column sums of the gain-folded W (fp32, from its bf16 values)
+  // output statistics for the NEXT norm, written by the v4 wide epilogue (gemm4_stats_ok); other kernels leave
+  // them to the fallback passes of launch_out_stats
+  float* col_part;          // [M / 128, N, 2]: per 128-row block and column (sum, sum of squares) -> GroupNorm
+  float* row_part;          // [M, row_part_slots, 2]: per row (sum, sum of squares) of each wave's column slice
+  int row_part_slots;       //   -> LayerNorm; slots = 4 * column tiles
 };
 void launch_dequant_fp8_rows(const uint8_t* w8, const float* scale, bf16_t* out, long N, int K, hipStream_t s);
 // fp8 e4m3 MFMA GEMM (gemm_f8.hip): C = epi(a_scale[m] w_scale[n] A8 W8^T); A8 / W8 are e4m3 bytes, lda / ldw in
@@ -150,6 +170,8 @@ void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipS
 // v4: 8-phase ping-pong 256x256 / 256x320 LDS-DMA GEMM / conv (gemm_8ph.hip); config indices
 // gemm2_num_cfgs() - 2 (bn 256) and - 1 (bn 320)
 bool gemm4_supported(const GemmArgs& a);
+// every tile of this problem takes the v4 wide epilogue (the only path that writes col_part / row_part)
+bool gemm4_stats_ok(const GemmArgs& a, int bn);
 void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t s, bool persist = false);
 // skinny (decode-shaped, M <= 64) streaming GEMM; ws: skinny_workspace_bytes (fp32 split-K partials)
 bool skinny_supported(const GemmArgs& a);

@@ -543,4 +543,166 @@ void launch_groupnorm_apply(const GroupNormArgs& a, hipStream_t s) {
                                               a.C, a.silu);
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// Norm statistics handed from a GEMM epilogue to the next norm (GemmArgs::col_part / row_part, gemm_8ph.hip), and
+// the passes that produce the same statistics when the producing kernel could not (fallbacks).
+
+// col partials [M / 128, N, 2] of x [M, N]: block = 128 rows; 256 threads = P row lanes x N / 8 channel vectors
+__global__ void __launch_bounds__(256) col_partials_kernel(const bf16_t* __restrict__ x, long M, int N, long ldx,
+                                                           float* __restrict__ part) {
+  __shared__ float4_ red[256][4];  // [thread][sum 0-3, sum 4-7, sq 0-3, sq 4-7]
+  const int C8 = N >> 3, P = 256 / C8, t = threadIdx.x;
+  const int pl = t / C8, cv = t - pl * C8;
+  const long r0 = (long)blockIdx.x * 128, r1 = min(M, r0 + 128);
+  float s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
+  if (pl < P) {
+    for (long r = r0 + pl; r < r1; r += P) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4_*>(x + r * ldx + cv * 8), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s[e] += f[e];
+        q[e] = fmaf(f[e], f[e], q[e]);
+      }
+    }
+  }
+  red[t][0] = float4_{s[0], s[1], s[2], s[3]};
+  red[t][1] = float4_{s[4], s[5], s[6], s[7]};
+  red[t][2] = float4_{q[0], q[1], q[2], q[3]};
+  red[t][3] = float4_{q[4], q[5], q[6], q[7]};
+  __syncthreads();
+  if (t < C8) {
+    float4_ a0 = red[t][0], a1 = red[t][1], b0 = red[t][2], b1 = red[t][3];
+    for (int l = 1; l < P; ++l) {
+      a0 += red[l * C8 + t][0];
+      a1 += red[l * C8 + t][1];
+      b0 += red[l * C8 + t][2];
+      b1 += red[l * C8 + t][3];
+    }
+    float4_* dst = reinterpret_cast<float4_*>(part + ((long)blockIdx.x * N + t * 8) * 2);
+    dst[0] = float4_{a0[0], b0[0], a0[1], b0[1]};
+    dst[1] = float4_{a0[2], b0[2], a0[3], b0[3]};
+    dst[2] = float4_{a1[0], b1[0], a1[1], b1[1]};
+    dst[3] = float4_{a1[2], b1[2], a1[3], b1[3]};
+  }
+}
+
+void launch_col_partials(const bf16_t* x, long M, int N, long ldx, float* part, hipStream_t s) {
+  if (M <= 0) return;
+  col_partials_kernel<<<(unsigned)((M + 127) / 128), 256, 0, s>>>(x, M, N, ldx, part);
+}
+
+// GroupNorm (scale, shift) of image n from the col partials of x (channels [0, C1)) and x2 ([C1, C1 + C2)):
+// per-channel totals over the image's HW / 128 row blocks in LDS, then per group in double (as gn_finalize_image)
+__global__ void __launch_bounds__(256) gn_from_partials_kernel(const float* __restrict__ part1, int C1,
+                                                               const float* __restrict__ part2, int C2, int HW, int G,
+                                                               const bf16_t* __restrict__ gamma,
+                                                               const bf16_t* __restrict__ beta, float eps,
+                                                               float* __restrict__ scale, float* __restrict__ shift) {
+  extern __shared__ float gfp_lds[];  // [C][2] channel totals
+  __shared__ float mean_s[128], rstd_s[128];
+  const int n = blockIdx.x, C = C1 + C2, R = HW / 128;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const bool first = c < C1;
+    const float* src = first ? part1 + ((long)n * R * C1 + c) * 2 : part2 + ((long)n * R * C2 + (c - C1)) * 2;
+    const long step = (long)(first ? C1 : C2) * 2;
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < R; ++r) {
+      const float2 v = *reinterpret_cast<const float2*>(src + r * step);
+      a += v.x;
+      b += v.y;
+    }
+    gfp_lds[2 * c] = a;
+    gfp_lds[2 * c + 1] = b;
+  }
+  __syncthreads();
+  const int Cg = C / G;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    double sa = 0.0, sb = 0.0;
+    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+      sa += gfp_lds[2 * c];
+      sb += gfp_lds[2 * c + 1];
+    }
+    const double cnt = (double)HW * Cg;
+    const double mean = sa / cnt;
+    double var = sb / cnt - mean * mean;
+    if (var < 0) var = 0;
+    mean_s[g] = (float)mean;
+    rstd_s[g] = (float)(1.0 / sqrt(var + (double)eps));
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int g = c / Cg;
+    const float sc = rstd_s[g] * (gamma ? bf2f(gamma[c]) : 1.f);
+    scale[(long)n * C + c] = sc;
+    shift[(long)n * C + c] = (beta ? bf2f(beta[c]) : 0.f) - mean_s[g] * sc;
+  }
+}
+
+void launch_gn_from_partials(const float* part1, int C1, const float* part2, int C2, int Nimg, int HW, int G,
+                             const bf16_t* gamma, const bf16_t* beta, float eps, float* scale, float* shift,
+                             hipStream_t s) {
+  const size_t lds = (size_t)(C1 + C2) * 2 * sizeof(float);
+  gn_from_partials_kernel<<<Nimg, 256, lds, s>>>(part1, C1, part2, C2, HW, G, gamma, beta, eps, scale, shift);
+}
+
+// LayerNorm row moments (mean, rstd) from the per-row partials of a GEMM epilogue: one thread per row
+__global__ void __launch_bounds__(256) row_moments_part_kernel(const float* __restrict__ part, long M, int slots,
+                                                               float inv_n, float eps, float* __restrict__ mr) {
+  const long m = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  const float2* src = reinterpret_cast<const float2*>(part) + m * slots;
+  float a = 0.f, b = 0.f;
+  for (int k = 0; k < slots; ++k) {
+    const float2 v = src[k];
+    a += v.x;
+    b += v.y;
+  }
+  const float mean = a * inv_n;
+  const float var = fmaxf(b * inv_n - mean * mean, 0.f);
+  *reinterpret_cast<float2*>(mr + 2 * m) = make_float2(mean, rsqrtf(var + eps));
+}
+
+void launch_row_moments_from_partials(const float* part, long M, int slots, int N, float eps, float* mr,
+                                      hipStream_t s) {
+  if (M <= 0) return;
+  row_moments_part_kernel<<<(unsigned)((M + 255) / 256), 256, 0, s>>>(part, M, slots, 1.f / N, eps, mr);
+}
+
+// the same moments straight from x [M, N] (fallback): one wave per row, lanes over 8-element vectors
+__global__ void __launch_bounds__(256) row_moments_kernel(const bf16_t* __restrict__ x, long M, int N, long ldx,
+                                                          float eps, float* __restrict__ mr) {
+  const long m = blockIdx.x * 4L + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (m >= M) return;
+  float a = 0.f, b = 0.f;
+  for (int c = lane * 8; c < N; c += 512) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4_*>(x + m * ldx + c), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a += f[e];
+      b = fmaf(f[e], f[e], b);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  if (lane == 0) {
+    const float mean = a / N;
+    const float var = fmaxf(b / N - mean * mean, 0.f);
+    *reinterpret_cast<float2*>(mr + 2 * m) = make_float2(mean, rsqrtf(var + eps));
+  }
+}
+
+void launch_row_moments(const bf16_t* x, long M, int N, long ldx, float eps, float* mr, hipStream_t s) {
+  if (M <= 0) return;
+  row_moments_kernel<<<(unsigned)((M + 3) / 4), 256, 0, s>>>(x, M, N, ldx, eps, mr);
+}
+
 }  // namespace shai

@@ -90,15 +90,21 @@ def count_flops():
 
 def sd21_unet_flops(batch: int = 2, res: int = 512) -> FlopCounter:
     """FLOPs of one SD2.1 UNet forward at `batch` (already CFG-doubled) and resolution."""
+    from ..models import unet2d
     from ..models.unet2d import UNet2DConditionModel, UNetConfig
     unet = UNet2DConditionModel(UNetConfig.sd21())
     h = res // 8
-    with count_flops() as fc, torch.no_grad():
-        ctx = torch.zeros(batch, 77, 1024, dtype=torch.bfloat16)
-        kv = unet.context_kv(ctx)
-        fc.flops.clear()
-        fc.calls.clear()
-        unet(torch.zeros(batch, h, h, 4, dtype=torch.bfloat16), torch.tensor([1.0]), kv)
+    handoff = unet2d.NORM_HANDOFF
+    unet2d.NORM_HANDOFF = False  # same GEMMs either way; the counter stubs the plain norm ops only
+    try:
+        with count_flops() as fc, torch.no_grad():
+            ctx = torch.zeros(batch, 77, 1024, dtype=torch.bfloat16)
+            kv = unet.context_kv(ctx)
+            fc.flops.clear()
+            fc.calls.clear()
+            unet(torch.zeros(batch, h, h, 4, dtype=torch.bfloat16), torch.tensor([1.0]), kv)
+    finally:
+        unet2d.NORM_HANDOFF = handoff
     return fc
 
 

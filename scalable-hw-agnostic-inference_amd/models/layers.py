@@ -40,6 +40,26 @@ class Linear(nn.Module):
     def forward(self, x, act=None, residual=None, alpha: float = 1.0):
         return ops.linear(x, self.weight, self.bias, act=act, residual=residual, alpha=alpha)
 
+    def forward_stats(self, x, residual=None, stats: str = "ln", eps: float = 1e-5):
+        """(y, statistics of y for the next norm) -- see ``ops.linear_stats``."""
+        return ops.linear_stats(x, self.weight, self.bias, residual=residual, stats=stats, eps=eps)
+
+    def folded(self, ln: "LayerNorm"):
+        """(w', bias', s) of this projection with LayerNorm ``ln`` folded in (``ops.fold_layernorm``); cached
+        until the weights change."""
+        return _folded(self, ln)
+
+
+def _folded(lin, ln):
+    # (inference-mode tensors carry no version counter: their storage identity is the key)
+    key = tuple((t.data_ptr(), 0 if t.is_inference() else t._version) if t is not None else None
+                for t in (lin.weight, lin.bias, ln.weight, ln.bias))
+    cache = getattr(lin, "_ln_fold", None)
+    if cache is None or cache[0] != key:
+        cache = (key, ops.fold_layernorm(lin.weight, lin.bias, ln.weight, ln.bias))
+        lin._ln_fold = cache
+    return cache[1]
+
 
 class GLULinear(nn.Module):
     """Linear producing 2*F features consumed as value * act(gate) -> F outputs.
@@ -72,6 +92,9 @@ class GLULinear(nn.Module):
     def forward(self, x, residual=None):
         return ops.linear(x, self.weight, self.bias, act=self.act, residual=residual, glu=True)
 
+    def folded(self, ln: "LayerNorm"):
+        return _folded(self, ln)
+
 
 class Conv2d(nn.Module):
     """NHWC conv on the implicit-GEMM kernel. Input channels padded to a multiple of 8."""
@@ -100,11 +123,14 @@ class Conv2d(nn.Module):
             x = torch.nn.functional.pad(x, (0, self.cin_p - x.shape[-1]))
         return x
 
-    def forward(self, x, norm=None, temb=None, residual=None, upsample: bool = False, x2=None, act=None):
+    def forward(self, x, norm=None, temb=None, residual=None, upsample: bool = False, x2=None, act=None,
+                stats=None, eps: float = 1e-5):
+        """stats="gn" / "ln": returns (out, statistics of out for the next norm), see ``ops.conv2d``."""
         if x2 is None:
             x = self._pad_in(x)
+        extra = {} if stats is None else {"stats": stats, "eps": eps}
         return ops.conv2d(x, self.weight, self.bias, self.k, self.k, self.stride, self.padding, upsample=upsample,
-                          x2=x2, norm=norm, temb=temb, residual=residual, act=act)
+                          x2=x2, norm=norm, temb=temb, residual=residual, act=act, **extra)
 
 
 class GroupNorm(nn.Module):
@@ -118,9 +144,16 @@ class GroupNorm(nn.Module):
         """(scale, shift) fp32 [N, C]: fed to a consumer conv's fused prologue."""
         return ops.groupnorm_stats(x, self.weight, self.bias, self.groups, self.eps, x2=x2)
 
-    def forward(self, x, silu: bool = False, x2=None):
-        """GroupNorm of x, or of cat([x, x2], -1) without materialising the concat."""
-        sc, sh = self.stats(x, x2)
+    def forward(self, x, silu: bool = False, x2=None, part=None, part2=None):
+        """GroupNorm of x, or of cat([x, x2], -1) without materialising the concat.  ``part`` / ``part2``:
+        partials of x / x2 handed over by their producing GEMM (``conv2d(stats="gn")``), which replace the
+        statistics pass over the input."""
+        if part is not None and (x2 is None or part2 is not None):
+            sc, sh = ops.groupnorm_stats_from_partials(part, self.weight, self.bias, self.groups, self.eps,
+                                                       x.shape[0], x.numel() // (x.shape[0] * x.shape[-1]),
+                                                       part2=part2 if x2 is not None else None)
+        else:
+            sc, sh = self.stats(x, x2)
         return ops.groupnorm_apply(x, sc, sh, silu, x2=x2)
 
 

@@ -17,6 +17,7 @@ runs (cuDNN/Inductor on GPU, NEFF on Inferentia).  MI355X-first design:
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Tuple
 
@@ -26,6 +27,10 @@ import torch.nn as nn
 from .. import ops
 from .attention import CrossAttention, FusedSelfAttention, merge_linear_keys
 from .layers import Conv2d, GLULinear, GroupNorm, LayerNorm, Linear, timestep_embedding
+
+# GroupNorm partials / LayerNorm moments handed from the producing GEMM epilogue to the next norm (and LayerNorms
+# folded into their consumer projections); SHAI_NORM_HANDOFF=0 restores the standalone norm passes (A/B)
+NORM_HANDOFF = os.environ.get("SHAI_NORM_HANDOFF", "1") != "0"
 
 
 @dataclass
@@ -67,14 +72,27 @@ class ResnetBlock2D(nn.Module):
     def forward(self, x, temb_proj=None, x2=None):
         """``x2``: up-block skip tensor -- the block's input is cat([x, x2], -1), read from the two
         sources by GroupNorm and by the 1x1 shortcut conv (fused concat), never materialised."""
+        return self.forward_parts(x, temb_proj, x2)[0]
+
+    def forward_parts(self, x, temb_proj=None, x2=None, xp=None, x2p=None, stats: bool = False):
+        """forward with the GroupNorm hand-off: ``xp`` / ``x2p`` are GroupNorm partials of x / x2 written by their
+        producers' epilogues (they replace the statistics pass of norm1); with ``stats`` conv1 and conv2 write
+        the partials of their outputs (norm2's input, and the next norm's).  Returns (out, partials or None)."""
         # GroupNorm+SiLU as one memory-bound pass (normalising inside the 3x3 gather would
         # redo the transform 9x per N-tile: VALU-bound, measured 5x slower).
-        h = self.conv1(self.norm1(x, silu=True, x2=x2), temb=temb_proj)
+        n1 = self.norm1(x, silu=True, x2=x2, part=xp, part2=x2p)
+        if stats:
+            h, hp = self.conv1(n1, temb=temb_proj, stats="gn")
+        else:
+            h, hp = self.conv1(n1, temb=temb_proj), None
         if self.conv_shortcut is not None:
             skip = self.conv_shortcut(x, x2=x2) if x2 is not None else self.conv_shortcut(x)
         else:
             skip = x if x2 is None else torch.cat([x, x2], dim=-1)
-        return self.conv2(self.norm2(h, silu=True), residual=skip)
+        n2 = self.norm2(h, silu=True, part=hp)
+        if stats:
+            return self.conv2(n2, residual=skip, stats="gn")
+        return self.conv2(n2, residual=skip), None
 
 
 class GEGLU(nn.Module):
@@ -108,6 +126,33 @@ class BasicTransformerBlock(nn.Module):
         x = self.attn2(self.norm2(x), ctx_kv, residual=x)
         return self.ff(self.norm3(x), residual=x)
 
+    def forward_folded(self, x, ctx_kv, mr, next_eps=None):
+        """forward with every LayerNorm folded into the projection that consumes it: ``mr`` = (mean, rstd) [rows, 2]
+        of x from its producer; each residual GEMM (attention out-projections, FF down) hands the next norm's
+        (mean, rstd) over from its epilogue, so no normalised activation is ever written.  ``next_eps``: the
+        following block's norm1 eps (its statistics are returned), None for the last block."""
+        B, T, C = x.shape
+        a1 = self.attn1
+        w, b, s = a1.qkv.folded(self.norm1)
+        q, k, v = a1.split(ops.linear(x, w, b, row_affine=(mr, s)))
+        o = ops.attention(q, k, v)
+        x, mr = a1.out.forward_stats(o.view(B, T, a1.heads * a1.head_dim), residual=x, stats="ln", eps=self.norm2.eps)
+        a2 = self.attn2
+        w, b, s = a2.q.folded(self.norm2)
+        H, hd = a2.heads, a2.head_dim
+        q = ops.linear(x, w, b, row_affine=(mr, s)).view(B, T, H, hd)
+        S = ctx_kv.shape[1]
+        o = ops.attention(q, ctx_kv[..., : H * hd].view(ctx_kv.shape[0], S, H, hd),
+                          ctx_kv[..., H * hd:].view(ctx_kv.shape[0], S, H, hd))
+        x, mr = a2.out.forward_stats(o.view(B, T, H * hd), residual=x, stats="ln", eps=self.norm3.eps)
+        proj = self.ff.net[0].proj
+        w, b, s = proj.folded(self.norm3)
+        h = ops.linear(x, w, b, act=proj.act, glu=True, row_affine=(mr, s))
+        down = self.ff.net[2]
+        if next_eps is None:
+            return down(h, residual=x), None
+        return down.forward_stats(h, residual=x, stats="ln", eps=next_eps)
+
 
 class Transformer2DModel(nn.Module):
     def __init__(self, channels: int, heads: int, ctx_dim: int, groups: int):
@@ -124,6 +169,24 @@ class Transformer2DModel(nn.Module):
             h = blk(h, ctx_kv)
         return self.proj_out(h, residual=x.view(B, H * W, C)).view(B, H, W, C)
 
+    def forward_parts(self, x, ctx_kv, xp=None, stats: bool = False):
+        """forward with the norm hand-offs: GroupNorm partials ``xp`` of x in, LayerNorms folded into the block
+        projections (``BasicTransformerBlock.forward_folded``), and with ``stats`` the GroupNorm partials of the
+        output out.  Returns (out, partials or None)."""
+        B, H, W, C = x.shape
+        blocks = list(self.transformer_blocks)
+        h, mr = self.proj_in(self.norm(x, part=xp), stats="ln", eps=blocks[0].norm1.eps)
+        h = h.view(B, H * W, C)
+        if mr is None:
+            mr = ops.row_moments(h, blocks[0].norm1.eps)
+        for i, blk in enumerate(blocks):
+            h, mr = blk.forward_folded(h, ctx_kv, mr, blocks[i + 1].norm1.eps if i + 1 < len(blocks) else None)
+        res = x.view(B, H * W, C)
+        if stats and ops.stats_supported(B * H * W, C, "gn", H * W):
+            out, op = self.proj_out.forward_stats(h, residual=res, stats="gn")
+            return out.view(B, H, W, C), op
+        return self.proj_out(h, residual=res).view(B, H, W, C), None
+
 
 class Downsample2D(nn.Module):
     def __init__(self, ch):
@@ -133,6 +196,9 @@ class Downsample2D(nn.Module):
     def forward(self, x):
         return self.conv(x)
 
+    def forward_parts(self, x, stats: bool = False):
+        return self.conv(x, stats="gn") if stats else (self.conv(x), None)
+
 
 class Upsample2D(nn.Module):
     def __init__(self, ch):
@@ -141,6 +207,9 @@ class Upsample2D(nn.Module):
 
     def forward(self, x):
         return self.conv(x, upsample=True)
+
+    def forward_parts(self, x, stats: bool = False):
+        return self.conv(x, upsample=True, stats="gn") if stats else (self.conv(x, upsample=True), None)
 
 
 class DownBlock(nn.Module):
@@ -262,29 +331,39 @@ class UNet2DConditionModel(nn.Module):
         ti = iter(tprojs)
         kvi = iter(ctx_kv)
 
-        x = self.conv_in(sample)
-        skips = [x]
+        # Norm hand-offs (NORM_HANDOFF): every conv / GEMM whose output feeds a GroupNorm writes that norm's
+        # partial sums from its epilogue (no statistics pass over the activation), and the transformer blocks'
+        # LayerNorms are folded into the projections that consume them (no normalised activation written).
+        st = NORM_HANDOFF
+        x, xp = self.conv_in(sample, stats="gn") if st else (self.conv_in(sample), None)
+        skips = [(x, xp)]
         for blk in self.down_blocks:
             for i, r in enumerate(blk.resnets):
-                x = r(x, next(ti))
+                x, xp = r.forward_parts(x, next(ti), xp=xp, stats=st)
                 if blk.attentions is not None:
-                    x = blk.attentions[i](x, next(kvi))
-                skips.append(x)
+                    x, xp = self._attn(blk.attentions[i], x, next(kvi), xp, st)
+                skips.append((x, xp))
             if blk.downsamplers is not None:
-                x = blk.downsamplers[0](x)
-                skips.append(x)
-        x = self.mid_block.resnets[0](x, next(ti))
-        x = self.mid_block.attentions[0](x, next(kvi))
-        x = self.mid_block.resnets[1](x, next(ti))
+                x, xp = blk.downsamplers[0].forward_parts(x, st)
+                skips.append((x, xp))
+        x, xp = self.mid_block.resnets[0].forward_parts(x, next(ti), xp=xp, stats=st)
+        x, xp = self._attn(self.mid_block.attentions[0], x, next(kvi), xp, st)
+        x, xp = self.mid_block.resnets[1].forward_parts(x, next(ti), xp=xp, stats=st)
         for blk in self.up_blocks:
             for i, r in enumerate(blk.resnets):
-                s = skips.pop()
-                x = r(x, next(ti), x2=s)
+                s, sp = skips.pop()
+                x, xp = r.forward_parts(x, next(ti), x2=s, xp=xp, x2p=sp, stats=st)
                 if blk.attentions is not None:
-                    x = blk.attentions[i](x, next(kvi))
+                    x, xp = self._attn(blk.attentions[i], x, next(kvi), xp, st)
             if blk.upsamplers is not None:
-                x = blk.upsamplers[0](x)
-        return self.conv_out(self.conv_norm_out(x, silu=True))
+                x, xp = blk.upsamplers[0].forward_parts(x, st)
+        return self.conv_out(self.conv_norm_out(x, silu=True, part=xp))
+
+    @staticmethod
+    def _attn(t: "Transformer2DModel", x, ctx_kv, xp, st: bool):
+        if st:
+            return t.forward_parts(x, ctx_kv, xp=xp, stats=True)
+        return t(x, ctx_kv), None
 
     # ------------------------------------------------------------------ checkpoints
     def convert_hf_state_dict(self, sd: dict) -> dict:

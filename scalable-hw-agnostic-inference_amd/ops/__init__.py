@@ -183,13 +183,16 @@ def gemm_f8(a8: torch.Tensor, w8: torch.Tensor, a_scale: torch.Tensor, w_scale: 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act=None,
            residual: Optional[torch.Tensor] = None, glu: bool = False, alpha: float = 1.0,
            res_alpha: float = 1.0, rms_eps: Optional[float] = None,
-           w_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
+           w_scale: Optional[torch.Tensor] = None, row_affine=None, force_cfg: int = -1) -> torch.Tensor:
     """y = act(alpha * x @ w^T + bias) (+ res_alpha * residual).
 
     glu=True: ``w`` rows are interleaved (value_i, gate_i) pairs and the output
     has N/2 columns: value * act(gate) (SwiGLU / GEGLU fused in the epilogue).
     rms_eps: x is RMS-normalised first (unweighted: the norm gain must already be
     folded into w's columns); on the GPU this is fused into the decode GEMM.
+    row_affine = (mr [M, 2] fp32, s [N] fp32): a LayerNorm of x folded into the GEMM -- y = rstd[m] * (x @ w^T -
+    mean[m] * s[n]) + bias, with the norm gain / shift pre-folded into w / bias (``fold_layernorm``) and
+    (mean, rstd) from the producer of x (``linear_stats`` / ``conv2d(stats="ln")``).
     w_scale: ``w`` is fp8 e4m3 with one fp32 scale per row (``quantize_fp8_rows``).  Decode-shaped
     problems (<= 64 rows) stream the fp8 bytes through the skinny kernel (half the weight
     traffic); larger ones run W8A8 on the fp8 MFMA (``FP8_PREFILL``: the activation is quantised per row, with
@@ -212,7 +215,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if not _gpu(x):
         if rms_eps is not None:
             x = ref.rmsnorm(x, None, rms_eps)[0]
-        return ref.linear(x, w, bias, act, residual, glu, alpha, res_alpha)
+        return ref.linear(x, w, bias, act, residual, glu, alpha, res_alpha, row_affine=row_affine)
+    if row_affine is not None:
+        return _linear_norm_io(x, w, bias, act, residual, glu, alpha, res_alpha, row_affine, None, 0.0, force_cfg)[0]
     K = x.shape[-1]
     N = w.shape[0]
     lead = x.shape[:-1]
@@ -226,6 +231,88 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     _K().gemm(x2, w, y, bias, None, 1, r2, float(alpha), float(res_alpha), act_id(act), bool(glu), None, 1, -1,
               float(rms_eps) if rms_eps is not None else -1.0, w_scale)
     return y.view(*lead, Nout)
+
+
+def _linear_norm_io(x, w, bias, act, residual, glu, alpha, res_alpha, row_affine, stats, eps, force_cfg=-1):
+    K = x.shape[-1]
+    x2 = x.reshape(-1, K) if (x.dim() == 2 or x.is_contiguous()) else x.contiguous().reshape(-1, K)
+    M, N = x2.shape[0], w.shape[0]
+    Nout = N // 2 if glu else N
+    y = torch.empty(M, Nout, dtype=x.dtype, device=x.device)
+    r2 = residual.reshape(-1, Nout) if residual is not None else None
+    mr, s = row_affine if row_affine is not None else (None, None)
+    gp = torch.empty(M // 128, Nout, 2, dtype=torch.float32, device=x.device) if stats == "gn" else None
+    ls = torch.empty(M, 2, dtype=torch.float32, device=x.device) if stats == "ln" else None
+    _K().gemm(x2, w, y, bias, None, 1, r2, float(alpha), float(res_alpha), act_id(act), bool(glu), None, 1,
+              int(force_cfg), -1.0, None, mr, s, gp, ls, float(eps))
+    return y.view(*x.shape[:-1], Nout), (gp if stats == "gn" else ls)
+
+
+def stats_supported(rows: int, cols: int, kind: str, hw: Optional[int] = None) -> bool:
+    """Whether ``linear_stats`` / ``conv2d(stats=...)`` can hand statistics of this output to the next norm:
+    GroupNorm partials need 128-row blocks inside one image (hw % 128 == 0), N % 8 == 0, N <= 2048."""
+    if cols % 8 != 0:
+        return False
+    if kind == "gn":
+        return rows % 128 == 0 and cols <= 2048 and (hw is None or hw % 128 == 0)
+    return True
+
+
+def linear_stats(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None, stats: str = "ln",
+                 eps: float = 1e-5, row_affine=None, force_cfg: int = -1):
+    """``linear`` that also returns statistics of its output for the next norm: stats="ln" -> (mean, rstd) [M, 2]
+    with ``eps``; "gn" -> GroupNorm partials [M / 128, N, 2] (``groupnorm_stats_from_partials``).  On the GPU the
+    v4 GEMM epilogue writes them (a pass over the output when the tuned kernel cannot)."""
+    if not _gpu(x):
+        y = ref.linear(x, w, bias, act, residual, False, 1.0, 1.0, row_affine=row_affine)
+        y2 = y.reshape(-1, y.shape[-1])
+        return y, (ref.row_moments(y2, eps) if stats == "ln" else ref.col_partials(y2))
+    return _linear_norm_io(x, w, bias, act, residual, False, 1.0, 1.0, row_affine, stats, eps, force_cfg)
+
+
+def fold_layernorm(w: torch.Tensor, bias: Optional[torch.Tensor], gamma: Optional[torch.Tensor],
+                   beta: Optional[torch.Tensor]):
+    """(w', bias', s) so that LayerNorm(x; gamma, beta) @ w^T + bias == rstd * (x @ w'^T - mean * s) + bias':
+    w' = w * gamma (columns), bias' = bias + w @ beta, s = row sums of w' (fp32, from its bf16 values)."""
+    wf = w.float()
+    w2 = (wf * gamma.float()[None, :]).to(w.dtype) if gamma is not None else w
+    b2 = bias.float() if bias is not None else torch.zeros(w.shape[0], dtype=torch.float32, device=w.device)
+    if beta is not None:
+        b2 = b2 + wf @ beta.float()
+    return w2.contiguous(), b2.to(w.dtype), w2.float().sum(1).contiguous()
+
+
+def row_moments(x: torch.Tensor, eps: float) -> torch.Tensor:
+    """(mean, rstd) [M, 2] of the rows of x [..., N] (the statistics a folded LayerNorm consumes)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    if not _gpu(x):
+        return ref.row_moments(x2, eps)
+    mr = torch.empty(x2.shape[0], 2, dtype=torch.float32, device=x.device)
+    _K().row_moments(x2, mr, float(eps))
+    return mr
+
+
+def col_partials(x: torch.Tensor) -> torch.Tensor:
+    """GroupNorm partials [M / 128, N, 2] of x [..., N] (rows grouped by 128)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    if not _gpu(x):
+        return ref.col_partials(x2)
+    part = torch.empty(x2.shape[0] // 128, x2.shape[1], 2, dtype=torch.float32, device=x.device)
+    _K().col_partials(x2, part)
+    return part
+
+
+def groupnorm_stats_from_partials(part: torch.Tensor, gamma, beta, groups: int, eps: float, nimg: int, hw: int,
+                                  part2: Optional[torch.Tensor] = None):
+    """GroupNorm (scale, shift) fp32 [N, C] from the partials of x (and of x2 for cat([x, x2], -1))."""
+    C1 = part.shape[-2]
+    C2 = part2.shape[-2] if part2 is not None else 0
+    if not part.is_cuda:
+        return ref.groupnorm_from_partials(part, part2, C1, C2, nimg, hw, gamma, beta, groups, eps)
+    scale = torch.empty(nimg, C1 + C2, dtype=torch.float32, device=part.device)
+    shift = torch.empty_like(scale)
+    _K().groupnorm_from_partials(part, part2, C1, C2, nimg, hw, gamma, beta, scale, shift, int(groups), float(eps))
+    return scale, shift
 
 
 def gemm_into(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias=None, act=None, residual=None, gate=None,
@@ -288,15 +375,23 @@ def bmm(a: torch.Tensor, w: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
 def conv2d(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], kh: int, kw: int, stride: int = 1,
            pad: int = 0, upsample: bool = False, x2: Optional[torch.Tensor] = None, norm=None,
            temb: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None, act=None,
-           res_alpha: float = 1.0) -> torch.Tensor:
+           res_alpha: float = 1.0, stats: Optional[str] = None, eps: float = 1e-5):
     """NHWC implicit-GEMM convolution with fused prologue/epilogue.
 
     norm = (scale [N,Cin] f32, shift [N,Cin] f32, act) applies GroupNorm(+act) to
     the gathered input; x2 is concatenated on channels; upsample reads a
     nearest-2x view; temb [N, Cout] is a per-image bias; residual is added last.
+    stats="gn" / "ln": also return statistics of the output for the next norm, as ``linear_stats`` -- (out, st);
+    st is None when the output shape cannot carry them (``stats_supported``).
     """
     if not _gpu(x):
-        return ref.conv2d(x, w_packed, bias, kh, kw, stride, pad, upsample, x2, norm, temb, residual, act, res_alpha)
+        y = ref.conv2d(x, w_packed, bias, kh, kw, stride, pad, upsample, x2, norm, temb, residual, act, res_alpha)
+        if stats is None:
+            return y
+        y2 = y.reshape(-1, y.shape[-1])
+        if not stats_supported(y2.shape[0], y2.shape[1], stats, y.shape[1] * y.shape[2]):
+            return y, None
+        return y, (ref.row_moments(y2, eps) if stats == "ln" else ref.col_partials(y2))
     N, H, W, _ = x.shape
     IH, IW = (2 * H, 2 * W) if upsample else (H, W)
     OH = (IH + 2 * pad - kh) // stride + 1
@@ -304,9 +399,18 @@ def conv2d(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor]
     cout = w_packed.shape[0]
     out = torch.empty(N, OH, OW, cout, dtype=x.dtype, device=x.device)
     sc, sh, nact = (norm if norm is not None else (None, None, None))
+    M = N * OH * OW
+    if stats is not None and not stats_supported(M, cout, stats, OH * OW):
+        want = None
+    else:
+        want = stats
+    gp = torch.empty(M // 128, cout, 2, dtype=torch.float32, device=x.device) if want == "gn" else None
+    ls = torch.empty(M, 2, dtype=torch.float32, device=x.device) if want == "ln" else None
     _K().conv2d(x, x2, w_packed, out, bias, temb, residual, sc, sh, act_id(nact), kh, kw, stride, pad, bool(upsample),
-                act_id(act), float(res_alpha))
-    return out
+                act_id(act), float(res_alpha), None, None, gp, ls, float(eps))
+    if stats is None:
+        return out
+    return out, (gp if want == "gn" else ls)
 
 
 # ----------------------------------------------------------------------------- attention

@@ -76,6 +76,42 @@ def groupnorm_stats(x, gamma, beta, groups, eps):
     return scale, shift
 
 
+def col_partials(y):
+    """[M, N] -> [M / 128, N, 2]: per 128-row block and column (sum, sum of squares) of the bf16 values."""
+    M, N = y.shape
+    f = y.float().reshape(M // 128, 128, N)
+    return torch.stack([f.sum(1), (f * f).sum(1)], -1)
+
+
+def row_moments(y, eps):
+    """[M, N] -> [M, 2] = (mean, rstd) (population variance), the LayerNorm statistics of each row."""
+    f = y.float()
+    mean = f.mean(-1)
+    var = (f * f).mean(-1) - mean * mean
+    return torch.stack([mean, torch.rsqrt(var.clamp_min(0) + eps)], -1)
+
+
+def groupnorm_from_partials(part1, part2, C1, C2, Nimg, HW, gamma, beta, groups, eps):
+    """GroupNorm (scale, shift) [Nimg, C1 + C2] from col partials [Nimg * HW / 128, C, 2] of one or two sources."""
+    R = HW // 128
+    t = part1.double().reshape(Nimg, R, C1, 2).sum(1)
+    if part2 is not None:
+        t = torch.cat([t, part2.double().reshape(Nimg, R, C2, 2).sum(1)], 1)
+    C = C1 + C2
+    tg = t.reshape(Nimg, groups, C // groups, 2).sum(2)
+    cnt = HW * (C // groups)
+    mean = tg[..., 0] / cnt
+    var = (tg[..., 1] / cnt - mean * mean).clamp_min(0)
+    rstd = 1.0 / torch.sqrt(var + eps)
+    g = gamma.double() if gamma is not None else torch.ones(C, dtype=torch.float64, device=part1.device)
+    b = beta.double() if beta is not None else torch.zeros(C, dtype=torch.float64, device=part1.device)
+    rs = rstd.repeat_interleave(C // groups, 1)
+    mu = mean.repeat_interleave(C // groups, 1)
+    scale = rs * g[None, :]
+    shift = b[None, :] - mu * scale
+    return scale.float(), shift.float()
+
+
 def groupnorm_apply(x, scale, shift, silu):
     N = x.shape[0]
     C = x.shape[-1]
@@ -85,8 +121,14 @@ def groupnorm_apply(x, scale, shift, silu):
     return y.to(x.dtype)
 
 
-def linear(x, w, bias=None, act=None, residual=None, glu=False, alpha=1.0, res_alpha=1.0):
-    y = torch.matmul(x.float(), w.float().t()) * alpha
+def linear(x, w, bias=None, act=None, residual=None, glu=False, alpha=1.0, res_alpha=1.0, row_affine=None):
+    y = torch.matmul(x.float(), w.float().t())
+    if row_affine is not None:  # LayerNorm folded in: rstd[m] * (x w'^T - mean[m] * s[n])
+        mr, s = row_affine
+        mr = mr.float().reshape(-1, 2)
+        y2 = y.reshape(-1, y.shape[-1])
+        y = (mr[:, 1:2] * (y2 - mr[:, 0:1] * s.float()[None, :])).reshape(y.shape)
+    y = y * alpha
     if bias is not None:
         y = y + bias.float()
     if glu:

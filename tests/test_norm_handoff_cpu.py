@@ -1,0 +1,70 @@
+"""CPU reference paths of the norm hand-offs (the GPU kernels are checked against the same functions in
+test_norm_handoff_gpu.py): LayerNorm folding algebra, GroupNorm from partials (with concat), and the UNet forward
+with hand-offs on vs off."""
+import torch
+
+from shai_amd import ops
+from shai_amd.ops import reference as ref
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def test_fold_layernorm_matches_layernorm_then_linear():
+    torch.manual_seed(0)
+    M, K, N = 64, 96, 40
+    x = (torch.randn(M, K) + 0.7).bfloat16()
+    w, b = (torch.randn(N, K) * 0.1).bfloat16(), (torch.randn(N) * 0.1).bfloat16()
+    gamma, beta = (1 + 0.1 * torch.randn(K)).bfloat16(), (0.1 * torch.randn(K)).bfloat16()
+    w2, b2, s = ops.fold_layernorm(w, b, gamma, beta)
+    mr = ops.row_moments(x, 1e-5)
+    y = ops.linear(x, w2, b2, row_affine=(mr, s))
+    xn = torch.nn.functional.layer_norm(x.float(), (K,), gamma.float(), beta.float(), 1e-5)
+    assert rel(y, ref.linear(xn, w, b)) < 1e-2
+    y_st, mr2 = ops.linear_stats(x, w, b, stats="ln", eps=1e-6)
+    assert rel(mr2, ref.row_moments(y_st, 1e-6)) < 1e-6
+
+
+def test_groupnorm_from_partials_concat():
+    torch.manual_seed(1)
+    N, HW, C1, C2 = 3, 256, 64, 32
+    x, x2 = torch.randn(N, HW, C1).bfloat16(), (torch.randn(N, HW, C2) + 1).bfloat16()
+    gamma, beta = torch.randn(C1 + C2).bfloat16(), torch.randn(C1 + C2).bfloat16()
+    sc, sh = ops.groupnorm_stats_from_partials(ops.col_partials(x), gamma, beta, 8, 1e-5, N, HW,
+                                               part2=ops.col_partials(x2))
+    sc0, sh0 = ref.groupnorm_stats(torch.cat([x, x2], -1), gamma, beta, 8, 1e-5)
+    assert rel(sc, sc0) < 1e-5 and rel(sh, sh0) < 1e-5
+
+
+def test_conv_stats_shapes():
+    torch.manual_seed(2)
+    x = torch.randn(2, 16, 16, 8).bfloat16()
+    w = ops.pack_conv_weight((torch.randn(16, 8, 3, 3) * 0.1).bfloat16())
+    y, p = ops.conv2d(x, w, None, 3, 3, 1, 1, stats="gn")
+    assert p.shape == (4, 16, 2) and rel(p, ref.col_partials(y.reshape(-1, 16))) < 1e-6
+    y, p = ops.conv2d(torch.randn(2, 8, 8, 8).bfloat16(), w, None, 3, 3, 1, 1, stats="gn")
+    assert p is None  # 64-pixel images: a 128-row block would straddle two images
+
+
+def test_unet_norm_handoff_cpu():
+    from shai_amd.models import unet2d
+    from shai_amd.models.unet2d import UNet2DConditionModel, UNetConfig
+    torch.manual_seed(3)
+    cfg = UNetConfig.tiny()
+    m = UNet2DConditionModel(cfg).eval()
+    for p in m.parameters():
+        torch.nn.init.normal_(p, std=0.05)
+    x = torch.randn(2, 16, 16, 4).bfloat16()
+    t = torch.tensor([500.0])
+    kv = m.context_kv(torch.randn(2, 77, cfg.cross_attention_dim).bfloat16())
+    old = unet2d.NORM_HANDOFF
+    try:
+        unet2d.NORM_HANDOFF = True
+        y1 = m(x, t, kv)
+        unet2d.NORM_HANDOFF = False
+        y0 = m(x, t, kv)
+    finally:
+        unet2d.NORM_HANDOFF = old
+    assert rel(y1, y0) < 1e-2
