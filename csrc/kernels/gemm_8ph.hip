@@ -68,7 +68,6 @@ __device__ __forceinline__ void g4_glds(__amdgpu_buffer_rsrc_t r, bf16_t* lds, u
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (g4_lds_void*)lds, 16, off, 0, 0, 0);
 }
 
-
 // Schedule variants (lab A/B; 0 = production):
 //   bit 0: no stagger (both wave groups in lockstep)
 //   bit 1: static priority (waves 4-7 at prio 1 for the whole loop) instead of per-segment setprio
@@ -521,11 +520,13 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
                     const uint4_ pv = pack8(v);
                     *reinterpret_cast<uint4_*>(crow + q * 32 + 8 * fq) = pv;
                     if (colp) *reinterpret_cast<uint4_*>(cst + (ii * 16 + fr) * WC + q * 32 + 8 * fq) = pv;
-                    if (rowp) {
+                    if (rowp) {  // moments of the stored (bf16-rounded) values: what the consumer reads
+                      float f[8];
+                      unpack8(pv, f);
 #pragma unroll
                       for (int e = 0; e < 8; ++e) {
-                        rs += v[e];
-                        rq = fmaf(v[e], v[e], rq);
+                        rs += f[e];
+                        rq = fmaf(f[e], f[e], rq);
                       }
                     }
                   }
@@ -543,10 +544,11 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
                     *reinterpret_cast<uint2_*>(crow + 2 * NP * 16 + 4 * fq) = o;
                     if (colp) *reinterpret_cast<uint2_*>(cst + (ii * 16 + fr) * WC + 2 * NP * 16 + 4 * fq) = o;
                     if (rowp) {
+                      const float f[4] = {bf2f(o[0] & 0xffff), bf2f(o[0] >> 16), bf2f(o[1] & 0xffff), bf2f(o[1] >> 16)};
 #pragma unroll
                       for (int e = 0; e < 4; ++e) {
-                        rs += v[e];
-                        rq = fmaf(v[e], v[e], rq);
+                        rs += f[e];
+                        rq = fmaf(f[e], f[e], rq);
                       }
                     }
                   }
