@@ -15,6 +15,7 @@ host does no per-pixel work.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
@@ -25,6 +26,11 @@ import torch.nn.functional as F
 from .. import ops
 from .attention import FusedSelfAttention, merge_linear_keys
 from .layers import Conv2d, LayerNorm, Linear
+
+
+# LayerNorms folded into the GEMMs that consume them, moments handed over by the producing GEMM (unet2d.py);
+# SHAI_NORM_HANDOFF=0 restores the standalone LayerNorm passes
+NORM_HANDOFF = os.environ.get("SHAI_NORM_HANDOFF", "1") != "0"
 
 
 @dataclass
@@ -73,6 +79,22 @@ class ViTLayer(nn.Module):
         x = self.attention(self.layernorm_before(x), residual=x)
         return self.output(self.intermediate(self.layernorm_after(x), act=self.act), residual=x)
 
+    def forward_folded(self, x, mr, next_eps=None):
+        """forward with both LayerNorms folded into the QKV / fc1 GEMMs (``ops.fold_layernorm``): ``mr`` = (mean,
+        rstd) of x's rows, the residual GEMMs hand the next norm's over (``next_eps``: the next layer's eps, None
+        for the last layer).  Returns (out, mr or None)."""
+        B, T, C = x.shape
+        a = self.attention
+        w, b, s = a.qkv.folded(self.layernorm_before)
+        q, k, v = a.split(ops.linear(x, w, b, row_affine=(mr, s)))
+        o = ops.attention(q, k, v).view(B, T, a.heads * a.head_dim)
+        x, mr = a.out.forward_stats(o, residual=x, stats="ln", eps=self.layernorm_after.eps)
+        w, b, s = self.intermediate.folded(self.layernorm_after)
+        h = ops.linear(x, w, b, act=self.act, row_affine=(mr, s))
+        if next_eps is None:
+            return self.output(h, residual=x), None
+        return self.output.forward_stats(h, residual=x, stats="ln", eps=next_eps)
+
 
 class ViTEncoderModel(nn.Module):
     def __init__(self, c: ViTConfig):
@@ -117,6 +139,13 @@ class ViTEncoderModel(nn.Module):
         x = torch.cat(toks, dim=1)
         pe = self.pos_embed(gh, gw).expand(B, -1, -1).contiguous()
         x = ops.bias_act(x.contiguous(), None, pe)
+        if NORM_HANDOFF:
+            layers = list(self.layers)
+            mr = ops.row_moments(x, layers[0].layernorm_before.eps)
+            for i, layer in enumerate(layers):
+                nxt = layers[i + 1].layernorm_before.eps if i + 1 < len(layers) else None
+                x, mr = layer.forward_folded(x, mr, nxt)
+            return self.layernorm(x)
         for layer in self.layers:
             x = layer(x)
         return self.layernorm(x)

@@ -68,3 +68,24 @@ def test_unet_norm_handoff_cpu():
     finally:
         unet2d.NORM_HANDOFF = old
     assert rel(y1, y0) < 1e-2
+
+
+def test_vit_norm_handoff_cpu():
+    from shai_amd.models import vit
+    from shai_amd.models.vit import ViTConfig, ViTEncoderModel
+    torch.manual_seed(4)
+    c = ViTConfig(image_size=(32, 32), patch_size=16, hidden_size=64, num_hidden_layers=2, num_attention_heads=2,
+                  intermediate_size=128)
+    m = ViTEncoderModel(c).eval()
+    for p in m.parameters():
+        torch.nn.init.normal_(p, std=0.05)
+    px = torch.randn(2, 32, 32, 3).bfloat16()
+    old = vit.NORM_HANDOFF
+    try:
+        vit.NORM_HANDOFF = True
+        y1 = m(px)
+        vit.NORM_HANDOFF = False
+        y0 = m(px)
+    finally:
+        vit.NORM_HANDOFF = old
+    assert rel(y1, y0) < 1e-2

@@ -127,3 +127,26 @@ def test_unet_norm_handoff_matches(cuda):
         unet2d.NORM_HANDOFF = old
     assert torch.isfinite(y1).all()
     assert rel(y1, y0) < 2e-2
+
+
+def test_vit_norm_handoff_matches(cuda):
+    """ViT-base widths (2 layers, batch 8: 1,576 token rows, not a multiple of 256 -> the producers' moments come
+    from the fallback pass, the folded QKV / fc1 GEMMs run on the v4 kernel)."""
+    from shai_amd.models import vit
+    from shai_amd.models.vit import ViTConfig, ViTEncoderModel
+    torch.manual_seed(6)
+    c = ViTConfig(num_hidden_layers=2)
+    m = ViTEncoderModel(c).cuda().eval()
+    for p in m.parameters():
+        torch.nn.init.normal_(p, std=0.03)
+    px = torch.randn(8, 224, 224, 3, device="cuda").bfloat16()
+    old = vit.NORM_HANDOFF
+    try:
+        vit.NORM_HANDOFF = True
+        y1 = m(px)
+        vit.NORM_HANDOFF = False
+        y0 = m(px)
+    finally:
+        vit.NORM_HANDOFF = old
+    assert torch.isfinite(y1).all()
+    assert rel(y1, y0) < 2e-2
