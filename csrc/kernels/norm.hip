@@ -595,58 +595,44 @@ void launch_col_partials(const bf16_t* x, long M, int N, long ldx, float* part, 
   col_partials_kernel<<<(unsigned)((M + 127) / 128), 256, 0, s>>>(x, M, N, ldx, part);
 }
 
-// GroupNorm (scale, shift) of image n from the col partials of x (channels [0, C1)) and x2 ([C1, C1 + C2)):
-// per-channel totals over the image's HW / 128 row blocks in LDS, then per group in double (as gn_finalize_image)
-__global__ void __launch_bounds__(256) gn_from_partials_kernel(const float* __restrict__ part1, int C1,
-                                                               const float* __restrict__ part2, int C2, int HW, int G,
-                                                               const bf16_t* __restrict__ gamma,
-                                                               const bf16_t* __restrict__ beta, float eps,
-                                                               float* __restrict__ scale, float* __restrict__ shift) {
-  extern __shared__ float gfp_lds[];  // [C][2] channel totals
-  __shared__ float mean_s[128], rstd_s[128];
-  const int n = blockIdx.x, C = C1 + C2, R = HW / 128;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const bool first = c < C1;
-    const float* src = first ? part1 + ((long)n * R * C1 + c) * 2 : part2 + ((long)n * R * C2 + (c - C1)) * 2;
-    const long step = (long)(first ? C1 : C2) * 2;
-    float a = 0.f, b = 0.f;
-    for (int r = 0; r < R; ++r) {
-      const float2 v = *reinterpret_cast<const float2*>(src + r * step);
-      a += v.x;
-      b += v.y;
-    }
-    gfp_lds[2 * c] = a;
-    gfp_lds[2 * c + 1] = b;
+// GroupNorm (scale, shift) from the col partials of x (channels [0, C1)) and x2 ([C1, C1 + C2)): one wave per
+// (image, group) sums the group's HW / 128 x C / G partial pairs (double), then writes its channels' scale / shift
+__global__ void __launch_bounds__(64) gn_from_partials_kernel(const float* __restrict__ part1, int C1,
+                                                              const float* __restrict__ part2, int C2, int HW, int G,
+                                                              const bf16_t* __restrict__ gamma,
+                                                              const bf16_t* __restrict__ beta, float eps,
+                                                              float* __restrict__ scale, float* __restrict__ shift) {
+  const int n = blockIdx.x, g = blockIdx.y, lane = threadIdx.x;
+  const int C = C1 + C2, R = HW / 128, Cg = C / G, c0 = g * Cg;
+  double a = 0.0, b = 0.0;
+  for (int e = lane; e < R * Cg; e += 64) {
+    const int r = e / Cg, c = c0 + (e - r * Cg);
+    const float2 v = c < C1 ? *reinterpret_cast<const float2*>(part1 + (((long)n * R + r) * C1 + c) * 2)
+                            : *reinterpret_cast<const float2*>(part2 + (((long)n * R + r) * C2 + (c - C1)) * 2);
+    a += v.x;
+    b += v.y;
   }
-  __syncthreads();
-  const int Cg = C / G;
-  for (int g = threadIdx.x; g < G; g += blockDim.x) {
-    double sa = 0.0, sb = 0.0;
-    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
-      sa += gfp_lds[2 * c];
-      sb += gfp_lds[2 * c + 1];
-    }
-    const double cnt = (double)HW * Cg;
-    const double mean = sa / cnt;
-    double var = sb / cnt - mean * mean;
-    if (var < 0) var = 0;
-    mean_s[g] = (float)mean;
-    rstd_s[g] = (float)(1.0 / sqrt(var + (double)eps));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
   }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const int g = c / Cg;
-    const float sc = rstd_s[g] * (gamma ? bf2f(gamma[c]) : 1.f);
+  const double cnt = (double)HW * Cg;
+  const double mean = a / cnt;
+  double var = b / cnt - mean * mean;
+  if (var < 0) var = 0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps)), m = (float)mean;
+  for (int c = c0 + lane; c < c0 + Cg; c += 64) {
+    const float sc = rstd * (gamma ? bf2f(gamma[c]) : 1.f);
     scale[(long)n * C + c] = sc;
-    shift[(long)n * C + c] = (beta ? bf2f(beta[c]) : 0.f) - mean_s[g] * sc;
+    shift[(long)n * C + c] = (beta ? bf2f(beta[c]) : 0.f) - m * sc;
   }
 }
 
 void launch_gn_from_partials(const float* part1, int C1, const float* part2, int C2, int Nimg, int HW, int G,
                              const bf16_t* gamma, const bf16_t* beta, float eps, float* scale, float* shift,
                              hipStream_t s) {
-  const size_t lds = (size_t)(C1 + C2) * 2 * sizeof(float);
-  gn_from_partials_kernel<<<Nimg, 256, lds, s>>>(part1, C1, part2, C2, HW, G, gamma, beta, eps, scale, shift);
+  gn_from_partials_kernel<<<dim3(Nimg, G), 64, 0, s>>>(part1, C1, part2, C2, HW, G, gamma, beta, eps, scale, shift);
 }
 
 // LayerNorm row moments (mean, rstd) from the per-row partials of a GEMM epilogue: one thread per row

@@ -175,12 +175,17 @@ class Transformer2DModel(nn.Module):
         output out.  Returns (out, partials or None)."""
         B, H, W, C = x.shape
         blocks = list(self.transformer_blocks)
-        h, mr = self.proj_in(self.norm(x, part=xp), stats="ln", eps=blocks[0].norm1.eps)
-        h = h.view(B, H * W, C)
-        if mr is None:
-            mr = ops.row_moments(h, blocks[0].norm1.eps)
-        for i, blk in enumerate(blocks):
-            h, mr = blk.forward_folded(h, ctx_kv, mr, blocks[i + 1].norm1.eps if i + 1 < len(blocks) else None)
+        if ops.fold_profitable(B * H * W, C):  # the Q projection (N = C) has the fewest tiles of the consumers
+            h, mr = self.proj_in(self.norm(x, part=xp), stats="ln", eps=blocks[0].norm1.eps)
+            h = h.view(B, H * W, C)
+            if mr is None:
+                mr = ops.row_moments(h, blocks[0].norm1.eps)
+            for i, blk in enumerate(blocks):
+                h, mr = blk.forward_folded(h, ctx_kv, mr, blocks[i + 1].norm1.eps if i + 1 < len(blocks) else None)
+        else:
+            h = self.proj_in(self.norm(x, part=xp)).view(B, H * W, C)
+            for blk in blocks:
+                h = blk(h, ctx_kv)
         res = x.view(B, H * W, C)
         if stats and ops.stats_supported(B * H * W, C, "gn", H * W):
             out, op = self.proj_out.forward_stats(h, residual=res, stats="gn")

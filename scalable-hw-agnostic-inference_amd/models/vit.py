@@ -139,7 +139,8 @@ class ViTEncoderModel(nn.Module):
         x = torch.cat(toks, dim=1)
         pe = self.pos_embed(gh, gw).expand(B, -1, -1).contiguous()
         x = ops.bias_act(x.contiguous(), None, pe)
-        if NORM_HANDOFF:
+        c = self.cfg
+        if NORM_HANDOFF and ops.fold_profitable(x.shape[0] * x.shape[1], min(3 * c.hidden_size, c.intermediate_size)):
             layers = list(self.layers)
             mr = ops.row_moments(x, layers[0].layernorm_before.eps)
             for i, layer in enumerate(layers):

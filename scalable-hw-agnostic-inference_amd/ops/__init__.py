@@ -258,6 +258,16 @@ def stats_supported(rows: int, cols: int, kind: str, hw: Optional[int] = None) -
     return True
 
 
+def fold_profitable(rows: int, cols: int) -> bool:
+    """A LayerNorm folded into a GEMM pins that GEMM to the v4 kernel (256-row tiles, unsplit): worth it only when
+    the problem has about a wave of 256 x 320 tiles for the 256 CUs -- otherwise the standalone norm pass plus the
+    tuner's choice (smaller tiles, split-K) is faster (SD2.1 at batch 1: 32 tiles)."""
+    return ((rows + 255) // 256) * ((cols + 319) // 320) >= FOLD_MIN_TILES
+
+
+FOLD_MIN_TILES = int(os.environ.get("SHAI_FOLD_MIN_TILES", "192"))  # tests lower it to force the folded path
+
+
 def linear_stats(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act=None, stats: str = "ln",
                  eps: float = 1e-5, row_affine=None, force_cfg: int = -1):
     """``linear`` that also returns statistics of its output for the next norm: stats="ln" -> (mean, rstd) [M, 2]

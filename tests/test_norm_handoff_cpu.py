@@ -59,14 +59,15 @@ def test_unet_norm_handoff_cpu():
     x = torch.randn(2, 16, 16, 4).bfloat16()
     t = torch.tensor([500.0])
     kv = m.context_kv(torch.randn(2, 77, cfg.cross_attention_dim).bfloat16())
-    old = unet2d.NORM_HANDOFF
+    old, old_min = unet2d.NORM_HANDOFF, ops.FOLD_MIN_TILES
     try:
+        ops.FOLD_MIN_TILES = 0  # fold at this small size too
         unet2d.NORM_HANDOFF = True
         y1 = m(x, t, kv)
         unet2d.NORM_HANDOFF = False
         y0 = m(x, t, kv)
     finally:
-        unet2d.NORM_HANDOFF = old
+        unet2d.NORM_HANDOFF, ops.FOLD_MIN_TILES = old, old_min
     assert rel(y1, y0) < 1e-2
 
 
@@ -80,12 +81,13 @@ def test_vit_norm_handoff_cpu():
     for p in m.parameters():
         torch.nn.init.normal_(p, std=0.05)
     px = torch.randn(2, 32, 32, 3).bfloat16()
-    old = vit.NORM_HANDOFF
+    old, old_min = vit.NORM_HANDOFF, ops.FOLD_MIN_TILES
     try:
+        ops.FOLD_MIN_TILES = 0
         vit.NORM_HANDOFF = True
         y1 = m(px)
         vit.NORM_HANDOFF = False
         y0 = m(px)
     finally:
-        vit.NORM_HANDOFF = old
+        vit.NORM_HANDOFF, ops.FOLD_MIN_TILES = old, old_min
     assert rel(y1, y0) < 1e-2

@@ -117,14 +117,15 @@ def test_unet_norm_handoff_matches(cuda):
     x = torch.randn(B, H, H, 4, device="cuda").bfloat16()
     t = torch.tensor([500.0], device="cuda")
     kv = m.context_kv(torch.randn(B, 77, 256, device="cuda").bfloat16())
-    old = unet2d.NORM_HANDOFF
+    old, old_min = unet2d.NORM_HANDOFF, ops.FOLD_MIN_TILES
     try:
+        ops.FOLD_MIN_TILES = 0  # fold at this small size too
         unet2d.NORM_HANDOFF = True
         y1 = m(x, t, kv)
         unet2d.NORM_HANDOFF = False
         y0 = m(x, t, kv)
     finally:
-        unet2d.NORM_HANDOFF = old
+        unet2d.NORM_HANDOFF, ops.FOLD_MIN_TILES = old, old_min
     assert torch.isfinite(y1).all()
     assert rel(y1, y0) < 2e-2
 
@@ -140,13 +141,14 @@ def test_vit_norm_handoff_matches(cuda):
     for p in m.parameters():
         torch.nn.init.normal_(p, std=0.03)
     px = torch.randn(8, 224, 224, 3, device="cuda").bfloat16()
-    old = vit.NORM_HANDOFF
+    old, old_min = vit.NORM_HANDOFF, ops.FOLD_MIN_TILES
     try:
+        ops.FOLD_MIN_TILES = 0
         vit.NORM_HANDOFF = True
         y1 = m(px)
         vit.NORM_HANDOFF = False
         y0 = m(px)
     finally:
-        vit.NORM_HANDOFF = old
+        vit.NORM_HANDOFF, ops.FOLD_MIN_TILES = old, old_min
     assert torch.isfinite(y1).all()
     assert rel(y1, y0) < 2e-2

@@ -10,7 +10,7 @@ mkdir -p gpurun_out
 HB=$!
 trap 'kill $HB 2>/dev/null' EXIT
 for P in 65536 127744; do
-  timeout -k 10 540 python -u -m shai_amd.bench.long_context --model llama31_8b --prompt-len $P --chunk 8192 \
-    --background 16 --gen 128 > gpurun_out/r4c_long_$P.log 2>&1 || { tail -20 gpurun_out/r4c_long_$P.log; exit 1; }
-  tail -1 gpurun_out/r4c_long_$P.log
+  timeout -k 10 500 python -u -m shai_amd.bench.long_context --model llama31_8b --prompt-len $P --chunk 8192 \
+    --background 16 --gen 128 > gpurun_out/r4g_long_$P.log 2>&1 || { tail -20 gpurun_out/r4g_long_$P.log; exit 1; }
+  tail -1 gpurun_out/r4g_long_$P.log
 done
