@@ -548,41 +548,54 @@ void launch_groupnorm_apply(const GroupNormArgs& a, hipStream_t s) {
 // Norm statistics handed from a GEMM epilogue to the next norm (GemmArgs::col_part / row_part, gemm_8ph.hip), and
 // the passes that produce the same statistics when the producing kernel could not (fallbacks).
 
-// col partials [M / 128, N, 2] of x [M, N]: block = 128 rows; 256 threads = P row lanes x N / 8 channel vectors
+// col partials [M / 128, N, 2] of x [M, N]: block = 128 rows x 64 channel vectors (512 channels); 256 threads =
+// 64 vectors x 4 row lanes, each lane 32 rows with 8 independent 16-B loads in flight (batch-1 steps give only a
+// few 128-row blocks, so the per-thread loop must not be latency-bound)
 __global__ void __launch_bounds__(256) col_partials_kernel(const bf16_t* __restrict__ x, long M, int N, long ldx,
                                                            float* __restrict__ part) {
-  __shared__ float4_ red[256][4];  // [thread][sum 0-3, sum 4-7, sq 0-3, sq 4-7]
-  const int C8 = N >> 3, P = 256 / C8, t = threadIdx.x;
-  const int pl = t / C8, cv = t - pl * C8;
-  const long r0 = (long)blockIdx.x * 128, r1 = min(M, r0 + 128);
+  __shared__ float4_ red[4][64][4];  // [row lane][vector][sum 0-3, sum 4-7, sq 0-3, sq 4-7]
+  const int C8 = N >> 3, t = threadIdx.x;
+  const int v = t & 63, rl = t >> 6;
+  const int cv = blockIdx.y * 64 + v;
+  const long r0 = (long)blockIdx.x * 128 + rl * 32;
   float s[8], q[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
-  if (pl < P) {
-    for (long r = r0 + pl; r < r1; r += P) {
-      float f[8];
-      unpack8(*reinterpret_cast<const uint4_*>(x + r * ldx + cv * 8), f);
+  if (cv < C8) {
+    const bf16_t* src = x + r0 * ldx + cv * 8;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        s[e] += f[e];
-        q[e] = fmaf(f[e], f[e], q[e]);
+    for (int r8 = 0; r8 < 32; r8 += 8) {
+      uint4_ u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        u[k] = r0 + r8 + k < M ? *reinterpret_cast<const uint4_*>(src + (long)(r8 + k) * ldx) : uint4_{0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float f[8];
+        unpack8(u[k], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s[e] += f[e];
+          q[e] = fmaf(f[e], f[e], q[e]);
+        }
       }
     }
   }
-  red[t][0] = float4_{s[0], s[1], s[2], s[3]};
-  red[t][1] = float4_{s[4], s[5], s[6], s[7]};
-  red[t][2] = float4_{q[0], q[1], q[2], q[3]};
-  red[t][3] = float4_{q[4], q[5], q[6], q[7]};
+  red[rl][v][0] = float4_{s[0], s[1], s[2], s[3]};
+  red[rl][v][1] = float4_{s[4], s[5], s[6], s[7]};
+  red[rl][v][2] = float4_{q[0], q[1], q[2], q[3]};
+  red[rl][v][3] = float4_{q[4], q[5], q[6], q[7]};
   __syncthreads();
-  if (t < C8) {
-    float4_ a0 = red[t][0], a1 = red[t][1], b0 = red[t][2], b1 = red[t][3];
-    for (int l = 1; l < P; ++l) {
-      a0 += red[l * C8 + t][0];
-      a1 += red[l * C8 + t][1];
-      b0 += red[l * C8 + t][2];
-      b1 += red[l * C8 + t][3];
+  if (rl == 0 && cv < C8) {
+    float4_ a0 = red[0][v][0], a1 = red[0][v][1], b0 = red[0][v][2], b1 = red[0][v][3];
+#pragma unroll
+    for (int l = 1; l < 4; ++l) {
+      a0 += red[l][v][0];
+      a1 += red[l][v][1];
+      b0 += red[l][v][2];
+      b1 += red[l][v][3];
     }
-    float4_* dst = reinterpret_cast<float4_*>(part + ((long)blockIdx.x * N + t * 8) * 2);
+    float4_* dst = reinterpret_cast<float4_*>(part + ((long)blockIdx.x * N + cv * 8) * 2);
     dst[0] = float4_{a0[0], b0[0], a0[1], b0[1]};
     dst[1] = float4_{a0[2], b0[2], a0[3], b0[3]};
     dst[2] = float4_{a1[0], b1[0], a1[1], b1[1]};
@@ -592,7 +605,8 @@ __global__ void __launch_bounds__(256) col_partials_kernel(const bf16_t* __restr
 
 void launch_col_partials(const bf16_t* x, long M, int N, long ldx, float* part, hipStream_t s) {
   if (M <= 0) return;
-  col_partials_kernel<<<(unsigned)((M + 127) / 128), 256, 0, s>>>(x, M, N, ldx, part);
+  const int C8 = N >> 3;
+  col_partials_kernel<<<dim3((unsigned)((M + 127) / 128), (C8 + 63) / 64), 256, 0, s>>>(x, M, N, ldx, part);
 }
 
 // GroupNorm (scale, shift) from the col partials of x (channels [0, C1)) and x2 ([C1, C1 + C2)): one wave per
