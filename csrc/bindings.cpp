@@ -867,6 +867,13 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
     }
     return;
   }
+  if (force_cfg >= 3000 && force_cfg < 4000) {  // tests: tile config (force % 100) with (force - 3000) / 100 K splits
+    const int cfg = (int)((force_cfg - 3000) % 100), splits = (int)((force_cfg - 3000) / 100);
+    SHAI_CHECK(cfg < shai::gemm2_num_cfgs() && shai::gemm2_cfg_supported(g, cfg) && splits >= 1 && !batched,
+               "bad forced split config");
+    launch_choice(g, a, Choice{cfg, splits});
+    return;
+  }
   if (force_cfg == kLibCfg) {  // tests: pin the hipBLASLt path
     SHAI_CHECK(lib_supported(g), "library GEMM path does not support this problem's epilogue");
     launch_lib(g, a);

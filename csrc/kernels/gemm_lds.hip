@@ -44,7 +44,8 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, bf16_t* lds_wav
 }
 
 template <int BM, int BN, int WM, int WN, bool CONV, bool FAST, bool GLU, int ACT, bool SPLITK, int STAGES>
-__global__ void __launch_bounds__(WM * WN * 64) gemm2_kernel(const GemmArgs p, float* __restrict__ ws, int k_per_split) {
+__global__ void __launch_bounds__(WM * WN * 64) gemm2_kernel(const GemmArgs p, float* __restrict__ ws, int k_per_split,
+                                                             unsigned* __restrict__ cnt) {
   constexpr int NW = WM * WN;
   constexpr int NT = NW * 64;
   constexpr int TM = BM / WM, TN = BN / WN;     // wave tile
@@ -249,6 +250,94 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm2_kernel(const GemmArgs p, f
   }
 
   // ---- epilogue: lane owns row m, 4 groups of 4 consecutive n per 32x32 block
+  // In-launch split-K fixup (tiles with <= 4 32x32 blocks per wave; the skinny kernel's write-through hand-off, gemv.hip): every K group
+  // stores its fp32 partial tile write-through (sc1), drains, joins the barrier and takes a ticket; the group
+  // drawing the last one re-arms it, sums the slabs in K-group order (its own from registers, so the sum matches
+  // the separate fold bit for bit whatever the arrival order) and runs the full epilogue.  Batch-1 SD2.1 steps
+  // run most of their GEMMs split-K at these tiles: the fold kernel was 8.7 % of their kernel time.
+  constexpr bool FIXOK = IM * JN <= 4;
+  if constexpr (SPLITK && FIXOK) {
+    if (cnt != nullptr) {
+      __shared__ unsigned g2_last;
+      const int S = gridDim.y;
+      const __amdgpu_buffer_rsrc_t rws = make_rsrc(ws, (uint32_t)min((long)S * p.M * p.N * 4, 0x7fffffffL));
+#pragma unroll
+      for (int i = 0; i < IM; ++i) {
+        const int m = m0 + wm * TM + i * 32 + fr;
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int n = n0 + wn * TN + j * 32 + 8 * g + 4 * fh;
+            const uint32_t off = (uint32_t)(((long)kz * p.M * p.N + (long)m * p.N + n) * 4);
+            if (m < p.M && n + 3 < p.N) {
+              const float4_ v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4_, v), rws, (int)off, 0, 16);
+            } else if (m < p.M) {
+              for (int e = 0; e < 4 && n + e < p.N; ++e)
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][4 * g + e]), rws, (int)(off + 4 * e), 0,
+                                                      16);
+            }
+          }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned old = __hip_atomic_fetch_add(&cnt[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        g2_last = old == (unsigned)(S - 1);
+      }
+      __syncthreads();
+      if (g2_last == 0u) return;
+      if (tid == 0) __hip_atomic_store(&cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int i = 0; i < IM; ++i) {
+        const int m = min(m0 + wm * TM + i * 32 + fr, p.M - 1);
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int n = n0 + wn * TN + j * 32 + 8 * g + 4 * fh;
+            const bool full = n + 3 < p.N;
+            float t[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int q = 0; q < S; ++q) {
+              if (q == kz) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t[e] += acc[i][j][4 * g + e];
+                continue;
+              }
+              const uint32_t off = (uint32_t)(((long)q * p.M * p.N + (long)m * p.N + n) * 4);
+              if (full) {
+                const float4_ v = __builtin_bit_cast(float4_, __builtin_amdgcn_raw_buffer_load_b128(rws, (int)off, 0, 16));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t[e] += v[e];
+              } else {
+                for (int e = 0; e < 4 && n + e < p.N; ++e)
+                  t[e] += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rws, (int)(off + 4 * e), 0, 16));
+              }
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] = t[e];
+          }
+      }
+      bf16_t* C = p.C;
+#pragma unroll
+      for (int i = 0; i < IM; ++i) {
+        const int m = m0 + wm * TM + i * 32 + fr;
+        if (m >= p.M) continue;
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int n = n0 + wn * TN + j * 32 + 8 * g + 4 * fh;
+            if (n >= p.N) continue;
+            float v[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+            epilogue4<GLU, ACT>(p, C, p.residual, m, n, v, 0);
+          }
+      }
+      return;
+    }
+  }
   if constexpr (SPLITK) {
     float* W = ws + (long)kz * p.M * p.N;
 #pragma unroll
@@ -340,15 +429,15 @@ static int g_stages() {
 }
 
 template <int BM, int BN, int WM, int WN, bool CONV, bool FAST, bool GLU, int ACT, bool SPLITK>
-static void launch_cfg(const GemmArgs& a, float* ws, int splits, int kps, hipStream_t s) {
+static void launch_cfg(const GemmArgs& a, float* ws, int splits, int kps, hipStream_t s, unsigned* cnt) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles, SPLITK ? splits : (a.batch > 0 ? a.batch : 1));
   if (g_stages() == 3 && (size_t)3 * (BM + BN) * BK2 * sizeof(bf16_t) <= 160 * 1024) {
     const size_t lds = (size_t)3 * (BM + BN) * BK2 * sizeof(bf16_t);
-    gemm2_kernel<BM, BN, WM, WN, CONV, FAST, GLU, ACT, SPLITK, 3><<<grid, WM * WN * 64, lds, s>>>(a, ws, kps);
+    gemm2_kernel<BM, BN, WM, WN, CONV, FAST, GLU, ACT, SPLITK, 3><<<grid, WM * WN * 64, lds, s>>>(a, ws, kps, cnt);
   } else {
     const size_t lds = (size_t)2 * (BM + BN) * BK2 * sizeof(bf16_t);
-    gemm2_kernel<BM, BN, WM, WN, CONV, FAST, GLU, ACT, SPLITK, 2><<<grid, WM * WN * 64, lds, s>>>(a, ws, kps);
+    gemm2_kernel<BM, BN, WM, WN, CONV, FAST, GLU, ACT, SPLITK, 2><<<grid, WM * WN * 64, lds, s>>>(a, ws, kps, cnt);
   }
 }
 
@@ -372,11 +461,11 @@ constexpr int kW4Cfg = kV4Cfg + 4;
 
 
 template <bool CONV, bool FAST, bool GLU, int ACT>
-static void launch_tiles(const GemmArgs& a, int cfg, float* ws, int splits, int kps, hipStream_t s) {
+static void launch_tiles(const GemmArgs& a, int cfg, float* ws, int splits, int kps, hipStream_t s, unsigned* cnt) {
   const bool sk = splits > 1;
 #define SHAI_CFG(BM_, BN_, WM_, WN_)                                                   \
-  if (sk) launch_cfg<BM_, BN_, WM_, WN_, CONV, FAST, GLU, ACT, true>(a, ws, splits, kps, s); \
-  else launch_cfg<BM_, BN_, WM_, WN_, CONV, FAST, GLU, ACT, false>(a, ws, splits, kps, s);
+  if (sk) launch_cfg<BM_, BN_, WM_, WN_, CONV, FAST, GLU, ACT, true>(a, ws, splits, kps, s, cnt); \
+  else launch_cfg<BM_, BN_, WM_, WN_, CONV, FAST, GLU, ACT, false>(a, ws, splits, kps, s, cnt);
   switch (cfg) {
     case 0: SHAI_CFG(256, 320, 4, 2); break;
     case 1: SHAI_CFG(256, 256, 4, 2); break;
@@ -452,10 +541,22 @@ static void launch_all(const GemmArgs& a, float* ws, int cfg, int splits, hipStr
   if (ws == nullptr) splits = 1;
   const long kt = (a.K + BK2 - 1) / BK2;
   const int kps = (int)(((kt + splits - 1) / splits) * BK2);
+  // split-K at the 64-128-column tiles (cfg 2 / 3 / 4): fixed up inside the launch when a ticket slice is available
+  // (SHAI_G2_FIXUP=0: the separate fold kernel)
+  static const bool fixup_on = [] {
+    const char* e = getenv("SHAI_G2_FIXUP");
+    return !(e && e[0] == '0');
+  }();
+  unsigned* cnt = nullptr;
+  if (splits > 1 && cfg >= 2 && fixup_on && !a.rms && (long)splits * a.M * a.N * 4 < 0x7fffffffL) {
+    const int bm = cfg == 2 ? 256 : 128, bn = cfg == 4 ? 64 : 128;
+    const long tiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+    if (tiles <= 4096) cnt = skinny_ticket_slice(s, (int)tiles);
+  }
 #define SHAI_G2(GLU_, ACT_)                                                   \
   do {                                                                        \
-    launch_tiles<CONV, FAST, GLU_, ACT_>(a, cfg, ws, splits, kps, s);         \
-    if (splits > 1) launch_reduce<GLU_, ACT_>(a, ws, splits, s);              \
+    launch_tiles<CONV, FAST, GLU_, ACT_>(a, cfg, ws, splits, kps, s, cnt);    \
+    if (splits > 1 && cnt == nullptr) launch_reduce<GLU_, ACT_>(a, ws, splits, s); \
   } while (0)
   if constexpr (CONV) {  // convs: no GLU, activation none / silu
     if (a.act == ACT_SILU) SHAI_G2(false, ACT_SILU);

@@ -477,3 +477,22 @@ def test_conv2d_small_spatial_splitk(cuda, cfg):
     temb = rnd(cfg["N"], cfg["Co"])
     close(ops.conv2d(x, w, b, 3, 3, 1, 1, temb=temb, residual=res),
           ref.conv2d(x, w, b, 3, 3, 1, 1, temb=temb, residual=res), 3e-2)
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4])
+@pytest.mark.parametrize("splits", [2, 3, 5])
+@pytest.mark.parametrize("M,N,K,glu", [(512, 1280, 2560, False), (130, 650, 1920, False), (512, 2560, 1280, True)])
+def test_gemm2_splitk_fixup(cuda, cfg, splits, M, N, K, glu):
+    """Split-K at the 64-128-column tiles, fixed up inside the launch (last-arriving K group sums the slabs in
+    K-group order and runs the epilogue): vs fp32, and bit-identical across runs (arrival order does not matter)."""
+    torch.manual_seed(22)
+    x, w, b = rnd(M, K), rnd(N, K, scale=1 / math.sqrt(K)), rnd(N)
+    r = rnd(M, N // 2 if glu else N)
+    force = 3000 + 100 * splits + cfg
+    out1 = torch.empty(M, N // 2 if glu else N, device="cuda", dtype=torch.bfloat16)
+    out2 = torch.empty_like(out1)
+    act = "gelu" if glu else "silu"
+    ops.gemm_into(x, w, out1, b, act=act, residual=r, glu=glu, force_cfg=force)
+    ops.gemm_into(x, w, out2, b, act=act, residual=r, glu=glu, force_cfg=force)
+    close(out1, ref.linear(x, w, b, act, r, glu), 2e-2)
+    assert torch.equal(out1, out2)
