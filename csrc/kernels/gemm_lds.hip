@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm2_kernel(const GemmArgs p, f
   // drawing the last one re-arms it, sums the slabs in K-group order (its own from registers, so the sum matches
   // the separate fold bit for bit whatever the arrival order) and runs the full epilogue.  Batch-1 SD2.1 steps
   // run most of their GEMMs split-K at these tiles: the fold kernel was 8.7 % of their kernel time.
-  constexpr bool FIXOK = IM * JN <= 4;
+  constexpr bool FIXOK = IM * JN <= 4 && !(BM == 128 && BN == 128);
   if constexpr (SPLITK && FIXOK) {
     if (cnt != nullptr) {
       __shared__ unsigned g2_last;
@@ -290,36 +290,58 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm2_kernel(const GemmArgs p, f
       __syncthreads();
       if (g2_last == 0u) return;
       if (tid == 0) __hip_atomic_store(&cnt[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // slabs in rounds of U: every (i, j, g) group's loads of the round are issued before the first add (a
+      // load-add chain per slab and group made the fixup latency-bound); the own slab is re-read and replaced by
+      // the registers, so the sum order is the K-group order
+      float4_ tot[IM][JN][4];
 #pragma unroll
-      for (int i = 0; i < IM; ++i) {
-        const int m = min(m0 + wm * TM + i * 32 + fr, p.M - 1);
+      for (int i = 0; i < IM; ++i)
 #pragma unroll
         for (int j = 0; j < JN; ++j)
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int n = n0 + wn * TN + j * 32 + 8 * g + 4 * fh;
-            const bool full = n + 3 < p.N;
-            float t[4] = {0.f, 0.f, 0.f, 0.f};
-            for (int q = 0; q < S; ++q) {
-              if (q == kz) {
+          for (int g = 0; g < 4; ++g) tot[i][j][g] = float4_{0.f, 0.f, 0.f, 0.f};
+      constexpr int U = IM * JN <= 2 ? 2 : 1;  // slabs per round (registers: U x the tile's accumulators)
+      for (int q0 = 0; q0 < S; q0 += U) {
+        float4_ ld[U][IM][JN][4];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) t[e] += acc[i][j][4 * g + e];
-                continue;
+        for (int u = 0; u < U; ++u) {
+          const int q = min(q0 + u, S - 1);
+#pragma unroll
+          for (int i = 0; i < IM; ++i) {
+            const int m = min(m0 + wm * TM + i * 32 + fr, p.M - 1);
+#pragma unroll
+            for (int j = 0; j < JN; ++j)
+#pragma unroll
+              for (int g = 0; g < 4; ++g) {
+                const int n = min(n0 + wn * TN + j * 32 + 8 * g + 4 * fh, ((p.N - 1) & ~3));
+                const uint32_t off = (uint32_t)(((long)q * p.M * p.N + (long)m * p.N + n) * 4);
+                ld[u][i][j][g] = __builtin_bit_cast(float4_, __builtin_amdgcn_raw_buffer_load_b128(rws, (int)off, 0, 16));
               }
-              const uint32_t off = (uint32_t)(((long)q * p.M * p.N + (long)m * p.N + n) * 4);
-              if (full) {
-                const float4_ v = __builtin_bit_cast(float4_, __builtin_amdgcn_raw_buffer_load_b128(rws, (int)off, 0, 16));
-#pragma unroll
-                for (int e = 0; e < 4; ++e) t[e] += v[e];
-              } else {
-                for (int e = 0; e < 4 && n + e < p.N; ++e)
-                  t[e] += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rws, (int)(off + 4 * e), 0, 16));
-              }
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] = t[e];
           }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int q = q0 + u;
+          if (q >= S) continue;
+#pragma unroll
+          for (int i = 0; i < IM; ++i)
+#pragma unroll
+            for (int j = 0; j < JN; ++j)
+#pragma unroll
+              for (int g = 0; g < 4; ++g) {
+                const float4_ own = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                tot[i][j][g] += q == kz ? own : ld[u][i][j][g];
+              }
+        }
       }
+#pragma unroll
+      for (int i = 0; i < IM; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] = tot[i][j][g][e];
       bf16_t* C = p.C;
 #pragma unroll
       for (int i = 0; i < IM; ++i) {
@@ -541,14 +563,15 @@ static void launch_all(const GemmArgs& a, float* ws, int cfg, int splits, hipStr
   if (ws == nullptr) splits = 1;
   const long kt = (a.K + BK2 - 1) / BK2;
   const int kps = (int)(((kt + splits - 1) / splits) * BK2);
-  // split-K at the 64-128-column tiles (cfg 2 / 3 / 4): fixed up inside the launch when a ticket slice is available
+  // split-K at the 256 x 128 / 128 x 64 tiles (cfg 2 / 4): fixed up inside the launch when a ticket slice is available
   // (SHAI_G2_FIXUP=0: the separate fold kernel)
   static const bool fixup_on = [] {
     const char* e = getenv("SHAI_G2_FIXUP");
     return !(e && e[0] == '0');
   }();
   unsigned* cnt = nullptr;
-  if (splits > 1 && cfg >= 2 && fixup_on && !a.rms && (long)splits * a.M * a.N * 4 < 0x7fffffffL) {
+  // (not at 128 x 128: the fixup's registers would halve that config's occupancy)
+  if (splits > 1 && (cfg == 2 || cfg == 4) && fixup_on && !a.rms && (long)splits * a.M * a.N * 4 < 0x7fffffffL) {
     const int bm = cfg == 2 ? 256 : 128, bn = cfg == 4 ? 64 : 128;
     const long tiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
     if (tiles <= 4096) cnt = skinny_ticket_slice(s, (int)tiles);

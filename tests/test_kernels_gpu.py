@@ -479,7 +479,7 @@ def test_conv2d_small_spatial_splitk(cuda, cfg):
           ref.conv2d(x, w, b, 3, 3, 1, 1, temb=temb, residual=res), 3e-2)
 
 
-@pytest.mark.parametrize("cfg", [2, 3, 4])
+@pytest.mark.parametrize("cfg", [2, 3, 4])  # 3 (128 x 128) keeps the separate fold
 @pytest.mark.parametrize("splits", [2, 3, 5])
 @pytest.mark.parametrize("M,N,K,glu", [(512, 1280, 2560, False), (130, 650, 1920, False), (512, 2560, 1280, True)])
 def test_gemm2_splitk_fixup(cuda, cfg, splits, M, N, K, glu):
