@@ -562,6 +562,14 @@ typedef __bf16 bf16x8d __attribute__((ext_vector_type(8)));
 // instructions per wave per block + one barrier), so HBM latency hides behind the dot products.
 // Per-block buffer descriptors (the cache can exceed 4 GiB) range-check the tail rows past the
 // context: zero-filled, since P = 0 times a never-written NaN pattern would poison P.V.
+// Split count of one sequence of nblk 64-token blocks when the launch has num_splits: at least kDaMinSplitBlocks
+// blocks per split, so that a batch whose factor was raised for one long context (up to 64 splits at 128k) does
+// not give every short sequence 64 mostly-empty workgroups and a 64-way combine.
+constexpr int kDaMinSplitBlocks = 4;
+__device__ __forceinline__ int da_splits(int nblk, int num_splits) {
+  return max(1, min(num_splits, (nblk + kDaMinSplitBlocks - 1) / kDaMinSplitBlocks));
+}
+
 template <int D, int NI>
 __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
   constexpr int CPR = D / 8;
@@ -579,7 +587,11 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
   const bool fused = p.knew != nullptr;
   const int ctx = p.ctx_lens[b] - (fused ? 1 : 0);  // tokens read from the cache
   const int nblk = (ctx + 63) / 64;
-  const int per = (nblk + p.num_splits - 1) / p.num_splits;
+  // this sequence's own split count (da_splits): a short sequence in a batch whose split factor was raised for a
+  // long one uses one split -- its other workgroups leave here, before any load
+  const int nsp = da_splits(nblk, p.num_splits);
+  if (split >= nsp) return;
+  const int per = (nblk + nsp - 1) / nsp;
   const int blk0 = split * per, blk1 = min(nblk, blk0 + per);
 
   // wave w issues instructions j = w + G*t (t < NI) of the block's 2 * 64 * D * 2 / 1024 = NI * G
@@ -624,7 +636,7 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
   if (blk0 < blk1) stage(0, blk0);
   const int rpos = fused ? p.positions[b] : 0;
   // this step's k / v (fused path, last split) loaded now and consumed after the loop, so their latency is hidden
-  const bool new_tok = fused && split == p.num_splits - 1 && p.slots[b] >= 0;
+  const bool new_tok = fused && split == nsp - 1 && p.slots[b] >= 0;
   // QKV fold fused in: element col of this row = bf16(sum of the kg partial slabs (in slab order, as the fold
   // adds them) x the folded RMSNorm scale)
   // This lane's six elements (q halves, k halves, two v) and the row's sum of squares, four slabs per round with
@@ -811,7 +823,7 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
       else vc[dst + lane] = f2bf(vn_one);
     }
   }
-  if (p.num_splits == 1) {  // no split-K: normalise and write the output here (no combine launch)
+  if (nsp == 1) {  // one split: normalise and write the output here (the combine skips this row)
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
     bf16_t* op = p.o + (long)b * p.o_bs + (long)hq * D;
     if constexpr (D == 128) {
@@ -838,18 +850,20 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
 __global__ void decode_combine_kernel(const DecodeAttnArgs p) {
   const int b = blockIdx.x, hq = blockIdx.y;
   const int D = p.D;
+  const int nsp = da_splits((p.ctx_lens[b] - (p.knew != nullptr ? 1 : 0) + 63) / 64, p.num_splits);
+  if (nsp == 1) return;  // written by the attention workgroup itself
   const float* src = p.ws + ((long)b * p.Hq + hq) * p.num_splits * (D + 2);
   float m = -INFINITY;
-  for (int s = 0; s < p.num_splits; ++s) m = fmaxf(m, src[s * (D + 2)]);
+  for (int s = 0; s < nsp; ++s) m = fmaxf(m, src[s * (D + 2)]);
   float l = 0.f;
-  for (int s = 0; s < p.num_splits; ++s) {
+  for (int s = 0; s < nsp; ++s) {
     const float ms = src[s * (D + 2)];
     if (ms != -INFINITY) l += src[s * (D + 2) + 1] * exp2f(ms - m);
   }
   const float inv = l > 0.f ? 1.f / l : 0.f;
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
     float acc = 0.f;
-    for (int s = 0; s < p.num_splits; ++s) {
+    for (int s = 0; s < nsp; ++s) {
       const float ms = src[s * (D + 2)];
       if (ms != -INFINITY) acc += src[s * (D + 2) + 2 + d] * exp2f(ms - m);
     }

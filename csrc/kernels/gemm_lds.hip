@@ -565,9 +565,12 @@ static void launch_all(const GemmArgs& a, float* ws, int cfg, int splits, hipStr
   const int kps = (int)(((kt + splits - 1) / splits) * BK2);
   // split-K at the 256 x 128 / 128 x 64 tiles (cfg 2 / 4): fixed up inside the launch when a ticket slice is available
   // (SHAI_G2_FIXUP=0: the separate fold kernel)
+  // Off by default: measured SLOWER end to end (SD2.1 bs1 p50 406 ms with it vs 356 ms with the fold kernel,
+  // profiles/norm_handoff_round4.md): the write-through slabs and the last arriver's serial sum cost more than
+  // the fold launch they replace.  SHAI_G2_FIXUP=1 enables it (tests force it through the forced-split hook).
   static const bool fixup_on = [] {
     const char* e = getenv("SHAI_G2_FIXUP");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   unsigned* cnt = nullptr;
   // (not at 128 x 128: the fixup's registers would halve that config's occupancy)
