@@ -20,6 +20,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <algorithm>
+
 #include <cstdlib>
 #include <type_traits>
 
@@ -571,18 +573,17 @@ __device__ __forceinline__ int da_splits(int nblk, int num_splits) {
 }
 
 template <int D, int NI>
-__global__ void decode_attn_kernel(const DecodeAttnArgs p) {
+__device__ __forceinline__ void decode_attn_item(const DecodeAttnArgs& p, char* dsm, const int b, const int hk,
+                                                 const int split) {
   constexpr int CPR = D / 8;
   constexpr int RPI = 1024 / (D * 2);           // K/V rows per 1-KB wave DMA instruction
   constexpr int SLOT = 2 * 64 * D;              // bf16 elements per ring slot (K then V)
-  extern __shared__ __attribute__((aligned(16))) char dsm[];
   bf16_t* ring = reinterpret_cast<bf16_t*>(dsm);              // [2][K 64xD swizzled | V 64xD linear]
   float* sQ = reinterpret_cast<float*>(ring + 2 * SLOT);      // [G][D]
   float* sP = sQ + 8 * D;                                     // [G][64]
   const int G = p.Hq / p.Hkv;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x, hk = blockIdx.y, split = blockIdx.z;
   const int hq = hk * G + w;
   const bool fused = p.knew != nullptr;
   const int ctx = p.ctx_lens[b] - (fused ? 1 : 0);  // tokens read from the cache
@@ -847,6 +848,22 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
   }
 }
 
+// Persistent form: a grid of about two workgroups per CU walks the (sequence, KV head, split) items, split
+// fastest, so one long context's 8 x 64 split items land on 512 different workgroups while the empty items of
+// short sequences (da_splits) cost a ctx_lens read each instead of a workgroup launch with 70 KB of LDS: a
+// batch with one 64k-token sequence launched 16,384 workgroups per layer, 97 % of them empty, and the
+// launch / LDS allocation of the empty ones took longer (1.17 ms per layer) than the attention itself.
+template <int D, int NI>
+__global__ void decode_attn_kernel(const DecodeAttnArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  const int total = p.B * p.Hkv * p.num_splits;
+  for (int item = blockIdx.x; item < total; item += gridDim.x) {
+    const int split = item % p.num_splits, r = item / p.num_splits;
+    decode_attn_item<D, NI>(p, dsm, r / p.Hkv, r % p.Hkv, split);
+    __syncthreads();  // the next item restages ring slot 0
+  }
+}
+
 __global__ void decode_combine_kernel(const DecodeAttnArgs p) {
   const int b = blockIdx.x, hq = blockIdx.y;
   const int D = p.D;
@@ -877,7 +894,15 @@ size_t decode_attn_workspace(int B, int Hq, int D, int num_splits) {
 
 void launch_decode_attn(const DecodeAttnArgs& a, hipStream_t s) {
   const int G = a.Hq / a.Hkv;
-  dim3 grid(a.B, a.Hkv, a.num_splits);
+  static const int width = [] {  // two workgroups per CU (70 KB of LDS each)
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+    return 2 * cus;
+  }();
+  const long items = (long)a.B * a.Hkv * a.num_splits;
+  dim3 grid((unsigned)std::min<long>(items, width));
   const size_t lds = (size_t)4 * 64 * a.D * sizeof(bf16_t) + (size_t)8 * a.D * 4 + 8 * 64 * 4;
   // NI = wave DMA instructions per block per wave = (2 * 64 * D * 2 / 1024) / G
 #define DA(D_, NI_) decode_attn_kernel<D_, NI_><<<grid, G * 64, lds, s>>>(a)
