@@ -901,8 +901,15 @@ void launch_decode_attn(const DecodeAttnArgs& a, hipStream_t s) {
       cus = 256;
     return 2 * cus;
   }();
+  // short-context batches (<= 8 splits: every item does work) keep one workgroup per item; the persistent walk is
+  // for the raised split factors of long contexts.  SHAI_DECODE_PERSIST=0 / 1 forces either form (A/B).
+  static const int force = [] {
+    const char* e = getenv("SHAI_DECODE_PERSIST");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
   const long items = (long)a.B * a.Hkv * a.num_splits;
-  dim3 grid((unsigned)std::min<long>(items, width));
+  const bool persist = force >= 0 ? force == 1 : a.num_splits > 8;
+  dim3 grid((unsigned)(persist ? std::min<long>(items, width) : items));
   const size_t lds = (size_t)4 * 64 * a.D * sizeof(bf16_t) + (size_t)8 * a.D * 4 + 8 * 64 * 4;
   // NI = wave DMA instructions per block per wave = (2 * 64 * D * 2 / 1024) / G
 #define DA(D_, NI_) decode_attn_kernel<D_, NI_><<<grid, G * 64, lds, s>>>(a)
