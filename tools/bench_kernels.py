@@ -245,6 +245,42 @@ def bench_dattn(rows):
         rows.append(r)
 
 
+def bench_dattn_long(rows):
+    """Decode attention over one 128k-token context (plus 16 short sequences beside it), block tables contiguous
+    vs scattered over a 4 GB-per-tensor pool, per split count: is the KV walk bound by page scatter (TLB) or by
+    the per-workgroup block loop?"""
+    h, hk, D = 32, 8, 128
+    ctx = 131072
+    nblk = ctx // 64
+    pool = 32768
+    kc = rnd(pool, hk, 64, D)
+    vc = rnd(pool, hk, 64, D)
+    cos, sin = torch.rand(ctx + 1, D // 2, device="cuda"), torch.rand(ctx + 1, D // 2, device="cuda")
+    gb = hk * (ctx - 1) * D * 2 * 2 / 1e9
+    for layout in ("contiguous", "scattered"):
+        long_ids = (torch.arange(nblk, device="cuda") if layout == "contiguous"
+                    else torch.randperm(pool, device="cuda")[:nblk])
+        for B in (1, 17):
+            bt = torch.zeros(B, nblk, dtype=torch.int32, device="cuda")
+            bt[0] = long_ids.int()
+            ctx_l = torch.full((B,), 256, device="cuda", dtype=torch.int32)
+            ctx_l[0] = ctx
+            for i in range(1, B):
+                bt[i, :4] = torch.arange(pool - 4 * i, pool - 4 * i + 4, device="cuda").int()
+            pos = ctx_l - 1
+            slots = torch.stack([bt[i, (int(ctx_l[i]) - 1) // 64] * 64 + (int(ctx_l[i]) - 1) % 64
+                                 for i in range(B)]).int()
+            qkv = rnd(B, (h + 2 * hk) * D)
+            r = dict(op="decode_attn_long", shape=f"B{B} ctx{ctx} {layout}")
+            for sp in (16, 32, 64):
+                t = timeit(lambda: ops.decode_attention_rope(qkv, kc, vc, bt, ctx_l, pos, cos, sin, slots, h, hk,
+                                                             num_splits=sp), iters=20)
+                r[f"s{sp}_us"] = t * 1e6
+            best = min(v for k, v in r.items() if k.endswith("_us"))
+            r["best_GBps"] = gb / (best / 1e6)
+            rows.append(r)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="gemm,conv,attn,norm")
@@ -255,7 +291,7 @@ def main():
         for name in a.only.split(","):
             {"gemm": bench_gemm, "conv": bench_conv, "attn": bench_attn, "norm": bench_norm,
              "decode": bench_decode, "decode_fp8": bench_decode_fp8, "sdgemm": bench_sdgemm, "f8": bench_f8,
-             "dattn": bench_dattn}[name](rows)
+             "dattn": bench_dattn, "dattn_long": bench_dattn_long}[name](rows)
     for r in rows:
         print("  ".join(f"{k}={v:.1f}" if isinstance(v, float) else f"{k}={v}" for k, v in r.items()), flush=True)
     if a.json:
