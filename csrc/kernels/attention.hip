@@ -858,13 +858,14 @@ __global__ void decode_attn_kernel(const DecodeAttnArgs p) {
   extern __shared__ __attribute__((aligned(16))) char dsm[];
   const int total = p.B * p.Hkv * p.num_splits;
   const int S = p.num_splits;
+  const bool rotate = (int)gridDim.x < total;  // persistent walk only (one workgroup per item needs no spreading)
   for (int item = blockIdx.x; item < total; item += gridDim.x) {
     // a sequence's splits sit at slots rotated by b: a short sequence's one real item lands on slot b % S instead
     // of slot 0, so the short sequences' items spread over the grid instead of piling onto the few workgroups
     // whose stride hits slot 0 (measured: 16 short sequences beside a 128k one made the launch 2.7x slower)
     const int sidx = item % S, r = item / S;
     const int b = r / p.Hkv, hk = r - b * p.Hkv;
-    const int split = (sidx - b % S + S) % S;
+    const int split = rotate ? (sidx - b % S + S) % S : sidx;
     decode_attn_item<D, NI>(p, dsm, b, hk, split);
     __syncthreads();  // the next item restages ring slot 0
   }
