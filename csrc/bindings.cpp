@@ -61,7 +61,8 @@ std::string gemm_key(const shai::GemmArgs& g) {
            g.Nimg, g.H, g.Wd, g.Cin, g.Cin1, g.KH, g.stride, g.upsample, g.A2 != nullptr);
   // library-eligible problems (plain GEMM, bias at most) race hipBLASLt in the tuner, so their winner must
   // not be reused by a same-shape problem with a fused epilogue (and vice versa): separate key class
-  return std::string(buf) + (g.rms ? "|rms" : "") + (g.w_scale ? "|fp8w" : "") +
+  // a folded-LayerNorm GEMM (row_mr) runs only unsplit on v4: it tunes and caches apart from the plain problem
+  return std::string(buf) + (g.rms ? "|rms" : "") + (g.w_scale ? "|fp8w" : "") + (g.row_mr ? "|ln" : "") +
          (lib_supported(g) && !g.residual ? "|lib" : "");
 }
 
@@ -155,12 +156,14 @@ constexpr int kSkinny2DeepCfg = 1250;
 inline bool is_skinny2(int cfg) { return cfg == kSkinny2Cfg || cfg == kSkinny2DeepCfg; }
 inline bool is_skinny(int cfg) { return cfg == kSkinnyCfg || cfg == kSkinnyFixCfg || is_skinny2(cfg); }
 
-// Last resort when neither the tuner nor the planner produced a usable config: the highest-numbered
-// config that supports the problem (the v2 128x64 tile supports everything v2 runs).
+// Last resort when neither the tuner nor the planner produced a usable config: an explicit, directly tested
+// config, never "whichever kernel happens to be numbered highest".  The v2 128x64 tile (cfg 4) runs every
+// problem the v2 kernel accepts; folded-LayerNorm problems (row_mr) are applied only by the v4 epilogue
+// (cfg 9 / 10, 256 x 256 / 256 x 320).  tests/test_gemm3_gpu.py forces each of these.
 Choice fallback_choice(const shai::GemmArgs& g) {
-  for (int c = shai::gemm2_num_cfgs() - 1; c >= 0; --c)
+  for (int c : {4, 9, 10})
     if (shai::gemm2_cfg_supported(g, c)) return Choice{c, 1};
-  return Choice{0, 1};
+  return Choice{4, 1};
 }
 
 bool stream_capturing() {

@@ -93,6 +93,7 @@ struct Epi {
   const uint4* gate = nullptr;
   int gate_ld8 = 0;
   int rows_per_gate = 1;
+  int row0 = 0;           // first message row's index in the gate's row space (a row slab of a larger output)
 };
 
 __device__ __forceinline__ void add_bf16x8(float acc[8], uint4 v) {
@@ -108,7 +109,7 @@ __device__ __forceinline__ void apply_epi(const Epi& E, long i, float acc[8]) {
   const int row = (int)i / E.ncols8, c8 = (int)i - row * E.ncols8;  // i < 2^31: the slot is <= 16 MiB
   if (E.bias) add_bf16x8(acc, E.bias[c8]);
   if (E.gate) {
-    const uint4 g = E.gate[(long)(row / E.rows_per_gate) * E.gate_ld8 + c8];
+    const uint4 g = E.gate[(long)((E.row0 + row) / E.rows_per_gate) * E.gate_ld8 + c8];
     const uint32_t w[4] = {g.x, g.y, g.z, g.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -123,9 +124,10 @@ __device__ __forceinline__ uint4 pack_bf16x8(const float acc[8]);
 
 // STAGED: the input already sits in this rank's slot A (the row-parallel GEMM wrote its partial there), so the
 // copy of step 1 is skipped; the slot is never rewritten before every peer is past this call's end barrier.
+// off: byte offset of the message inside every rank's slot (a row slab of a staged output; 0 otherwise).
 template <bool STAGED>
 __global__ void __launch_bounds__(512) p2p_one_shot(Peers P, int rank, int world, const uint4* in,
-                                                    uint4* out, long n16, Epi E) {
+                                                    uint4* out, long n16, Epi E, size_t off) {
   __shared__ uint32_t s_epoch;
   Layout* me = reinterpret_cast<Layout*>(P.base[rank]);
   if (threadIdx.x == 0) {
@@ -135,7 +137,7 @@ __global__ void __launch_bounds__(512) p2p_one_shot(Peers P, int rank, int world
   }
   __syncthreads();
   const uint32_t epoch = s_epoch;
-  uint4* mine = reinterpret_cast<uint4*>(P.base[rank] + kDataOff);
+  uint4* mine = reinterpret_cast<uint4*>(P.base[rank] + kDataOff + off);
   const long stride = (long)gridDim.x * blockDim.x;
   if (!STAGED) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) mine[i] = in[i];
@@ -146,7 +148,7 @@ __global__ void __launch_bounds__(512) p2p_one_shot(Peers P, int rank, int world
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int r = 0; r < world; ++r) {
-      const uint4 v = r == rank ? mine[i] : peer_load16(peer_rsrc(P.base[r] + kDataOff, n16 * 16), i);
+      const uint4 v = r == rank ? mine[i] : peer_load16(peer_rsrc(P.base[r] + kDataOff + off, n16 * 16), i);
       add_bf16x8(acc, v);
     }
     apply_epi(E, i, acc);
@@ -181,7 +183,7 @@ __device__ __forceinline__ uint4 pack_bf16x8(const float acc[8]) {
 // segment's owner in phase 1, so every element gets it exactly once and phase 2 gathers final values.
 template <bool STAGED>
 __global__ void __launch_bounds__(512) p2p_two_shot(Peers P, int rank, int world, const uint4* in, uint4* out,
-                                                    long n16, size_t slot_bytes, Epi E) {
+                                                    long n16, size_t slot_bytes, Epi E, size_t off) {
   __shared__ uint32_t s_epoch;
   Layout* me = reinterpret_cast<Layout*>(P.base[rank]);
   if (threadIdx.x == 0) {
@@ -194,8 +196,8 @@ __global__ void __launch_bounds__(512) p2p_two_shot(Peers P, int rank, int world
   const long seg = (n16 + world - 1) / world;
   const long stride = (long)gridDim.x * blockDim.x;
   const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  uint4* slotA = reinterpret_cast<uint4*>(P.base[rank] + kDataOff);
-  uint4* slotB = reinterpret_cast<uint4*>(P.base[rank] + kDataOff + slot_bytes);
+  uint4* slotA = reinterpret_cast<uint4*>(P.base[rank] + kDataOff + off);
+  uint4* slotB = reinterpret_cast<uint4*>(P.base[rank] + kDataOff + slot_bytes + off);
   if (!STAGED) {
     for (int s = 0; s < world; ++s) {
       const long beg = s * seg, end = min(n16, beg + seg);
@@ -211,7 +213,7 @@ __global__ void __launch_bounds__(512) p2p_two_shot(Peers P, int rank, int world
       float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int r = 0; r < world; ++r) {
         const int src = (rank + r) % world;  // stagger the peers so the links are loaded evenly
-        const uint4 v = src == rank ? slotA[i] : peer_load16(peer_rsrc(P.base[src] + kDataOff, n16 * 16), i);
+        const uint4 v = src == rank ? slotA[i] : peer_load16(peer_rsrc(P.base[src] + kDataOff + off, n16 * 16), i);
         add_bf16x8(acc, v);
       }
       apply_epi(E, i, acc);
@@ -227,7 +229,7 @@ __global__ void __launch_bounds__(512) p2p_two_shot(Peers P, int rank, int world
     if (s == rank) {
       for (long i = beg + t0; i < end; i += stride) out[i] = slotB[i];
     } else {
-      const __amdgpu_buffer_rsrc_t rb = peer_rsrc(P.base[s] + kDataOff + slot_bytes, n16 * 16);
+      const __amdgpu_buffer_rsrc_t rb = peer_rsrc(P.base[s] + kDataOff + slot_bytes + off, n16 * 16);
       for (long i = beg + t0; i < end; i += stride) out[i] = peer_load16(rb, i);
     }
   }
@@ -358,7 +360,7 @@ int shai_p2p_allreduce_bf16(void* ctx, const void* in, void* out, size_t bytes, 
   if (blocks < 1) blocks = 1;
   // every rank must use the same grid: it is a function of bytes only
   hipLaunchKernelGGL(p2p_one_shot<false>, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world,
-                     static_cast<const uint4*>(in), static_cast<uint4*>(out), n16, Epi{nullptr, nullptr, 1});
+                     static_cast<const uint4*>(in), static_cast<uint4*>(out), n16, Epi{nullptr, nullptr, 1}, (size_t)0);
   ++c->launches[0];
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
@@ -374,7 +376,7 @@ int shai_p2p_allreduce2_bf16(void* ctx, const void* in, void* out, size_t bytes,
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(p2p_two_shot<false>, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world,
                      static_cast<const uint4*>(in), static_cast<uint4*>(out), n16, c->max_bytes,
-                     Epi{nullptr, nullptr, 1});
+                     Epi{nullptr, nullptr, 1}, (size_t)0);
   ++c->launches[1];
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
@@ -387,15 +389,19 @@ void* shai_p2p_staging(void* ctx, size_t* bytes) {
   return c->local + kDataOff;
 }
 
-// out[rows, ncols] = residual + gate[row / rows_per_gate] * (sum over ranks of every rank's staged partial + bias)
-// (bytes = rows * ncols * 2 at the start of slot A; bias / residual / gate optional, gate row stride gate_ld
-// elements; out may be the residual itself), bf16, fp32 accumulation.  two_shot selects
+// out[rows, ncols] = residual + gate[(row0 + row) / rows_per_gate] * (sum over ranks of every rank's staged
+// partial + bias) for the `bytes` = rows * ncols * 2 message at byte offset `slot_off` of slot A (a row slab of a
+// larger staged output: a row-parallel GEMM split into slabs reduces slab i while slab i + 1 is computed; every
+// slab is its own collective, issued in the same order on every rank).  bias / residual / gate optional, gate row
+// stride gate_ld elements; out may be the residual itself; bf16, fp32 accumulation.  two_shot selects
 // reduce-scatter + all-gather (mid-size messages) over one-shot.  Every rank must pass the same bytes / ncols /
-// two_shot.  0 on success.
-int shai_p2p_allreduce_staged(void* ctx, void* out, size_t bytes, int ncols, const void* bias, const void* residual,
-                              const void* gate, int gate_ld, int rows_per_gate, int two_shot, hipStream_t stream) {
+// slot_off / two_shot.  0 on success.
+int shai_p2p_allreduce_staged_at(void* ctx, void* out, size_t bytes, int ncols, const void* bias,
+                                 const void* residual, const void* gate, int gate_ld, int rows_per_gate, int row0,
+                                 size_t slot_off, int two_shot, hipStream_t stream) {
   Ctx* c = static_cast<Ctx*>(ctx);
-  if (bytes % 16 != 0 || bytes > c->max_bytes || ncols <= 0 || ncols % 8 != 0 || (bytes / 2) % ncols != 0)
+  if (bytes % 16 != 0 || slot_off % 16 != 0 || slot_off + bytes > c->max_bytes || ncols <= 0 || ncols % 8 != 0 ||
+      (bytes / 2) % ncols != 0 || row0 < 0)
     return -1;
   if ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(residual) |
        reinterpret_cast<uintptr_t>(gate)) & 15)
@@ -406,7 +412,8 @@ int shai_p2p_allreduce_staged(void* ctx, void* out, size_t bytes, int ncols, con
   E.gate = static_cast<const uint4*>(gate);
   E.gate_ld8 = gate_ld / 8;
   E.rows_per_gate = rows_per_gate;
-  const uint4* in = reinterpret_cast<const uint4*>(c->local + kDataOff);
+  E.row0 = row0;
+  const uint4* in = reinterpret_cast<const uint4*>(c->local + kDataOff + slot_off);
   int blocks;
   if (two_shot) {
     blocks = (int)(((n16 + c->world - 1) / c->world + 511) / 512);
@@ -417,14 +424,21 @@ int shai_p2p_allreduce_staged(void* ctx, void* out, size_t bytes, int ncols, con
   if (blocks < 1) blocks = 1;
   if (two_shot) {
     hipLaunchKernelGGL(p2p_two_shot<true>, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world, in,
-                       static_cast<uint4*>(out), n16, c->max_bytes, E);
+                       static_cast<uint4*>(out), n16, c->max_bytes, E, slot_off);
     ++c->launches[3];
   } else {
     hipLaunchKernelGGL(p2p_one_shot<true>, dim3(blocks), dim3(512), 0, stream, c->peers, c->rank, c->world, in,
-                       static_cast<uint4*>(out), n16, E);
+                       static_cast<uint4*>(out), n16, E, slot_off);
     ++c->launches[2];
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// The whole message at the start of slot A (row0 = 0).
+int shai_p2p_allreduce_staged(void* ctx, void* out, size_t bytes, int ncols, const void* bias, const void* residual,
+                              const void* gate, int gate_ld, int rows_per_gate, int two_shot, hipStream_t stream) {
+  return shai_p2p_allreduce_staged_at(ctx, out, bytes, ncols, bias, residual, gate, gate_ld, rows_per_gate, 0, 0,
+                                      two_shot, stream);
 }
 
 // Host-side launch counts (captured launches count once): [one-shot, two-shot, staged one-shot, staged two-shot,

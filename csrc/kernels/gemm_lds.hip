@@ -480,6 +480,9 @@ constexpr int kV4Cfg = kNumCfgs + 4;
 // kV4Cfg + 4 / + 5: the four-wave kernel (gemm_w4.hip) with 256 x 256 / 192 x 320 tiles (128 x 128 / 96 x 160
 // wave tiles; plain GEMM, GLU, conv; no split-K).
 constexpr int kW4Cfg = kV4Cfg + 4;
+// kW4Cfg + 2: the W-stationary low-K kernel (gemm_ws.hip): K = 320, N a multiple of 320, weights resident in VGPRs,
+// persistent over M (plain / bias / act / GLU / residual / folded LayerNorm; no split-K).
+constexpr int kWsCfg = kW4Cfg + 2;
 
 
 template <bool CONV, bool FAST, bool GLU, int ACT>
@@ -605,6 +608,10 @@ static void launch_all(const GemmArgs& a, float* ws, int cfg, int splits, hipStr
 }
 
 void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStream_t s) {
+  if (cfg == kWsCfg) {  // whole K resident: a split-K choice is run unsplit
+    launch_gemm_ws(a, s);
+    return;
+  }
   if (cfg == kW4Cfg || cfg == kW4Cfg + 1) {  // whole K per tile: a split-K choice is run unsplit
     launch_gemm_w4(a, cfg == kW4Cfg ? 256 : 320, s);
     return;
@@ -646,13 +653,15 @@ void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipS
   }
 }
 
-int gemm2_num_cfgs() { return kW4Cfg + 2; }
+int gemm2_num_cfgs() { return kWsCfg + 1; }
 
-bool gemm2_cfg_splittable(int cfg) { return cfg != kW4Cfg && cfg != kW4Cfg + 1; }
+bool gemm2_cfg_splittable(int cfg) { return cfg != kW4Cfg && cfg != kW4Cfg + 1 && cfg != kWsCfg; }
 
 bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
   // folded LayerNorm (row_mr): only the v4 kernel's epilogue applies it, and only unsplit, batch 1
-  if (a.row_mr != nullptr) return cfg >= kV4Cfg && cfg < kV4Cfg + 4 && a.batch <= 1 && gemm4_supported(a);
+  if (a.row_mr != nullptr)
+    return cfg == kWsCfg ? gemm_ws_supported(a) : cfg >= kV4Cfg && cfg < kV4Cfg + 4 && a.batch <= 1 && gemm4_supported(a);
+  if (cfg == kWsCfg) return gemm_ws_supported(a);
   if (cfg == kW4Cfg) return gemm_w4_supported(a);
   if (cfg == kW4Cfg + 1) return false;  // 192 x 320 four-wave tile: lab only (gemm_w4.hip launch_gemm_w4)
   if (cfg >= kV4Cfg) return cfg < kV4Cfg + 4 && gemm4_supported(a);
@@ -663,6 +672,11 @@ bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
 }
 
 void gemm2_cfg_info(int cfg, int* bm, int* bn) {
+  if (cfg == kWsCfg) {  // W-stationary kernel: reported as "1x-320"
+    *bm = 1;
+    *bn = -320;
+    return;
+  }
   if (cfg == kW4Cfg || cfg == kW4Cfg + 1) {  // four-wave kernel: reported as "4x-256" / "4x-320"
     *bm = 4;
     *bn = cfg == kW4Cfg ? -256 : -320;

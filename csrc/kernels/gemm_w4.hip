@@ -409,6 +409,7 @@ bool gemm_w4_supported(const GemmArgs& a) {
   if ((long)a.N * a.ldw * 2 >= 0x7fffffffL) return false;
   if (a.conv) {
     if (a.Cin % 64 != 0 || (a.A2 != nullptr && a.Cin1 % 64 != 0)) return false;
+    if (a.act != ACT_NONE && a.act != ACT_SILU) return false;  // the conv branch instantiates these two only
     return (long)a.Nimg * a.H * a.Wd * a.Cin * 2 < 0x7fffffffL;
   }
   return a.A2 == nullptr && (long)a.M * a.lda * 2 < 0x7fffffffL;

@@ -163,6 +163,9 @@ bool gemm2_cfg_splittable(int cfg);  // false: the config always runs the whole 
 // v5: four-wave GEMM / implicit-GEMM conv (gemm_w4.hip), bn = 256: 256 x 256 tiles, bn = 320: 192 x 320 tiles
 bool gemm_w4_supported(const GemmArgs& a);
 void launch_gemm_w4(const GemmArgs& a, int bn, hipStream_t s);
+// v6: W-stationary low-K GEMM (gemm_ws.hip): K = 320, N % 320 == 0, persistent over M, weights in VGPRs
+bool gemm_ws_supported(const GemmArgs& a);
+void launch_gemm_ws(const GemmArgs& a, hipStream_t s);
 // v3: pipelined 256x256 LDS-DMA GEMM / conv (gemm_pipe.hip); config index gemm2_num_cfgs() - 1
 bool gemm3_supported(const GemmArgs& a);
 void launch_gemm3(const GemmArgs& a, float* ws, int splits, int stages, hipStream_t s, int bn = 256);

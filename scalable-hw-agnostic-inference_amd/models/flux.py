@@ -162,8 +162,11 @@ def _gated_out(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], resi
     if tp().size == 1:
         ops.gemm_into(x, w, residual, b, residual=residual, gate=gate, rows_per_gate=rows)
         return
-    # xGMI P2P: GEMM into the IPC staging slot, then one kernel reduces and applies the gated residual in place
-    if comm.row_parallel_reduce(x, w, b, residual, gate=gate, rows_per_gate=rows, out=residual) is not None:
+    # xGMI P2P: GEMM into the IPC staging slot (row slabs, each reduced beside the next slab's GEMM), then one kernel
+    # per slab reduces and applies the gated residual in place
+    nrows = x.numel() // x.shape[-1]
+    if comm.row_parallel_reduce(x, w, b, residual, gate=gate, rows_per_gate=rows, out=residual,
+                                chunks=comm.overlap_chunks(nrows)) is not None:
         return
     y = ops.linear(x, w, None)
     comm.all_reduce(y)

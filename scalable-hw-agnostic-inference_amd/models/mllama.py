@@ -187,9 +187,10 @@ def _attn_any_head_dim(q, k, v, scale):
 
 
 class VisionAttention(nn.Module):
-    """Head-sharded at TP > 1 (the reference serves the whole model at TP32, cova/mllama-32-11b-vllm-trn1-
-    config.yaml:9): fused QKV column-parallel by heads, o_proj row-parallel with the residual added after the
-    reduction -- each rank runs attention for its own heads over all tiles."""
+    """Head-sharded at TP > 1 (the reference serves the whole model under vLLM TP32,
+    cova/mllama-32-11b-vllm-trn1-config.yaml:9; here the vision tower's 16 heads shard over TP <= 16): fused QKV
+    column-parallel by heads, o_proj row-parallel with the residual added after the reduction -- each rank runs
+    attention for its own heads over all tiles."""
 
     def __init__(self, c: MllamaVisionConfig):
         super().__init__()
@@ -254,6 +255,10 @@ class VisionLayer(nn.Module):
 
 
 class MllamaVisionModel(nn.Module):
+    # ``quantization: fp8`` quantises the language model only: the vision tower's prefill-sized GEMMs stay bf16
+    # (parallel.layers.quantize_fp8_ skips every linear under a ``no_fp8`` module)
+    no_fp8 = True
+
     def __init__(self, c: MllamaVisionConfig):
         super().__init__()
         self.cfg = c

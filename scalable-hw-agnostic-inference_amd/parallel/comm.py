@@ -16,7 +16,8 @@ and capturable in HIP graphs.  Two transports:
   ``SHAI_P2P_MAX_BYTES`` (32 MiB, the staging capacity), RCCL above; a one-shot all-gather for vocab-parallel logits.
   A row-parallel layer (:func:`row_parallel_reduce`) writes its GEMM partial
   straight into this rank's IPC staging slot and one fused kernel reduces it and
-  adds the bias and the residual (no staging copy, no separate residual launch).
+  adds the bias and the residual (no staging copy, no separate residual launch);
+  large outputs are split into row slabs whose reduces overlap the next slab's GEMM.
   A peer that never arrives sets an error word the engines poll after every step
   (:func:`raise_if_p2p_error`).
 
@@ -75,9 +76,12 @@ def all_reduce(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> to
     return x
 
 
-# Row-parallel compute/communication overlap: a RowParallel GEMM with at least
-# OVERLAP_MIN_ROWS rows is split into OVERLAP_CHUNKS row chunks; chunk i's all-reduce runs on a side stream
-# while chunk i+1's GEMM runs on the compute stream (a fork / join of events, so it is HIP-graph capturable).
+# Row-parallel output stage: fused AND overlapped.  A RowParallel GEMM with at least
+# OVERLAP_MIN_ROWS rows is split into OVERLAP_CHUNKS row slabs; slab i's GEMM writes its partial product into its own
+# region of this rank's IPC staging slot, and slab i's staged reduce (one-shot or two-shot by slab size, with the
+# bias / AdaLN gate / residual epilogue fused) runs on a side stream while slab i + 1's GEMM runs on the compute
+# stream.  Fork / join by events, so it is HIP-graph capturable; every slab is its own collective, issued in the
+# same order on every rank.
 OVERLAP_CHUNKS = int(os.environ.get("SHAI_TP_OVERLAP_CHUNKS", "2"))
 OVERLAP_MIN_ROWS = int(os.environ.get("SHAI_TP_OVERLAP_MIN_ROWS", "1024"))
 _SIDE: dict = {}
@@ -91,71 +95,104 @@ def _side_stream(device: torch.device) -> "torch.cuda.Stream":
 
 
 def overlap_chunks(rows: int) -> int:
-    """How many row chunks a row-parallel GEMM of ``rows`` rows is split into (1: no overlap)."""
+    """How many row slabs a row-parallel GEMM of ``rows`` rows is split into (1: no overlap)."""
     if tp().size == 1 or OVERLAP_CHUNKS <= 1 or rows < OVERLAP_MIN_ROWS:
         return 1
     return max(1, min(OVERLAP_CHUNKS, rows))
 
 
-def all_reduce_overlapped(x2d: torch.Tensor, gemm_chunk, out: torch.Tensor, chunks: int,
-                          group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
-    """out[r0:r1] = sum over the TP group of gemm_chunk(x2d[r0:r1], out[r0:r1]) for ``chunks`` row chunks.
+def row_slabs(rows: int, chunks: int):
+    """[(r0, r1), ...]: the row slabs of a ``chunks``-way split (equal slabs, the last one ragged)."""
+    chunks = max(1, min(chunks, rows))
+    step = (rows + chunks - 1) // chunks
+    return [(r, min(rows, r + step)) for r in range(0, rows, step)]
 
-    GPU: the GEMMs run in order on the current stream; after each, an event forks the chunk's all-reduce onto a
-    side stream (RCCL or the xGMI P2P kernel, both stream-ordered), so chunk i's collective overlaps chunk
-    i+1's GEMM; the current stream joins the side stream at the end.  CPU (gloo): the same chunking, serially."""
-    M = x2d.shape[0]
-    step = (M + chunks - 1) // chunks
-    bounds = [(r, min(M, r + step)) for r in range(0, M, step)]
-    if not x2d.is_cuda:
-        for r0, r1 in bounds:
-            gemm_chunk(x2d[r0:r1], out[r0:r1])
-            all_reduce(out[r0:r1], group)
-        return out
-    cur = torch.cuda.current_stream(x2d.device)
-    side = _side_stream(x2d.device)
-    side.wait_stream(cur)   # the output buffer / inputs are ready before the side stream touches them
-    for r0, r1 in bounds:
-        gemm_chunk(x2d[r0:r1], out[r0:r1])
-        ev = torch.cuda.Event()
-        ev.record(cur)
-        side.wait_event(ev)
-        with torch.cuda.stream(side):
-            all_reduce(out[r0:r1], group)
-    cur.wait_stream(side)
-    return out
+
+def _epilogue_rows(y: torch.Tensor, out: torch.Tensor, bias, residual, gate, rows_per_gate: int, row0: int) -> None:
+    """out = residual + gate[(row0 + r) // rows_per_gate] * (y + bias) for a slab of rows (host reference of the
+    fused staged-reduce epilogue, p2p_allreduce.hip apply_epi)."""
+    v = y.float()
+    if bias is not None:
+        v = v + bias.float()
+    if gate is not None:
+        idx = torch.div(torch.arange(row0, row0 + y.shape[0], device=y.device), rows_per_gate, rounding_mode="floor")
+        v = v * gate[idx, : y.shape[1]].float()
+    if residual is not None:
+        v = v + residual.float()
+    out.copy_(v.to(out.dtype))
+
+
+def _al16(t: Optional[torch.Tensor]) -> bool:
+    return t is None or t.data_ptr() % 16 == 0
 
 
 def row_parallel_reduce(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
                         residual: Optional[torch.Tensor], w_scale: Optional[torch.Tensor] = None,
                         gate: Optional[torch.Tensor] = None, rows_per_gate: int = 1,
-                        out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
-    """Fused output stage of a row-parallel layer on the xGMI P2P path: the GEMM writes this rank's partial
-    product ([..., N], x's leading shape) straight into the IPC staging slot, then ONE kernel sums every rank's
-    slot (one-shot or two-shot by size) and applies ``residual + gate * (sum + bias)`` -- the TP=1 epilogue
-    fusion kept at TP > 1 (``out`` may be ``residual``: the in-place gated update of the Flux blocks).
-    Returns None when the message does not qualify (no P2P, too large, fp8 prefill, odd widths, strided
-    tensors); the caller then takes the generic GEMM -> all_reduce -> epilogue path."""
-    p = _P2P
-    if p is None or not P2P_STAGED or not x.is_cuda or x.dtype != torch.bfloat16:
-        return None
+                        out: Optional[torch.Tensor] = None, chunks: int = 1) -> Optional[torch.Tensor]:
+    """Fused output stage of a row-parallel layer: out = residual + gate[row // rows_per_gate] * (sum over the TP
+    group of x @ weight^T + bias), ``out`` may be ``residual`` (the in-place gated update of the Flux blocks).
+
+    xGMI P2P (GPU): the GEMM writes this rank's partial product ([..., N], x's leading shape) straight into the IPC
+    staging slot and ONE kernel per slab sums every rank's slot region (one-shot or two-shot by size) and applies
+    the epilogue; with ``chunks`` > 1 the slabs' reduces overlap the next slabs' GEMMs (side stream).  CPU (gloo):
+    the same slab schedule with an all-reduce per slab and the epilogue in torch.  Returns None when the message
+    does not qualify (no P2P, too large, fp8 prefill, odd widths, strided or unaligned tensors); the caller then
+    takes the generic GEMM -> all_reduce -> epilogue path."""
     n = weight.shape[0]
     rows = x.numel() // x.shape[-1]
+    x2 = x.reshape(rows, x.shape[-1])
+    for t in (residual, out):
+        if t is not None and (t.numel() != rows * n or not t.is_contiguous()):
+            return None
+    gate2 = gate.reshape(-1, gate.shape[-1]) if gate is not None else None
+    bounds = row_slabs(rows, chunks)
+    if not x.is_cuda:
+        from .. import ops
+        if out is None:
+            out = torch.empty(*x.shape[:-1], n, dtype=x.dtype, device=x.device)
+        o2, r2 = out.view(rows, n), residual.reshape(rows, n) if residual is not None else None
+        for r0, r1 in bounds:
+            y = ops.linear(x2[r0:r1], weight, None, w_scale=w_scale)
+            all_reduce(y)
+            _epilogue_rows(y, o2[r0:r1], bias, r2[r0:r1] if r2 is not None else None, gate2, rows_per_gate, r0)
+        return out
+    p = _P2P
+    if p is None or not P2P_STAGED or x.dtype != torch.bfloat16:
+        return None
     nbytes = rows * n * 2
     if n % 8 or nbytes > p.max_bytes or (w_scale is not None and rows > 64):
         return None
-    for t in (residual, out):
-        if t is not None and (t.dtype != torch.bfloat16 or t.numel() != rows * n or not t.is_contiguous()):
+    for t in (residual, out, bias):
+        if t is not None and (t.dtype != torch.bfloat16 or not _al16(t)):
             return None
-    if gate is not None and (gate.dtype != torch.bfloat16 or gate.stride(-1) != 1 or gate.shape[-1] < n):
+    if bias is not None and (not bias.is_contiguous() or bias.numel() != n):
+        return None
+    if gate2 is not None and (gate2.dtype != torch.bfloat16 or gate2.stride(-1) != 1 or gate2.shape[-1] < n
+                              or gate2.stride(0) % 8 or not _al16(gate2)):
         return None
     from .. import ops
-    stage = p.staging(rows, n, x.device).view(*x.shape[:-1], n)
-    ops.gemm_into(x, weight, stage, w_scale=w_scale)
+    stage = p.staging(rows, n, x.device)
     if out is None:
         out = torch.empty(*x.shape[:-1], n, dtype=x.dtype, device=x.device)
-    p.reduce_staged(out, n, bias, residual, gate.reshape(-1, gate.shape[-1]) if gate is not None else None,
-                    rows_per_gate)
+    o2 = out.view(rows, n)
+    r2 = residual.view(rows, n) if residual is not None else None
+    if len(bounds) == 1:
+        ops.gemm_into(x2, weight, stage, w_scale=w_scale)
+        p.reduce_staged(o2, n, bias, r2, gate2, rows_per_gate)
+        return out
+    cur = torch.cuda.current_stream(x.device)
+    side = _side_stream(x.device)
+    side.wait_stream(cur)   # out / residual / gate are ready before the side stream touches them
+    for r0, r1 in bounds:
+        ops.gemm_into(x2[r0:r1], weight, stage[r0:r1], w_scale=w_scale)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            p.reduce_staged(o2[r0:r1], n, bias, r2[r0:r1] if r2 is not None else None, gate2, rows_per_gate,
+                            row0=r0, slot_off=r0 * n * 2)
+    cur.wait_stream(side)
     return out
 
 
@@ -258,6 +295,10 @@ class P2PAllReduce:
         self.lib.shai_p2p_allreduce_staged.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                                        ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        self.lib.shai_p2p_allreduce_staged_at.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                          ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
         self.lib.shai_p2p_launch_counts.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong)]
         self.lib.shai_p2p_error.argtypes = [ctypes.c_void_p]
         self.lib.shai_p2p_set_max_blocks.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -307,10 +348,11 @@ class P2PAllReduce:
 
     def reduce_staged(self, out: torch.Tensor, ncols: int, bias: Optional[torch.Tensor] = None,
                       residual: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None,
-                      rows_per_gate: int = 1) -> torch.Tensor:
-        """out = residual + gate[row // rows_per_gate] * (sum over ranks of the staged partials + bias)
-        (contiguous bf16, ``out.numel()`` elements: the first ``out.numel()`` of the staging slot; ``out`` may
-        be ``residual``; ``gate`` [G, >= ncols] with rows of stride ``gate.stride(0)``)."""
+                      rows_per_gate: int = 1, row0: int = 0, slot_off: int = 0) -> torch.Tensor:
+        """out = residual + gate[(row0 + row) // rows_per_gate] * (sum over ranks of the staged partials + bias)
+        (contiguous bf16, ``out.numel()`` elements at byte ``slot_off`` of every rank's staging slot -- a row slab
+        of a larger staged output; ``out`` may be ``residual``; ``gate`` [G, >= ncols] with rows of stride
+        ``gate.stride(0)``)."""
         nbytes = out.numel() * 2
         two = nbytes > self.one_shot_max
         for t in (bias, residual):
@@ -318,12 +360,12 @@ class P2PAllReduce:
         if gate is not None:
             assert gate.dtype == torch.bfloat16 and gate.dim() == 2 and gate.stride(1) == 1
         st = torch.cuda.current_stream(out.device).cuda_stream
-        rc = self.lib.shai_p2p_allreduce_staged(self.ctx, out.data_ptr(), nbytes, int(ncols),
-                                                bias.data_ptr() if bias is not None else None,
-                                                residual.data_ptr() if residual is not None else None,
-                                                gate.data_ptr() if gate is not None else None,
-                                                int(gate.stride(0)) if gate is not None else 0, int(rows_per_gate),
-                                                int(two), st)
+        rc = self.lib.shai_p2p_allreduce_staged_at(self.ctx, out.data_ptr(), nbytes, int(ncols),
+                                                   bias.data_ptr() if bias is not None else None,
+                                                   residual.data_ptr() if residual is not None else None,
+                                                   gate.data_ptr() if gate is not None else None,
+                                                   int(gate.stride(0)) if gate is not None else 0, int(rows_per_gate),
+                                                   int(row0), int(slot_off), int(two), st)
         if rc != 0:
             raise RuntimeError(f"p2p staged all-reduce launch failed ({rc})")
         return out

@@ -108,24 +108,14 @@ class RowParallelLinear(_ShardLoadMixin, nn.Module):
         if self.tp_size == 1:
             return ops.linear(x, self.weight, self.bias, residual=residual, w_scale=self.w_scale)
         rows = x.numel() // x.shape[-1]
-        nch = comm.overlap_chunks(rows)
-        if nch > 1:  # chunk i's all-reduce overlaps chunk i+1's GEMM
-            x2 = x.reshape(rows, x.shape[-1])
-            y = torch.empty(rows, self.out_features, dtype=x.dtype, device=x.device)
-            def gemm_chunk(xs, ys):
-                if ys.is_cuda and self.w_scale is None:
-                    ops.gemm_into(xs, self.weight, ys)
-                else:
-                    ys.copy_(ops.linear(xs, self.weight, None, w_scale=self.w_scale))
-            comm.all_reduce_overlapped(x2, gemm_chunk, y, nch)
-            y = y.view(*x.shape[:-1], self.out_features)
-        else:
-            # xGMI P2P: the GEMM writes into the IPC staging slot and one kernel reduces + adds bias / residual
-            y = comm.row_parallel_reduce(x, self.weight, self.bias, residual, self.w_scale)
-            if y is not None:
-                return y.view(*x.shape[:-1], self.out_features)
-            y = ops.linear(x, self.weight, None, w_scale=self.w_scale)
-            comm.all_reduce(y)
+        # fused (GEMM into the IPC staging slot, one kernel reduces + adds bias / residual) and, at >= 1024 rows,
+        # overlapped (row slab i's reduce runs beside slab i + 1's GEMM); CPU (gloo): the same slab schedule
+        y = comm.row_parallel_reduce(x, self.weight, self.bias, residual, self.w_scale,
+                                     chunks=comm.overlap_chunks(rows))
+        if y is not None:
+            return y.view(*x.shape[:-1], self.out_features)
+        y = ops.linear(x, self.weight, None, w_scale=self.w_scale)
+        comm.all_reduce(y)
         if self.bias is not None or residual is not None:
             y = ops.bias_act(y, self.bias, residual)
         return y
@@ -234,10 +224,16 @@ FP8_LAYER_TYPES = (ColumnParallelLinear, RowParallelLinear, QKVParallelLinear, G
 @torch.no_grad()
 def quantize_fp8_(model: nn.Module) -> int:
     """Quantise every TP linear layer of ``model`` to fp8 weights in place (embeddings / LM head
-    stay bf16).  Call after any weight transform (e.g. RMSNorm gain folding).  Returns the count."""
+    stay bf16).  Call after any weight transform (e.g. RMSNorm gain folding).  Returns the count.
+    A sub-module with ``no_fp8 = True`` (e.g. the mllama vision tower: vLLM's ``quantization: fp8`` leaves the
+    vision encoder in bf16) keeps every linear under it bf16."""
     n = 0
+    skip = set()
     for m in model.modules():
-        if isinstance(m, FP8_LAYER_TYPES):
+        if getattr(m, "no_fp8", False):
+            skip.update(id(c) for c in m.modules())
+    for m in model.modules():
+        if isinstance(m, FP8_LAYER_TYPES) and id(m) not in skip:
             m.quantize_fp8_()
             n += 1
     return n

@@ -59,6 +59,24 @@ def run(rank, world, port):
         key = "staged_two_shot" if rows * cols * 2 > ar.one_shot_max else "staged_one_shot"
         assert after[key] == before[key] + 1, (key, before, after)
         dist.barrier()
+    # row slabs of one staged output (the overlapped row-parallel stage): slab i reduced from byte offset
+    # r0 * cols * 2 of every rank's slot, the gate indexed from the slab's first row
+    rows, cols, rpg = 1000, 3072, 250
+    torch.manual_seed(99)
+    parts = [torch.randn(rows, cols, device="cuda").bfloat16() for _ in range(world)]
+    bias = torch.randn(cols, device="cuda").bfloat16()
+    res = torch.randn(rows, cols, device="cuda").bfloat16()
+    gate = torch.randn(rows // rpg, 2 * cols, device="cuda").bfloat16()[:, cols:]
+    want = res.float() + gate.float().repeat_interleave(rpg, 0) * (sum(p.float() for p in parts) + bias.float())
+    stage = ar.staging(rows, cols, torch.device("cuda", 0))
+    stage.copy_(parts[rank])
+    out = torch.empty_like(res)
+    for r0, r1 in ((0, 40), (40, 600), (600, 1000)):     # one-shot and two-shot sized slabs
+        ar.reduce_staged(out[r0:r1], cols, bias, res[r0:r1], gate, rpg, row0=r0, slot_off=r0 * cols * 2)
+    torch.cuda.synchronize()
+    err = ((out.float() - want).abs().max() / want.abs().max()).item()
+    assert err < 2e-2, err
+    dist.barrier()
     # all-gather (vocab-parallel logits: [B, V / world] shards -> [world * B, V / world] rank-major)
     for rows, cols in ((1, 8), (64, 4096), (3, 1000), (64, 16032)):
         torch.manual_seed(rows * 7 + cols)

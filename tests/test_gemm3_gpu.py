@@ -2,7 +2,10 @@
 
 * gemm_pipe.hip (v3): configs 5 / 6 (256x256 tile, 4- / 2-stage ring) and 7 / 8 (256x320 tile: 128x80 per
   wave, the extra W rows staged by waves 0-3).
-* gemm_8ph.hip (v4, 8-phase ping-pong): configs 9 (256x256) and 10 (256x320).
+* gemm_8ph.hip (v4, 8-phase ping-pong): configs 9 (256x256) and 10 (256x320), 11 / 12 persistent.
+* gemm_w4.hip (four-wave, one 128x128 wave tile per SIMD): config 13 (256x256) -- in production for the VAE
+  decoder convs and the LLM prefill / Flux shapes, so every epilogue it implements is forced here too
+  (test_w4_* below).
 """
 import os
 import subprocess
@@ -14,7 +17,7 @@ import torch
 from shai_amd import ops
 
 pytestmark = pytest.mark.gpu
-CFGS = [5, 7, 8, 9, 10, 11, 12]
+CFGS = [5, 7, 8, 9, 10, 11, 12, 13]
 
 
 def _rel(a, b):
@@ -96,3 +99,87 @@ def test_gemm3_conv_forced(cuda, cfg):
     r = subprocess.run([sys.executable, "-c", CONV_SCRIPT.format(root=root)], env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+W4 = 13
+
+
+@pytest.mark.parametrize("act", ["gelu", "silu", "gelu_tanh"])
+def test_w4_glu_acts_ragged(cuda, act):
+    """GLU epilogue of the four-wave kernel with ragged M / N (edge tiles take the element-wise path)."""
+    M, N, K = 777, 2 * 648, 320
+    torch.manual_seed(1)
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16()
+    out = torch.empty(M, N // 2, device=cuda, dtype=torch.bfloat16)
+    ops.gemm_into(a, w, out, b, act=act, glu=True, force_cfg=W4)
+    y = a.float() @ w.float().t() + b.float()
+    f = {"gelu": torch.nn.functional.gelu, "silu": torch.nn.functional.silu,
+         "gelu_tanh": lambda t: torch.nn.functional.gelu(t, approximate="tanh")}[act]
+    assert _rel(out, y[:, 0::2] * f(y[:, 1::2])) < 1e-2
+
+
+@pytest.mark.parametrize("M,N", [(512, 512), (600, 264)])
+def test_w4_gate_residual_inplace(cuda, M, N):
+    """out = x + gate[row // rpg] * act(x W^T + b), in place on the residual (AdaLN-Zero gated output)."""
+    K, rpg = 384, 128
+    torch.manual_seed(2)
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16()
+    g = torch.randn((M + rpg - 1) // rpg, N, device=cuda).bfloat16()
+    x = torch.randn(M, N, device=cuda).bfloat16()
+    want = x.float() + g.float().repeat_interleave(rpg, 0)[:M] * torch.nn.functional.silu(a.float() @ w.float().t() + b.float())
+    ops.gemm_into(a, w, x, b, act="silu", residual=x, gate=g, rows_per_gate=rpg, force_cfg=W4)
+    assert _rel(x, want) < 1e-2
+
+
+def test_w4_batched_alpha(cuda):
+    """Batched strided operands (blockIdx.y) with alpha / res_alpha scaling."""
+    B, M, N, K = 2, 520, 512, 256
+    torch.manual_seed(3)
+    a = torch.randn(B, M, K, device=cuda).bfloat16()
+    w = torch.randn(N, K, device=cuda).bfloat16()
+    r = torch.randn(B, M, N, device=cuda).bfloat16()
+    j = torch.zeros(B, M + 8, N, device=cuda).bfloat16()
+    ops.gemm_into(a, w, j[:, 8:], residual=r, alpha=0.5, res_alpha=-2.0, force_cfg=W4)
+    assert _rel(j[:, 8:], 0.5 * (a.float() @ w.float().t()) - 2.0 * r.float()) < 1e-2
+    assert j[:, :8].abs().sum().item() == 0
+
+
+@pytest.mark.parametrize("up,c2", [(False, 0), (True, 0), (False, 256), (True, 128)])
+def test_w4_conv_temb_residual(cuda, up, c2):
+    """Implicit-GEMM conv on the four-wave kernel as the VAE decoder / UNet use it: nearest-2x upsample, channel
+    concat, per-image bias (temb), SiLU, residual -- against the fp32 reference conv (own process: the forced
+    config is read once per process from SHAI_GEMM_FORCE)."""
+    code = CONV_W4_SCRIPT.format(root=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), up=up, c2=c2)
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SHAI_GEMM_FORCE=str(W4)),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+CONV_W4_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+import shai_amd.ops as ops
+from shai_amd.ops import reference as ref
+torch.manual_seed(4)
+up, c2 = {up}, {c2}
+N, H, C, Co = 2, 24, 256, 256
+x = torch.randn(N, H, H, C, device="cuda").bfloat16()
+x2 = torch.randn(N, H, H, c2, device="cuda").bfloat16() if c2 else None
+cin = C + c2
+w = (torch.randn(Co, cin, 3, 3, device="cuda") / (cin * 9) ** 0.5).bfloat16()
+wp = ops.pack_conv_weight(w)
+b = torch.randn(Co, device="cuda").bfloat16()
+temb = torch.randn(N, Co, device="cuda").bfloat16()
+OH = 2 * H if up else H
+res = torch.randn(N, OH, OH, Co, device="cuda").bfloat16()
+y = ops.conv2d(x, wp, b, 3, 3, 1, 1, upsample=up, x2=x2, temb=temb, residual=res, act="silu")
+yr = ref.conv2d(x.cpu(), wp.cpu(), b.cpu(), 3, 3, 1, 1, upsample=up, x2=x2.cpu() if x2 is not None else None,
+                temb=temb.cpu(), residual=res.cpu(), act="silu")
+rel = ((y.float().cpu() - yr.float()).norm() / yr.float().norm()).item()
+print("REL", rel)
+assert rel < 2e-2, rel
+"""

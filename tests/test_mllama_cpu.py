@@ -143,3 +143,20 @@ def test_text_only_and_mixed_batch():
     assert len(b.output) == 3 and eng.bm.num_free == eng.num_kv_blocks
     with pytest.raises(ValueError):
         LLMEngine(c.text, device="cpu", max_num_seqs=1, max_model_len=64).add_request([1, 2], p, image=_image())
+
+
+def test_fp8_quantization_leaves_vision_tower_bf16():
+    """``quantization: fp8`` converts the language model's TP linears only: every linear under the vision tower
+    (no_fp8) keeps its bf16 weight (the tower's prefill-sized GEMMs must not silently go W8A8)."""
+    from shai_amd.models.mllama import MllamaForConditionalGeneration
+    from shai_amd.parallel.layers import FP8_LAYER_TYPES, quantize_fp8_
+    torch.manual_seed(0)
+    m = MllamaForConditionalGeneration(MllamaConfig.tiny())
+    n = quantize_fp8_(m)
+    assert n > 0
+    vis = [mod for mod in m.vision_model.modules() if isinstance(mod, FP8_LAYER_TYPES)]
+    txt = [mod for name, mod in m.named_modules()
+           if isinstance(mod, FP8_LAYER_TYPES) and not name.startswith("vision_model")]
+    assert vis and txt
+    assert all(mod.weight.dtype == torch.bfloat16 for mod in vis)
+    assert all(mod.weight.dtype == torch.float8_e4m3fn for mod in txt)

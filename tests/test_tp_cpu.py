@@ -14,8 +14,8 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("which", ["llama", "t5", "flux", "flux_sp", "flux_ovl", "row_overlap", "seq_comm",
-                                   "mllama_vision"])
+@pytest.mark.parametrize("which", ["llama", "t5", "flux", "flux_sp", "flux_ovl", "row_overlap", "row_gated_slabs",
+                                   "seq_comm", "mllama_vision"])
 def test_tp2_matches_tp1(which):
     mp.spawn(tp_worker.run, args=(2, _port(), which), nprocs=2, join=True)
 

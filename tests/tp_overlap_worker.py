@@ -1,6 +1,6 @@
-"""Two ranks on ONE GPU: the row-parallel compute / communication overlap path (chunk GEMMs on the compute
-stream, each chunk's all-reduce forked onto a side stream through the IPC P2P all-reduce) equals the dense
-product, eagerly and replayed from a HIP graph."""
+"""Two ranks on ONE GPU: the fused + overlapped row-parallel output stage (row-slab GEMMs into the IPC staging
+slot on the compute stream, each slab's staged reduce + residual epilogue forked onto a side stream) equals the
+dense product, eagerly and replayed from a HIP graph; below OVERLAP_MIN_ROWS one staged reduce runs unsplit."""
 import os
 
 import torch
@@ -34,10 +34,25 @@ def run(rank, world, port):
         return ((a.float() - want).norm() / want.norm()).item()
 
     for _ in range(3):
+        c0 = p2p.launch_counts()
         y = lin(xc, residual=rc)
         torch.cuda.synchronize()
         assert rel(y) < 2e-2, rel(y)
+        c1 = p2p.launch_counts()
+        # 4 slabs of 264 rows x 3072 (1.6 MB each): four staged two-shot reduces, no unfused all-reduce
+        assert c1["staged_two_shot"] - c0["staged_two_shot"] == 4, (c0, c1)
+        assert c1["two_shot"] == c0["two_shot"] and c1["one_shot"] == c0["one_shot"], (c0, c1)
         dist.barrier()
+    # the small-row regime (< OVERLAP_MIN_ROWS): one unsplit staged reduce
+    xs, rs = xc[:128], rc[:128]
+    c0 = p2p.launch_counts()
+    ys = lin(xs, residual=rs)
+    torch.cuda.synchronize()
+    c1 = p2p.launch_counts()
+    assert sum(c1[k] - c0[k] for k in ("staged_one_shot", "staged_two_shot")) == 1, (c0, c1)
+    ws = (x[:128].float() @ w.float().t() + res[:128].float()).cuda()
+    assert ((ys.float() - ws).norm() / ws.norm()).item() < 2e-2
+    dist.barrier()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):

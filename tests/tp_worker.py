@@ -156,6 +156,27 @@ def run(rank, world, port, which):
         load_into(lin, {"weight": w, "bias": b}, strict=True)
         assert comm.overlap_chunks(600) == 3 and comm.overlap_chunks(2) == 2
         _close(lin(x, residual=res), x @ w.t() + b + res, 1e-5)
+    elif which == "row_gated_slabs":
+        # the slab schedule of the fused + overlapped row-parallel output stage (comm.row_parallel_reduce): 3 slabs
+        # of 200 rows over 2 images of 300 rows, so a slab straddles the image boundary and the per-image AdaLN gate
+        # is indexed from the slab's row offset; in place on the residual (the Flux gated update)
+        from shai_amd.parallel import comm
+        init_distributed("gloo", tp_size=world)
+        assert comm.row_slabs(600, 3) == [(0, 200), (200, 400), (400, 600)]
+        assert comm.row_slabs(601, 3) == [(0, 201), (201, 402), (402, 601)] and comm.row_slabs(2, 8) == [(0, 1), (1, 2)]
+        g = torch.Generator().manual_seed(7)
+        K, N = 64, 48
+        w, b = torch.randn(N, K, generator=g), torch.randn(N, generator=g)
+        x, res = torch.randn(2, 300, K, generator=g), torch.randn(2, 300, N, generator=g)
+        mod = torch.randn(2, 3 * N, generator=g)
+        gate = mod[:, N:2 * N]                      # strided column chunk of a modulation tensor
+        want = res + gate[:, None, :] * (x @ w.t() + b)
+        kl = K // world
+        out = res.clone()
+        y = comm.row_parallel_reduce(x[..., rank * kl:(rank + 1) * kl], w[:, rank * kl:(rank + 1) * kl], b, out,
+                                     gate=gate, rows_per_gate=300, out=out, chunks=3)
+        assert y is out
+        _close(out, want, 1e-4)
     elif which == "seq_comm":
         from shai_amd.parallel import comm
         init_distributed("gloo", tp_size=world)

@@ -20,6 +20,8 @@ bool gemm4_supported(const GemmArgs& a);
 void launch_gemm4_var(const GemmArgs& a, int var, int bn, hipStream_t s);
 bool gemm_w4_supported(const GemmArgs& a);
 void launch_gemm_w4(const GemmArgs& a, int bn, hipStream_t s);
+bool gemm_ws_supported(const GemmArgs& a);
+void launch_gemm_ws(const GemmArgs& a, hipStream_t s);
 }  // namespace shai
 
 using shai::bf16_t;
@@ -161,6 +163,9 @@ int main(int argc, char** argv) {
       gemm("sd_proj_res", 262144, 320, 320, true, true),
       gemm("sd_ff_dn_res", 65536, 640, 2560, true, true),
       gemm("llm_pf_qkv", 8192, 6144, 4096),
+      gemm("ws_ragged_res", 1000, 640, 320, true, true),
+      geglu("ws_ragged_glu", 1000, 960, 320),
+      gemm("sd_q320", 262144, 320, 320, true),
       conv("unet64_320", 64, 64, 320, 320, 3),
       conv("unet32_640", 64, 32, 640, 640, 3),
       conv("unet16_1280", 64, 16, 1280, 1280, 3),
@@ -169,6 +174,12 @@ int main(int argc, char** argv) {
       conv("vae256_256", 4, 256, 256, 256, 3),
   };
   if (quick) probs.resize(3);
+  if (argc > 1 && !strcmp(argv[1], "--ws")) {  // the low-K problems of the W-stationary kernel only
+    std::vector<Problem> q;
+    for (auto& P : probs)
+      if (!P.conv && P.K == 320) q.push_back(P);
+    probs = q;
+  }
   if (plain_only) {
     std::vector<Problem> q;
     for (auto& P : probs)
@@ -206,7 +217,8 @@ int main(int argc, char** argv) {
     const char* name;
     int kind;  // 0: v3 256 4-stage, 1: v3 256 2-stage, 2: v3 320 2-stage, 10+v: v4 schedule variant v
   };
-  const Var vars[] = {{"v4_256w", 30}, {"v4_256pwn", 70}, {"v4_320w", 130}, {"v4_320pwn", 170}, {"w4_256", 5}, {"w4_320", 6}};
+  const Var vars[] = {{"v4_256w", 30}, {"v4_256pwn", 70}, {"v4_320w", 130}, {"v4_320pwn", 170}, {"w4_256", 5}, {"w4_320", 6},
+                      {"ws_320", 7}};
   constexpr int NV = sizeof(vars) / sizeof(vars[0]);
   auto run = [&](const Var& v, const shai::GemmArgs& g) {
     switch (v.kind) {
@@ -215,6 +227,7 @@ int main(int argc, char** argv) {
       case 2: shai::launch_gemm3(g, nullptr, 1, 2, s, 320); break;
       case 5: shai::launch_gemm_w4(g, 256, s); break;
       case 6: shai::launch_gemm_w4(g, 320, s); break;
+      case 7: shai::launch_gemm_ws(g, s); break;
       default: shai::launch_gemm4_var(g, v.kind % 100 - 10, v.kind >= 100 ? 320 : 256, s); break;
     }
   };
@@ -242,6 +255,7 @@ int main(int argc, char** argv) {
     for (int vi = 0; vi < NV; ++vi) {
       if (vars[vi].kind >= 10 && !shai::gemm4_supported(g)) continue;
       if ((vars[vi].kind == 5 || vars[vi].kind == 6) && !shai::gemm_w4_supported(g)) continue;
+      if (vars[vi].kind == 7 && !shai::gemm_ws_supported(g)) continue;
       CK(hipMemset(C, 0, (size_t)P.M * P.N * 2));
       CK(hipMemset(err, 0, 8));
       run(vars[vi], g);
@@ -259,6 +273,8 @@ int main(int argc, char** argv) {
       for (int vi = 0; vi < NV; ++vi) {
         if (vars[vi].kind >= 10 && !shai::gemm4_supported(g)) continue;
         if ((vars[vi].kind == 5 || vars[vi].kind == 6) && !shai::gemm_w4_supported(g)) continue;
+        if (vars[vi].kind == 7 && !shai::gemm_ws_supported(g)) continue;
+      if (vars[vi].kind == 7 && !shai::gemm_ws_supported(g)) continue;
         run(vars[vi], g);
         CK(hipEventRecord(e0, s));
         for (int it = 0; it < iters; ++it) run(vars[vi], g);
