@@ -1452,6 +1452,54 @@ void dequant_fp8(const Tensor& w8, const Tensor& scale, const Tensor& out) {
                                 w8.size(0), w8.size(1), stream());
 }
 
+// y = a w^T + bias + res_alpha residual into c, and LayerNorm(y) gamma + beta into c2, on the W-stationary kernel
+// (gemm_ws.hip: K = 320, N = 320, the row moments from the epilogue's registers).  Returns false (nothing launched)
+// when the problem is outside the kernel's contract; the caller then runs the GEMM and the norm separately.
+bool gemm_lnout(const Tensor& a, const Tensor& w, const Tensor& c, const Tensor& c2, const optional<Tensor>& bias,
+                const Tensor& residual, double res_alpha, const optional<Tensor>& gamma, const optional<Tensor>& beta,
+                double eps) {
+  check_rows(a, "a");
+  check_rows(w, "w");
+  check_bf16(c, "c");
+  check_bf16(c2, "c2");
+  check_rows(residual, "residual");
+  if (a.dim() != 2 || w.dim() != 2 || c.dim() != 2 || c2.dim() != 2 || residual.dim() != 2) return false;
+  shai::GemmArgs g{};
+  g.A = cptr(a);
+  g.W = cptr(w);
+  g.C = mptr(c);
+  g.M = a.size(0);
+  g.K = a.size(1);
+  g.N = w.size(0);
+  SHAI_CHECK(w.size(1) == g.K, "gemm_lnout K mismatch");
+  SHAI_CHECK(c.size(0) == g.M && c.size(1) == g.N && c2.sizes() == c.sizes() && residual.sizes() == c.sizes(),
+             "gemm_lnout output / residual shape mismatch");
+  if (c.stride(0) != c2.stride(0)) return false;
+  g.lda = a.stride(0);
+  g.ldw = w.stride(0);
+  g.ldc = c.stride(0);
+  g.residual = cptr(residual);
+  g.ldr = residual.stride(0);
+  g.alpha = 1.f;
+  g.res_alpha = (float)res_alpha;
+  g.batch = 1;
+  g.rows_per_bias2d = 1;
+  g.rows_per_gate = 1;
+  if (bias.has_value()) {
+    check_bf16(*bias, "bias");
+    SHAI_CHECK(bias->numel() == g.N, "gemm_lnout bias [N]");
+    g.bias = cptr(*bias);
+  }
+  for (const optional<Tensor>* t : {&gamma, &beta})
+    if (t->has_value()) {
+      check_bf16(**t, "gamma/beta");
+      SHAI_CHECK((*t)->numel() == g.N, "gemm_lnout gamma / beta [N]");
+    }
+  if (!shai::gemm_ws_lnout_supported(g)) return false;
+  shai::launch_gemm_ws_lnout(g, mptr(c2), optr(gamma), optr(beta), (float)eps, stream());
+  return true;
+}
+
 // W8A8 fp8 GEMM (gemm_f8.hip): a8 [M, K] / w8 [N, K] float8_e4m3fn, a_scale [M] / w_scale [N] fp32.
 // cfg < 0 picks the tile: 256 x 128 when that still yields >= 256 tiles, else 128 x 128.
 void gemm_f8(const Tensor& a8, const Tensor& w8, const Tensor& a_scale, const Tensor& w_scale, const Tensor& c,
@@ -1548,6 +1596,7 @@ TORCH_LIBRARY(shai, m) {
         "Tensor ctx_lens, Tensor positions, Tensor cos, Tensor sin, Tensor slots, Tensor(d!) ws, int h, int hk, "
         "int num_splits, float scale, Tensor? qkv_ws=None, int qkv_kg=0, int qkv_k=0, float qkv_eps=-1.0) -> ()");
   m.def("gemm_partials(Tensor a, Tensor w, float rms_eps) -> Tensor");
+  m.def("gemm_lnout(Tensor a, Tensor w, Tensor(a!) c, Tensor(b!) c2, Tensor? bias, Tensor residual, float res_alpha, Tensor? gamma, Tensor? beta, float eps) -> bool");
   m.def("gemm_tuning() -> str[]", &gemm_tuning);
   m.def("gemm_tuning_export() -> str[]", &gemm_tuning_export);
   m.def("gemm_tuning_import(str[] entries) -> int", &gemm_tuning_import);
@@ -1564,6 +1613,7 @@ TORCH_LIBRARY_IMPL(shai, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("dequant_fp8", &dequant_fp8);
   m.impl("gemm_f8", &gemm_f8);
+  m.impl("gemm_lnout", &gemm_lnout);
   m.impl("quant_rows_fp8", &quant_rows_fp8);
   m.impl("layernorm_mod", &layernorm_mod);
   m.impl("qk_norm_rope", &qk_norm_rope);

@@ -166,6 +166,11 @@ void launch_gemm_w4(const GemmArgs& a, int bn, hipStream_t s);
 // v6: W-stationary low-K GEMM (gemm_ws.hip): K = 320, N % 320 == 0, persistent over M, weights in VGPRs
 bool gemm_ws_supported(const GemmArgs& a);
 void launch_gemm_ws(const GemmArgs& a, hipStream_t s);
+// the same with the next LayerNorm in the epilogue: C = x W^T + bias + res_alpha R and C2 = LayerNorm(C) gamma + beta
+// (N = 320: the whole row in one workgroup; residual, no activation)
+bool gemm_ws_lnout_supported(const GemmArgs& a);
+void launch_gemm_ws_lnout(const GemmArgs& a, bf16_t* C2, const bf16_t* gamma, const bf16_t* beta, float eps,
+                          hipStream_t s);
 // v3: pipelined 256x256 LDS-DMA GEMM / conv (gemm_pipe.hip); config index gemm2_num_cfgs() - 1
 bool gemm3_supported(const GemmArgs& a);
 void launch_gemm3(const GemmArgs& a, float* ws, int splits, int stages, hipStream_t s, int bn = 256);

@@ -136,18 +136,34 @@ class BasicTransformerBlock(nn.Module):
         w, b, s = a1.qkv.folded(self.norm1)
         q, k, v = a1.split(ops.linear(x, w, b, row_affine=(mr, s)))
         o = ops.attention(q, k, v)
-        x, mr = a1.out.forward_stats(o.view(B, T, a1.heads * a1.head_dim), residual=x, stats="ln", eps=self.norm2.eps)
         a2 = self.attn2
-        w, b, s = a2.q.folded(self.norm2)
         H, hd = a2.heads, a2.head_dim
-        q = ops.linear(x, w, b, row_affine=(mr, s)).view(B, T, H, hd)
+        # 320-wide level: the out-projections compute the next LayerNorm in their epilogue (whole rows in one
+        # workgroup of the W-stationary kernel), so Q and the GEGLU run plain on the normalised rows; wider levels
+        # hand (mean, rstd) over and fold the norm into the consumer
+        lnout = x.is_cuda and ops.lnout_supported(B * T, C, a1.heads * a1.head_dim)
+        if lnout:
+            n2, n3 = self.norm2, self.norm3
+            x, xn = ops.linear_lnout(o.view(B, T, a1.heads * a1.head_dim), a1.out.weight, a1.out.bias, x, n2.weight,
+                                     n2.bias, n2.eps)
+            q = a2.q(xn).view(B, T, H, hd)
+        else:
+            x, mr = a1.out.forward_stats(o.view(B, T, a1.heads * a1.head_dim), residual=x, stats="ln",
+                                         eps=self.norm2.eps)
+            w, b, s = a2.q.folded(self.norm2)
+            q = ops.linear(x, w, b, row_affine=(mr, s)).view(B, T, H, hd)
         S = ctx_kv.shape[1]
         o = ops.attention(q, ctx_kv[..., : H * hd].view(ctx_kv.shape[0], S, H, hd),
                           ctx_kv[..., H * hd:].view(ctx_kv.shape[0], S, H, hd))
-        x, mr = a2.out.forward_stats(o.view(B, T, H * hd), residual=x, stats="ln", eps=self.norm3.eps)
         proj = self.ff.net[0].proj
-        w, b, s = proj.folded(self.norm3)
-        h = ops.linear(x, w, b, act=proj.act, glu=True, row_affine=(mr, s))
+        if lnout:
+            x, xn = ops.linear_lnout(o.view(B, T, H * hd), a2.out.weight, a2.out.bias, x, self.norm3.weight,
+                                     self.norm3.bias, self.norm3.eps)
+            h = ops.linear(xn, proj.weight, proj.bias, act=proj.act, glu=True)
+        else:
+            x, mr = a2.out.forward_stats(o.view(B, T, H * hd), residual=x, stats="ln", eps=self.norm3.eps)
+            w, b, s = proj.folded(self.norm3)
+            h = ops.linear(x, w, b, act=proj.act, glu=True, row_affine=(mr, s))
         down = self.ff.net[2]
         if next_eps is None:
             return down(h, residual=x), None

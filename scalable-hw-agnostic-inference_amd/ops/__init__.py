@@ -280,6 +280,33 @@ def linear_stats(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act
     return _linear_norm_io(x, w, bias, act, residual, False, 1.0, 1.0, row_affine, stats, eps, force_cfg)
 
 
+def linear_lnout(x: torch.Tensor, w: torch.Tensor, bias, residual: torch.Tensor, gamma, beta, eps: float = 1e-5):
+    """(y, LayerNorm(y; gamma, beta)) with y = x @ w^T + bias + residual: the next LayerNorm computed by the producing
+    GEMM's epilogue (the W-stationary kernel holds whole 320-wide rows: exact two-pass moments of the stored bf16 y),
+    so the consumer runs a plain GEMM on the normalised rows.  Falls back to GEMM + standalone LayerNorm wherever
+    the fused kernel does not apply (other widths, CPU)."""
+    if not _gpu(x):
+        y = ref.linear(x, w, bias, None, residual)
+        return y, ref.layernorm(y, gamma, beta, eps)[0]
+    K, N = x.shape[-1], w.shape[0]
+    x2 = x.reshape(-1, K) if (x.dim() == 2 or x.is_contiguous()) else x.contiguous().reshape(-1, K)
+    r2 = residual.reshape(-1, N)
+    y = torch.empty(x2.shape[0], N, dtype=x.dtype, device=x.device)
+    y2 = torch.empty_like(y)
+    if LNOUT and _K().gemm_lnout(x2, w, y, y2, bias, r2, 1.0, gamma, beta, float(eps)):
+        return y.view(*x.shape[:-1], N), y2.view(*x.shape[:-1], N)
+    y = linear(x, w, bias, residual=residual)
+    return y, layernorm(y, gamma, beta, eps)[0]
+
+
+LNOUT = os.environ.get("SHAI_LNOUT", "1") != "0"  # A/B switch for the producer-side LayerNorm (linear_lnout)
+
+
+def lnout_supported(rows: int, n: int, k: int) -> bool:
+    """Whether linear_lnout runs fused on the GPU (W-stationary kernel: K = N = 320)."""
+    return LNOUT and n == 320 and k == 320
+
+
 def fold_layernorm(w: torch.Tensor, bias: Optional[torch.Tensor], gamma: Optional[torch.Tensor],
                    beta: Optional[torch.Tensor]):
     """(w', bias', s) so that LayerNorm(x; gamma, beta) @ w^T + bias == rstd * (x @ w'^T - mean * s) + bias':

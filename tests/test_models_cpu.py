@@ -69,3 +69,16 @@ def test_flops_counter():
     from shai_amd.bench.flops import sd21_unet_flops
     fc = sd21_unet_flops(2)
     assert 1.4e12 < fc.total < 1.8e12
+
+
+def test_linear_lnout_cpu_reference():
+    """ops.linear_lnout on the CPU: (x W^T + b + R, LayerNorm of it) -- the contract the fused GPU epilogue meets."""
+    import torch
+    from shai_amd import ops
+    torch.manual_seed(0)
+    x, w, b = torch.randn(37, 320), torch.randn(320, 320) / 18, torch.randn(320)
+    r, g, be = torch.randn(37, 320) + 5, 1 + 0.1 * torch.randn(320), 0.1 * torch.randn(320)
+    y, yn = ops.linear_lnout(x, w, b, r, g, be, 1e-5)
+    want = x @ w.t() + b + r
+    assert torch.allclose(y, want, atol=1e-4)
+    assert torch.allclose(yn, torch.nn.functional.layer_norm(want, (320,), g, be, 1e-5), atol=1e-4)

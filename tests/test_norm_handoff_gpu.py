@@ -103,8 +103,10 @@ def test_conv_gn_partials(cuda, up, temb):
     assert rel(p8, ref.col_partials(y8.reshape(-1, cout))) < 1e-5
 
 
-def test_unet_norm_handoff_matches(cuda):
-    """SD2.1-shaped (reduced-width) UNet: the hand-off forward vs the standalone-norm forward."""
+@pytest.mark.parametrize("lnout", [True, False])
+def test_unet_norm_handoff_matches(cuda, lnout):
+    """SD2.1-shaped (reduced-width) UNet: the hand-off forward vs the standalone-norm forward (at the 320-wide level
+    either with the LayerNorms computed by the producing out-projections, ops.linear_lnout, or folded into Q / GEGLU)."""
     from shai_amd.models import unet2d
     from shai_amd.models.unet2d import UNet2DConditionModel, UNetConfig
     torch.manual_seed(5)
@@ -117,15 +119,16 @@ def test_unet_norm_handoff_matches(cuda):
     x = torch.randn(B, H, H, 4, device="cuda").bfloat16()
     t = torch.tensor([500.0], device="cuda")
     kv = m.context_kv(torch.randn(B, 77, 256, device="cuda").bfloat16())
-    old, old_min = unet2d.NORM_HANDOFF, ops.FOLD_MIN_TILES
+    old, old_min, old_lo = unet2d.NORM_HANDOFF, ops.FOLD_MIN_TILES, ops.LNOUT
     try:
         ops.FOLD_MIN_TILES = 0  # fold at this small size too
+        ops.LNOUT = lnout
         unet2d.NORM_HANDOFF = True
         y1 = m(x, t, kv)
         unet2d.NORM_HANDOFF = False
         y0 = m(x, t, kv)
     finally:
-        unet2d.NORM_HANDOFF, ops.FOLD_MIN_TILES = old, old_min
+        unet2d.NORM_HANDOFF, ops.FOLD_MIN_TILES, ops.LNOUT = old, old_min, old_lo
     assert torch.isfinite(y1).all()
     assert rel(y1, y0) < 2e-2
 

@@ -9,7 +9,8 @@ for src in gemm_lds gemm_pipe gemm_8ph gemm_w4 gemm_ws gemv attention attention2
   # incremental: rebuild an object only when its source or a shared header is newer
   if [ ! -f "$OUT/$src.o" ] || [ -n "$(find "$ROOT/csrc/kernels/$src.hip" "$ROOT/csrc/kernels/"*.h -newer "$OUT/$src.o")" ]; then
     extra=""
-    [ "$src" = gemm_w4 ] && extra="-mllvm -pragma-unroll-threshold=100000"   # as csrc/build.py EXTRA_KFLAGS
+    { [ "$src" = gemm_w4 ] || [ "$src" = gemm_ws ]; } && extra="-mllvm -pragma-unroll-threshold=100000"
+    [ "$src" = gemm_ws ] && extra="$extra -fno-slp-vectorize"   # as csrc/build.py EXTRA_KFLAGS
     hipcc $FLAGS $extra -c "$ROOT/csrc/kernels/$src.hip" -o "$OUT/$src.o" &
   fi
 done

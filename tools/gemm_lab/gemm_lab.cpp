@@ -22,6 +22,7 @@ bool gemm_w4_supported(const GemmArgs& a);
 void launch_gemm_w4(const GemmArgs& a, int bn, hipStream_t s);
 bool gemm_ws_supported(const GemmArgs& a);
 void launch_gemm_ws(const GemmArgs& a, hipStream_t s);
+void gemm_ws_set_ablation(int a);
 }  // namespace shai
 
 using shai::bf16_t;
@@ -110,6 +111,7 @@ struct Problem {
   int M, N, K;            // plain GEMM (conv: M = N*OH*OW, K = KH*KW*Cin)
   int conv = 0, Nimg = 0, H = 0, Wd = 0, Cin = 0, KH = 1, stride = 1, pad = 0, ups = 0;
   bool bias = false, res = false, glu = false;
+  bool lnf = false;  // folded LayerNorm with (mean, rstd) = (0, 1) and zero column sums: same product, fold path timed
 };
 
 static Problem gemm(const char* nm, int M, int N, int K, bool bias = false, bool res = false) {
@@ -120,6 +122,11 @@ static Problem gemm(const char* nm, int M, int N, int K, bool bias = false, bool
 static Problem geglu(const char* nm, int M, int N, int K) {
   Problem p = gemm(nm, M, N, K, true);
   p.glu = true;
+  return p;
+}
+static Problem ln(Problem p) {
+  p.lnf = true;
+  p.name += "_ln";
   return p;
 }
 static Problem conv(const char* nm, int Nimg, int H, int Cin, int Cout, int KH, int ups = 0) {
@@ -166,6 +173,8 @@ int main(int argc, char** argv) {
       gemm("ws_ragged_res", 1000, 640, 320, true, true),
       geglu("ws_ragged_glu", 1000, 960, 320),
       gemm("sd_q320", 262144, 320, 320, true),
+      ln(geglu("sd_geglu64", 262144, 2560, 320)),
+      ln(gemm("sd_qkv", 262144, 960, 320)),
       conv("unet64_320", 64, 64, 320, 320, 3),
       conv("unet32_640", 64, 32, 640, 640, 3),
       conv("unet16_1280", 64, 16, 1280, 1280, 3),
@@ -194,7 +203,7 @@ int main(int argc, char** argv) {
     maxC = std::max(maxC, (size_t)P.M * P.N);
   }
   bf16_t *A, *W, *C, *bias, *R;
-  float *ref, *err, *ws;
+  float *ref, *err, *ws, *mr, *cols;
   CK(hipMalloc(&A, maxA * 2));
   CK(hipMalloc(&W, maxW * 2));
   CK(hipMalloc(&C, maxC * 2));
@@ -203,6 +212,16 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&ref, maxC * 6));  // GLU problems keep the product and the GLU output
   CK(hipMalloc(&err, 8));
   CK(hipMalloc(&ws, 64));
+  {
+    size_t maxM = 0;
+    for (auto& P : probs) maxM = std::max(maxM, (size_t)P.M);
+    std::vector<float> h(2 * maxM);
+    for (size_t i = 0; i < maxM; ++i) { h[2 * i] = 0.f; h[2 * i + 1] = 1.f; }
+    CK(hipMalloc(&mr, 2 * maxM * 4));
+    CK(hipMemcpy(mr, h.data(), 2 * maxM * 4, hipMemcpyHostToDevice));
+    CK(hipMalloc(&cols, 65536 * 4));
+    CK(hipMemset(cols, 0, 65536 * 4));
+  }
   fill_kernel<<<4096, 256>>>(A, maxA, 1u, 1.f);
   fill_kernel<<<4096, 256>>>(W, maxW, 2u, 1.f);
   fill_kernel<<<4096, 256>>>(R, maxC, 3u, 1.f);
@@ -218,7 +237,7 @@ int main(int argc, char** argv) {
     int kind;  // 0: v3 256 4-stage, 1: v3 256 2-stage, 2: v3 320 2-stage, 10+v: v4 schedule variant v
   };
   const Var vars[] = {{"v4_256w", 30}, {"v4_256pwn", 70}, {"v4_320w", 130}, {"v4_320pwn", 170}, {"w4_256", 5}, {"w4_320", 6},
-                      {"ws_320", 7}};
+                      {"ws_320", 7}, {"ws_nost", 107}, {"ws_nomfma", 207}, {"ws_nodma", 407}, {"ws_dmaonly", 307}};
   constexpr int NV = sizeof(vars) / sizeof(vars[0]);
   auto run = [&](const Var& v, const shai::GemmArgs& g) {
     switch (v.kind) {
@@ -227,13 +246,21 @@ int main(int argc, char** argv) {
       case 2: shai::launch_gemm3(g, nullptr, 1, 2, s, 320); break;
       case 5: shai::launch_gemm_w4(g, 256, s); break;
       case 6: shai::launch_gemm_w4(g, 320, s); break;
-      case 7: shai::launch_gemm_ws(g, s); break;
+      case 7: case 107: case 207: case 307: case 407:
+        shai::gemm_ws_set_ablation(v.kind / 100);
+        shai::launch_gemm_ws(g, s);
+        shai::gemm_ws_set_ablation(0);
+        break;
       default: shai::launch_gemm4_var(g, v.kind % 100 - 10, v.kind >= 100 ? 320 : 256, s); break;
     }
   };
 
   for (auto& P : probs) {
     shai::GemmArgs g = make_args(P, A, W, C, bias, R);
+    if (P.lnf) {
+      g.row_mr = mr;
+      g.col_s = cols;
+    }
     // reference
     if (P.conv) {
       ref_conv<<<dim3((P.N + 127) / 128, P.M), 128>>>(A, W, ref, P.Nimg, P.H, P.Wd, P.Cin, g.OH, g.OW, P.N, P.KH, P.KH,
@@ -253,9 +280,10 @@ int main(int argc, char** argv) {
     printf("== %s M=%d N=%d K=%d%s\n", P.name.c_str(), P.M, P.N, P.K, P.conv ? " (conv)" : "");
     std::vector<float> best(NV, 1e30f);
     for (int vi = 0; vi < NV; ++vi) {
-      if (vars[vi].kind >= 10 && !shai::gemm4_supported(g)) continue;
+      if (vars[vi].kind >= 10 && vars[vi].kind % 100 != 7 && !shai::gemm4_supported(g)) continue;
       if ((vars[vi].kind == 5 || vars[vi].kind == 6) && !shai::gemm_w4_supported(g)) continue;
-      if (vars[vi].kind == 7 && !shai::gemm_ws_supported(g)) continue;
+      if (vars[vi].kind % 100 == 7 && !shai::gemm_ws_supported(g)) continue;
+      if (vars[vi].kind > 100 && vars[vi].kind % 100 == 7) continue;  // ablations: timing only
       CK(hipMemset(C, 0, (size_t)P.M * P.N * 2));
       CK(hipMemset(err, 0, 8));
       run(vars[vi], g);
@@ -271,10 +299,9 @@ int main(int argc, char** argv) {
     const int rounds = quick ? 2 : 5, iters = 10;
     for (int r = 0; r < rounds; ++r) {
       for (int vi = 0; vi < NV; ++vi) {
-        if (vars[vi].kind >= 10 && !shai::gemm4_supported(g)) continue;
+        if (vars[vi].kind >= 10 && vars[vi].kind % 100 != 7 && !shai::gemm4_supported(g)) continue;
         if ((vars[vi].kind == 5 || vars[vi].kind == 6) && !shai::gemm_w4_supported(g)) continue;
-        if (vars[vi].kind == 7 && !shai::gemm_ws_supported(g)) continue;
-      if (vars[vi].kind == 7 && !shai::gemm_ws_supported(g)) continue;
+        if (vars[vi].kind % 100 == 7 && !shai::gemm_ws_supported(g)) continue;
         run(vars[vi], g);
         CK(hipEventRecord(e0, s));
         for (int it = 0; it < iters; ++it) run(vars[vi], g);
