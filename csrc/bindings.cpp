@@ -282,7 +282,7 @@ Choice tune(const shai::GemmArgs& g_real, const Tensor& like, bool skinny_only =
     shai::gemm2_plan(g, &def.cfg, &def.splits);
     const int ms = max_splits_for(g);
     for (int c = 0; c < shai::gemm2_num_cfgs(); ++c) {
-      if (!shai::gemm2_cfg_supported(g, c)) continue;
+      if (!shai::gemm2_cfg_candidate(c) || !shai::gemm2_cfg_supported(g, c)) continue;
       for (int s = 1; s <= (shai::gemm2_cfg_splittable(c) ? ms : 1); s *= 2) cands.push_back({c, s});
     }
   }
@@ -916,11 +916,13 @@ void conv2d(const Tensor& x, const optional<Tensor>& x2, const Tensor& w, const 
   g.Wd = x.size(2);
   g.Cin1 = x.size(3);
   g.Cin = g.Cin1;
-  Tensor xcat;  // concat fallback: the fused two-source gather needs the split at a multiple of 32 channels
+  // concat fallback: the fused two-source gather of the tile kernels (v4 / four-wave / v2) needs both sources at
+  // multiples of 64 channels, so a 64-deep K-tile never straddles the split (every SD2.1 skip concat qualifies)
+  Tensor xcat;
   if (x2) {
     check_bf16(*x2, "x2");
     SHAI_CHECK(x2->is_contiguous() && x2->size(0) == g.Nimg && x2->size(1) == g.H && x2->size(2) == g.Wd, "x2 shape");
-    if (g.Cin1 % 32 != 0 || x2->size(3) % 32 != 0) {
+    if (g.Cin1 % 64 != 0 || x2->size(3) % 64 != 0) {
       xcat = at::cat({x, *x2}, 3);
       g.Cin1 = g.Cin = xcat.size(3);
     } else {

@@ -32,7 +32,7 @@ BUILD = os.path.join(ROOT, "build", "native")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
-KERNEL_SRCS = ["kernels/norm.hip", "kernels/gemm.hip", "kernels/gemm_lds.hip", "kernels/gemm_pipe.hip", "kernels/gemm_8ph.hip", "kernels/gemm_w4.hip", "kernels/gemm_ws.hip", "kernels/attention.hip", "kernels/attention2.hip", "kernels/attention3.hip", "kernels/elementwise.hip", "kernels/dit.hip",
+KERNEL_SRCS = ["kernels/norm.hip", "kernels/gemm.hip", "kernels/gemm_lds.hip", "kernels/gemm_8ph.hip", "kernels/gemm_w4.hip", "kernels/gemm_ws.hip", "kernels/attention.hip", "kernels/attention2.hip", "kernels/attention3.hip", "kernels/elementwise.hip", "kernels/dit.hip",
                "kernels/sampling.hip", "kernels/gemv.hip", "kernels/gemv2.hip",
                "kernels/gemm_f8.hip"]
 # per-source extra hipcc flags: gemm_w4's epilogue (256 accumulators x an activation) is larger than LLVM's

@@ -2,7 +2,7 @@
 //
 //   C[b,m,n] = gate * act(alpha * sum_k A[b,m,k] * W[b,n,k] + bias[n] + bias2d) + res_alpha * Res[b,m,n]
 //
-// Why a fourth kernel: v3 (gemm_pipe.hip) keeps several K-tiles of LDS-DMA in flight, but every K-step
+// Why a fourth kernel: v3 (the pipelined gemm_pipe.hip, retired in round 5) kept several K-tiles of LDS-DMA in flight, but every K-step
 // still starts with all 8 waves issuing their fragment reads at once, so each SIMD's matrix pipe idles
 // for the LDS latency of both of its waves once per 32-deep step (measured 1.08-1.2 PF on large plain
 // GEMMs vs 1.5-1.6 PF for hipBLASLt).  Here the two waves that share a SIMD run half a phase apart:

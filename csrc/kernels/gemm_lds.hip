@@ -473,8 +473,8 @@ struct TileCfg {
 static const TileCfg kCfgs[] = {{256, 320, 1.00f}, {256, 256, 1.00f}, {256, 128, 0.90f}, {128, 128, 0.75f},
                                 {128, 64, 0.55f}};
 constexpr int kNumCfgs = 5;
-// Config index space: [0, kNumCfgs) this file's tile configs; kNumCfgs + 0..3 the pipelined v3 kernel
-// (gemm_pipe.hip); kNumCfgs + 4 / + 5 the 8-phase ping-pong v4 kernel (gemm_8ph.hip) with 256 / 320 wide tiles,
+// Config index space: [0, kNumCfgs) this file's tile configs; kNumCfgs + 0..3 the retired pipelined v3 kernel
+// (cached choices run on v4); kNumCfgs + 4 / + 5 the 8-phase ping-pong v4 kernel (gemm_8ph.hip) with 256 / 320 wide tiles,
 // kNumCfgs + 6 / + 7 the same in its persistent form (next tile's operands prefetched under the epilogue).
 constexpr int kV4Cfg = kNumCfgs + 4;
 // kV4Cfg + 4 / + 5: the four-wave kernel (gemm_w4.hip) with 256 x 256 / 192 x 320 tiles (128 x 128 / 96 x 160
@@ -621,9 +621,8 @@ void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStre
     launch_gemm4(a, ws, splits, (v & 1) ? 320 : 256, s, v >= 2);
     return;
   }
-  if (cfg >= kNumCfgs) {  // pipelined kernel (gemm_pipe.hip): 256x256 / 256x320 tile, 4- / 2-stage ring
-    const int v = cfg - kNumCfgs;
-    launch_gemm3(a, ws, splits, (v & 1) ? 2 : 4, s, v >= 2 ? 320 : 256);
+  if (cfg >= kNumCfgs) {  // retired v3 (pipelined 256x256 / 256x320): a cached choice runs on v4, same tile width
+    launch_gemm4(a, ws, splits, cfg - kNumCfgs >= 2 ? 320 : 256, s, false);
     return;
   }
   if (!a.conv) {
@@ -655,6 +654,11 @@ void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipS
 
 int gemm2_num_cfgs() { return kWsCfg + 1; }
 
+// Configs the autotuner races: not the retired v3 indices (kNumCfgs .. + 3; the pipelined kernel held 2 cached
+// shapes when it was removed in round 5 -- every index stays valid for old caches) nor the lab-only 192 x 320
+// four-wave tile.
+bool gemm2_cfg_candidate(int cfg) { return !(cfg >= kNumCfgs && cfg < kV4Cfg) && cfg != kW4Cfg + 1; }
+
 bool gemm2_cfg_splittable(int cfg) { return cfg != kW4Cfg && cfg != kW4Cfg + 1 && cfg != kWsCfg; }
 
 bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
@@ -665,7 +669,7 @@ bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
   if (cfg == kW4Cfg) return gemm_w4_supported(a);
   if (cfg == kW4Cfg + 1) return false;  // 192 x 320 four-wave tile: lab only (gemm_w4.hip launch_gemm_w4)
   if (cfg >= kV4Cfg) return cfg < kV4Cfg + 4 && gemm4_supported(a);
-  if (cfg >= kNumCfgs) return gemm3_supported(a);
+  if (cfg >= kNumCfgs) return gemm4_supported(a);  // retired v3 -> v4
   if (a.in_scale != nullptr) return false;
   if (a.conv && a.A2 != nullptr && (a.Cin % 64 != 0 || a.Cin1 % 64 != 0)) return false;  // 64-wide K tiles
   return cfg >= 0 && cfg < kNumCfgs;
@@ -687,10 +691,9 @@ void gemm2_cfg_info(int cfg, int* bm, int* bn) {
     *bn = ((cfg - kV4Cfg) & 1) ? -320 : -256;
     return;
   }
-  if (cfg >= kNumCfgs) {
-    const int v = cfg - kNumCfgs;
-    *bm = (v & 1) ? 2 : 4;  // pipelined v3 kernel: stages
-    *bn = v >= 2 ? -320 : -256;
+  if (cfg >= kNumCfgs) {  // retired v3: runs as v4
+    *bm = 8;
+    *bn = cfg - kNumCfgs >= 2 ? -320 : -256;
     return;
   }
   *bm = kCfgs[cfg].bm;

@@ -171,9 +171,8 @@ void launch_gemm_ws(const GemmArgs& a, hipStream_t s);
 bool gemm_ws_lnout_supported(const GemmArgs& a);
 void launch_gemm_ws_lnout(const GemmArgs& a, bf16_t* C2, const bf16_t* gamma, const bf16_t* beta, float eps,
                           hipStream_t s);
-// v3: pipelined 256x256 LDS-DMA GEMM / conv (gemm_pipe.hip); config index gemm2_num_cfgs() - 1
-bool gemm3_supported(const GemmArgs& a);
-void launch_gemm3(const GemmArgs& a, float* ws, int splits, int stages, hipStream_t s, int bn = 256);
+// whether config cfg is raced by the autotuner (retired configs still run a cached choice, on their successor)
+bool gemm2_cfg_candidate(int cfg);
 void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipStream_t s);
 // v4: 8-phase ping-pong 256x256 / 256x320 LDS-DMA GEMM / conv (gemm_8ph.hip); config indices
 // gemm2_num_cfgs() - 2 (bn 256) and - 1 (bn 320)

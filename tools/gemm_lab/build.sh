@@ -5,7 +5,7 @@ ROOT=$(cd "$(dirname "$0")/../.." && pwd)
 OUT=$ROOT/build/gemm_lab
 mkdir -p "$OUT"
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=fast -I$ROOT/csrc -DSHAI_GEMM_LAB"
-for src in gemm_lds gemm_pipe gemm_8ph gemm_w4 gemm_ws gemv attention attention2 attention3; do
+for src in gemm_lds gemm_8ph gemm_w4 gemm_ws gemv attention attention2 attention3; do
   # incremental: rebuild an object only when its source or a shared header is newer
   if [ ! -f "$OUT/$src.o" ] || [ -n "$(find "$ROOT/csrc/kernels/$src.hip" "$ROOT/csrc/kernels/"*.h -newer "$OUT/$src.o")" ]; then
     extra=""
@@ -19,7 +19,7 @@ hipcc $FLAGS -x hip -c "$ROOT/tools/gemm_lab/attn_lab.cpp" -o "$OUT/attn_lab.o" 
 wait
 [ -s "$OUT/gemm_lab.o" ] && [ "$OUT/gemm_lab.o" -nt "$ROOT/tools/gemm_lab/gemm_lab.cpp" ] || { echo "gemm_lab.o stale"; exit 1; }
 mkdir -p "$ROOT/tools/gemm_lab/bin"
-hipcc --offload-arch=gfx950 "$OUT"/gemm_lab.o "$OUT"/gemm_lds.o "$OUT"/gemm_pipe.o "$OUT"/gemm_8ph.o "$OUT"/gemm_w4.o "$OUT"/gemm_ws.o "$OUT"/gemv.o \
+hipcc --offload-arch=gfx950 "$OUT"/gemm_lab.o "$OUT"/gemm_lds.o "$OUT"/gemm_8ph.o "$OUT"/gemm_w4.o "$OUT"/gemm_ws.o "$OUT"/gemv.o \
   -o "$ROOT/tools/gemm_lab/bin/gemm_lab"
 hipcc --offload-arch=gfx950 "$OUT"/attn_lab.o "$OUT"/attention.o "$OUT"/attention2.o "$OUT"/attention3.o -o "$ROOT/tools/gemm_lab/bin/attn_lab"
 echo "built tools/gemm_lab/bin/gemm_lab tools/gemm_lab/bin/attn_lab"

@@ -1,5 +1,5 @@
 // Standalone GEMM / implicit-GEMM conv lab: numerics of the hand-written kernels against a naive fp32
-// GPU reference, then interleaved timing rounds (guide rule 24) of v3 (gemm_pipe.hip) vs v4
+// GPU reference, then interleaved timing rounds (guide rule 24) of v4 (gemm_8ph.hip) vs v5 (gemm_w4.hip) vs v6
 // (gemm_8ph.hip) on random [-1, 1) bf16 operands.  No torch: builds in seconds with hipcc.
 //
 //   bash tools/gemm_lab/build.sh && ./build/gemm_lab [--quick]
@@ -241,9 +241,6 @@ int main(int argc, char** argv) {
   constexpr int NV = sizeof(vars) / sizeof(vars[0]);
   auto run = [&](const Var& v, const shai::GemmArgs& g) {
     switch (v.kind) {
-      case 0: shai::launch_gemm3(g, nullptr, 1, 4, s, 256); break;
-      case 1: shai::launch_gemm3(g, nullptr, 1, 2, s, 256); break;
-      case 2: shai::launch_gemm3(g, nullptr, 1, 2, s, 320); break;
       case 5: shai::launch_gemm_w4(g, 256, s); break;
       case 6: shai::launch_gemm_w4(g, 320, s); break;
       case 7: case 107: case 207: case 307: case 407:

@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gemm_ws_gpu.py tests/test_norm_handoff_gpu.py -x -q --timeout 200 \
+timeout -k 10 400 python -u -m pytest tests/test_gemm_ws_gpu.py tests/test_norm_handoff_gpu.py tests/test_gemm3_gpu.py -x -q --timeout 200 \
   --timeout-method thread > gpurun_out/r5g_pytest.log 2>&1 || { tail -30 gpurun_out/r5g_pytest.log; exit 1; }
 tail -1 gpurun_out/r5g_pytest.log
 bash tools/gpu_runs/gpu_retune_subset.sh '",320,b1" in key and key.startswith("0:")' \
