@@ -524,7 +524,9 @@ void launch_flash64(const AttnArgs& a, hipStream_t s) {
     return e == nullptr || atoi(e) != 0;
   }();
   if (dma && flash64_dma_supported(a)) {
-    launch_flash64_dma(a, 2, s);
+    // two 32-query groups per wave when the 256-query grid still fills the chip several times over
+    if ((long)((a.Sq + 255) / 256) * a.Hq * a.B >= 1024) launch_flash64_x2(a, s);
+    else launch_flash64_dma(a, s);
     return;
   }
   dim3 grid((a.Sq + 127) / 128, a.Hq, a.B);

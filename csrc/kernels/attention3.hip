@@ -5,7 +5,16 @@
 // instead of 3 (168): more co-resident waves to overlap one wave's MFMAs with another's softmax, which is what
 // bounds D = 64 attention (VALU issue + latency, profiles/pmc_round3.md: 37 % MFMA busy).  Measured (attention lab,
 // round 4): at 3 waves / SIMD (150 VGPRs) 906 vs 821 TF/s at the SD2.1 64x64 shape, 616 vs 557 at 32x32; forcing 4
-// waves spills (23 VGPRs) and halves the rate, so production runs the 3-wave build.
+// waves spills (23 VGPRs) and halves the rate, so production runs the 3-wave build (the 4-wave one is retired).
+//
+// flash64x2 (below) doubles the queries per wave; launch_flash64 picks it when the launch has >= 1024 of its
+// 256-query workgroups (the SD2.1 batch-64 shapes), the 128-query kernel for smaller grids where the x2 grid's tail
+// costs more than it gains.  Round 5 attention lab (tools/gemm_lab/attn_lab.cpp, this file built with
+// -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize as csrc/build.py does): B64 H5 S4096 1330 us (1033 TF/s) vs
+// 1378 us for the 128-query kernel and 1430 us before the flags; B64 H10 S1024 202 vs 225 us.  A variant that
+// software-pipelines the two groups half a tile apart (QK / PV of one group beside the other's exponentials, no
+// branch on the fast path) measured 1433-1491 us: hipcc kept its LDS reads just in time (a lgkmcnt(0) before every
+// MFMA) at 246 VGPRs, so it was dropped.
 #include "common.h"
 #include "launchers.h"
 
@@ -228,6 +237,253 @@ __global__ void __launch_bounds__(256, OCC) flash64_dma_kernel(const AttnArgs p)
   }
 }
 
+// flash64x2: the same K/V pipeline with TWO groups of 32 queries per wave (64 per wave, 256 per workgroup).  Each K /
+// V fragment read out of LDS feeds both groups' MFMAs (half the LDS traffic per FLOP), and the two groups' chains are
+// independent: group B's score MFMAs are in the matrix pipe while group A's softmax runs on the VALU, and A's P.V
+// MFMAs beside B's softmax -- the overlap a single 32-query chain (QK -> softmax -> PV, each waiting on the last)
+// can only get from other waves.  2 waves / SIMD (<= 256 registers).
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256, 2) flash64x2_kernel(const AttnArgs p) {
+  constexpr int D = 64, KT = 64, NS = 4, ND = 2, G = 2;
+  constexpr float kSumThr = 256.f;
+  constexpr float kL2e = 1.4426950408889634f;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 31, fh = lane >> 5;
+  const int b = blockIdx.z, hq = blockIdx.y;
+  const int hk = hq / (p.Hq / p.Hkv);
+  const int q_len = p.q_lens ? p.q_lens[b] : p.Sq;
+  const int kv_len = p.kv_lens ? p.kv_lens[b] : p.Skv;
+  const int c_off = p.q_lens ? kv_len - q_len : p.causal_offset;
+  if ((int)blockIdx.x * 256 >= q_len) return;
+  const int q0 = blockIdx.x * 256;
+  int qi[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) qi[g] = q0 + wid * 64 + 32 * g + fr;
+  const float sl2 = p.scale * kL2e;
+
+  const bf16_t* kbase = p.k + (long)b * p.k_bs + (long)hk * D;
+  const bf16_t* vbase = p.v + (long)b * p.v_bs + (long)hk * D;
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(kbase), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(vbase), (short)0, 0x7fffffff, 0x00020000);
+  int kv_end = kv_len;
+  if (CAUSAL) kv_end = min(kv_end, q0 + 255 + c_off + 1);
+  const int ntiles = kv_end > 0 ? (kv_end + KT - 1) / KT : 0;
+  const int drow = wid * 16 + (lane >> 3), dpos = lane & 7;
+  const int kch0 = dpos ^ ((drow >> 1) & 7), kch1 = dpos ^ (((drow + 8) >> 1) & 7);
+  const int vch0 = dpos ^ (((drow >> 1) & 1) << 2), vch1 = dpos ^ ((((drow + 8) >> 1) & 1) << 2);
+  auto dma = [&](int stage, int t) {
+    bf16_t* ks = smem + stage * 2 * KT * D;
+    bf16_t* vs = ks + KT * D;
+    const int key = t * KT + drow;
+    const uint32_t ok0 = key < kv_len ? 0u : 0x80000000u, ok1 = key + 8 < kv_len ? 0u : 0x80000000u;
+    const uint32_t r0 = (uint32_t)((long)key * p.k_ts * 2), r1 = (uint32_t)((long)(key + 8) * p.k_ts * 2);
+    const uint32_t v0 = (uint32_t)((long)key * p.v_ts * 2), v1 = (uint32_t)((long)(key + 8) * p.v_ts * 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (f3_lds_void*)(ks + (wid * 16) * D), 16, (r0 + kch0 * 16) | ok0, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (f3_lds_void*)(ks + (wid * 16 + 8) * D), 16, (r1 + kch1 * 16) | ok1, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (f3_lds_void*)(vs + (wid * 16) * D), 16, (v0 + vch0 * 16) | ok0, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (f3_lds_void*)(vs + (wid * 16 + 8) * D), 16, (v1 + vch1 * 16) | ok1, 0, 0, 0);
+  };
+  if (ntiles > 0) dma(0, 0);
+
+  f3bf16x8 qf[G][NS];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const bf16_t* qp = p.q + (p.q_start ? (long)p.q_start[b] * p.q_ts : (long)b * p.q_bs) +
+                        (long)min(qi[g], q_len - 1) * p.q_ts + (long)hq * D;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      uint4_ v = *reinterpret_cast<const uint4_*>(qp + 16 * s + 8 * fh);
+      if (qi[g] >= q_len) v = uint4_{0u, 0u, 0u, 0u};
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= sl2;
+      qf[g][s] = __builtin_bit_cast(f3bf16x8, pack8(f));
+    }
+  }
+
+  float16_ o[G][ND];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[g][d][r] = 0.f;
+  float m_run[G], l_run[G];
+  f3bf16x8 b_negm[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    m_run[g] = -INFINITY;
+    l_run[g] = 0.f;
+    b_negm[g] = __builtin_bit_cast(f3bf16x8, uint4_{0u, 0u, 0u, 0u});
+  }
+  const f3bf16x8 a_one = __builtin_bit_cast(f3bf16x8, uint4_{lane < 32 ? 0x3F80u : 0u, 0u, 0u, 0u});
+
+  const int g16 = lane >> 4, i16 = lane & 15;
+  const int tq = i16 >> 2, tp = i16 & 3;
+  int koff[NS], voff[ND];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) koff[s] = f3_kswz(fr, 2 * s + fh);
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    const int col = d * 32 + 16 * (g16 & 1) + 4 * tp;
+    voff[d] = f3_vswz(4 * fh + tq, col >> 3) + 4 * ((col >> 2) & 1);
+  }
+
+  float16_ sacc[G][2];
+  f3bf16x8 pf[G][2][2];
+  auto expo = [&](int g, float add, auto addt) {
+    constexpr bool ADD = decltype(addt)::value;
+    float ls4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          e[j] = __builtin_amdgcn_exp2f(ADD ? sacc[g][kb][8 * s + j] + add : sacc[g][kb][8 * s + j]);
+        f3bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ls4[j & 3] += e[j];
+          v[j] = (__bf16)e[j];
+        }
+        pf[g][kb][s] = v;
+      }
+    return (ls4[0] + ls4[1]) + (ls4[2] + ls4[3]);
+  };
+  // softmax of group g on its scores (lazy max: rescale only when the tile's row sum would exceed 2^8)
+  auto softmax = [&](int g, int key0) {
+    if ((key0 + KT > kv_len) || (CAUSAL && key0 + KT - 1 > q0 + c_off)) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          const bool bad = key >= kv_len || (CAUSAL && key > qi[g] + c_off);
+          sacc[g][kb][r] = bad ? -INFINITY : sacc[g][kb][r];
+        }
+    }
+    float ls = 0.f;
+    bool slow = __any(m_run[g] == -INFINITY);
+    if (!slow) {
+      ls = expo(g, 0.f, std::false_type{});
+      slow = __any(!(ls <= kSumThr));
+    }
+    if (slow) {
+      float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) m4[r & 3] = fmaxf(m4[r & 3], sacc[g][kb][r]);
+      const float mb = m_run[g] == -INFINITY ? 0.f : m_run[g];
+      float mloc = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64)) + mb;
+      uint32_t u = __float_as_uint(fmaxf(m_run[g], mloc));
+      if ((u & 0xffffu) != 0u && u != 0xff800000u) u = (u & 0x80000000u) ? (u & 0xffff0000u) : ((u + 0x10000u) & 0xffff0000u);
+      const float m_new = __uint_as_float(u);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = __builtin_amdgcn_exp2f(m_run[g] - m_use);
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[g][d][r] *= alpha;
+      l_run[g] *= alpha;
+      const float shift = mb - m_use;
+      m_run[g] = m_new;
+      const uint32_t nb = __float_as_uint(-(m_run[g] == -INFINITY ? 0.f : m_run[g])) >> 16;
+      b_negm[g] = __builtin_bit_cast(f3bf16x8, uint4_{lane < 32 ? nb : 0u, 0u, 0u, 0u});
+      ls = expo(g, shift, std::true_type{});
+    }
+    l_run[g] += ls;
+  };
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < ntiles) dma(cur ^ 1, t + 1);
+    const bf16_t* ks = smem + cur * 2 * KT * D;
+    const bf16_t* vs = ks + KT * D;
+    // scores of both groups: each K fragment feeds both
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const float16_ z = {};
+#pragma unroll
+      for (int g = 0; g < G; ++g) sacc[g][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, b_negm[g], z, 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const f3bf16x8 kf = *reinterpret_cast<const f3bf16x8*>(ks + koff[s] + kb * 2048);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+          sacc[g][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[g][s], sacc[g][kb], 0, 0, 0);
+      }
+    }
+    const int key0 = t * KT;
+    softmax(0, key0);
+    // group A's P.V (its MFMAs beside group B's softmax), then group B's; V fragments read once for both
+    f3bf16x8 vf[ND][2][2];
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16_t* a0 = vs + voff[d] + kb * 2048 + s * 1024;
+          const f3s4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) f3s4v*)(a0));
+          const f3s4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) f3s4v*)(a0 + 512));
+          short8 vv;
+          vv[0] = t0[0]; vv[1] = t0[1]; vv[2] = t0[2]; vv[3] = t0[3];
+          vv[4] = t1[0]; vv[5] = t1[1]; vv[6] = t1[2]; vv[7] = t1[3];
+          vf[d][kb][s] = __builtin_bit_cast(f3bf16x8, vv);
+          o[0][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[d][kb][s], pf[0][kb][s], o[0][d], 0, 0, 0);
+        }
+    softmax(1, key0);
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          o[1][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[d][kb][s], pf[1][kb][s], o[1][d], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const float l_tot = l_run[g] + __shfl_xor(l_run[g], 32, 64);
+    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+    if (qi[g] < q_len) {
+      bf16_t* op = p.o + (p.q_start ? (long)p.q_start[b] * p.o_ts : (long)b * p.o_bs) + (long)qi[g] * p.o_ts +
+                   (long)hq * D;
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          const int dd = d * 32 + 8 * gg + 4 * fh;
+          uint2_ w;
+          w[0] = pack2(o[g][d][4 * gg] * inv, o[g][d][4 * gg + 1] * inv);
+          w[1] = pack2(o[g][d][4 * gg + 2] * inv, o[g][d][4 * gg + 3] * inv);
+          *reinterpret_cast<uint2_*>(op + dd) = w;
+        }
+    }
+  }
+}
+
+void launch_flash64_x2(const AttnArgs& a, hipStream_t s) {
+  dim3 grid((a.Sq + 255) / 256, a.Hq, a.B);
+  const size_t lds = (size_t)2 * 2 * 64 * 64 * sizeof(bf16_t);
+  if (a.causal) flash64x2_kernel<true><<<grid, 256, lds, s>>>(a);
+  else flash64x2_kernel<false><<<grid, 256, lds, s>>>(a);
+}
+
 // Same contract as flash64 (attention.hip): D = 64, causal (+ offset), per-batch q / kv lengths, packed varlen
 // q / o, GQA; K / V rows addressed through 32-bit buffer offsets.
 bool flash64_dma_supported(const AttnArgs& a) {
@@ -235,16 +491,11 @@ bool flash64_dma_supported(const AttnArgs& a) {
          (long)a.Skv * a.k_ts * 2 < 0x7fffffffL && (long)a.Skv * a.v_ts * 2 < 0x7fffffffL;
 }
 
-void launch_flash64_dma(const AttnArgs& a, int occ, hipStream_t s) {
+void launch_flash64_dma(const AttnArgs& a, hipStream_t s) {
   dim3 grid((a.Sq + 127) / 128, a.Hq, a.B);
   const size_t lds = (size_t)2 * 2 * 64 * 64 * sizeof(bf16_t);
-  if (occ >= 4) {
-    if (a.causal) flash64_dma_kernel<4, true><<<grid, 256, lds, s>>>(a);
-    else flash64_dma_kernel<4, false><<<grid, 256, lds, s>>>(a);
-  } else {
-    if (a.causal) flash64_dma_kernel<2, true><<<grid, 256, lds, s>>>(a);
-    else flash64_dma_kernel<2, false><<<grid, 256, lds, s>>>(a);
-  }
+  if (a.causal) flash64_dma_kernel<2, true><<<grid, 256, lds, s>>>(a);
+  else flash64_dma_kernel<2, false><<<grid, 256, lds, s>>>(a);
 }
 
 }  // namespace shai

@@ -228,7 +228,10 @@ void launch_flash64(const AttnArgs& a, hipStream_t s);
 void launch_flash2(const AttnArgs& a, hipStream_t s);
 // flash64 with LDS-DMA K/V staging (attention3.hip; launch_flash64 routes to it, SHAI_FLASH64_DMA=0 opts out)
 bool flash64_dma_supported(const AttnArgs& a);
-void launch_flash64_dma(const AttnArgs& a, int occ, hipStream_t s);
+void launch_flash64_dma(const AttnArgs& a, hipStream_t s);
+// the same pipeline with two 32-query groups per wave (256 queries per workgroup, flash64_dma_supported contract;
+// launch_flash64 picks it for grids of >= 1024 such workgroups)
+void launch_flash64_x2(const AttnArgs& a, hipStream_t s);
 // D = 512 single-head fused attention (attention3.hip; the VAE mid-block)
 bool attn512_supported(const AttnArgs& a);
 void launch_attn512(const AttnArgs& a, hipStream_t s);

@@ -281,6 +281,26 @@ def test_flash2_d64_long_spikes_varlen(cuda, causal):
         close(o[b, :n], orf[b, :n], 2e-2)
 
 
+@pytest.mark.parametrize("causal", [False, True])
+def test_flash64_x2_large_grid(cuda, causal):
+    """D = 64 launches of >= 1024 256-query workgroups run the two-group kernel (flash64x2, attention3.hip):
+    spikes in the first tile and past the fast-path bound, per-batch lengths with partial query / key tiles,
+    GQA 4:1 -- against the fp32 reference."""
+    torch.manual_seed(17)
+    B, S, Hq, Hkv, D = 8, 1100, 32, 8, 64
+    q, k, v = rnd(B, S, Hq, D), rnd(B, S, Hkv, D), rnd(B, S, Hkv, D)
+    k[:, 3] = q[:, 700, :Hkv] * 3
+    k[:, 900] = q[:, 10, :Hkv] * 5
+    k[:, 513] = q[:, 600, :Hkv] * 0.7
+    kl = torch.tensor([1100, 1090, 1024, 777, 300, 1100, 65, 1000], device="cuda", dtype=torch.int32)
+    ql = kl.clone() if causal else None
+    o = ops.attention(q, k, v, causal=causal, kv_lens=kl, q_lens=ql)
+    orf = ref.attention(q, k, v, 1 / math.sqrt(D), causal, 0, kl, ql)
+    for b in range(B):
+        n = int((ql if ql is not None else torch.full_like(kl, S))[b])
+        close(o[b, :n], orf[b, :n], 2e-2)
+
+
 def test_flash2_causal_offset_chunk(cuda):
     """Chunked-prefill shape: 600 new queries attending causally over 1500 keys (offset 900)."""
     torch.manual_seed(15)

@@ -64,7 +64,7 @@ __global__ void ref_rows(const bf16_t* q, const bf16_t* k, const bf16_t* v, floa
 
 int main() {
   struct Case { int B, H, S, D; };
-  const Case cases[] = {{8, 5, 4096, 64}, {8, 10, 1024, 64}, {1, 24, 4608, 128}, {4, 32, 2048, 128}};
+  const Case cases[] = {{8, 5, 4096, 64}, {64, 5, 4096, 64}, {8, 10, 1024, 64}, {64, 10, 1024, 64}, {1, 24, 4608, 128}, {4, 32, 2048, 128}};
   setenv("SHAI_FLASH_V1", "1", 1);  // launch_flash_attn -> v1 kernel
   setenv("SHAI_FLASH64_DMA", "0", 1);  // launch_flash64 -> the register-staged kernel (the DMA one is its own row)
   hipEvent_t e0, e1;
@@ -94,7 +94,8 @@ int main() {
       for (int kv = 0; kv < (c.D == 64 ? 3 : 1); ++kv) {
       if (c.D == 64) {
         if (kv == 0) shai::launch_flash64(a, 0);  // production d64 kernel
-        else shai::launch_flash64_dma(a, kv == 1 ? 2 : 4, 0);
+        else if (kv == 2) shai::launch_flash64_x2(a, 0);
+        else shai::launch_flash64_dma(a, 0);
       } else shai::launch_flash2_exp(a, 0, 0);
       CK(hipDeviceSynchronize());
       std::vector<float> hr(rows * c.D);
@@ -110,12 +111,12 @@ int main() {
           err = fmax(err, fabs(f - hr[i * c.D + d]));
           mx = fmax(mx, fabs(hr[i * c.D + d]));
         }
-      printf("  %s max_abs_err %.4f (max |ref| %.3f) %s\n", c.D == 64 ? (kv == 0 ? "flash64" : kv == 1 ? "f64dma-occ2" : "f64dma-occ4") : "flash2", err, mx, err < 0.02 * mx + 0.01 ? "OK" : "MISMATCH");
+      printf("  %s max_abs_err %.4f (max |ref| %.3f) %s\n", c.D == 64 ? (kv == 0 ? "flash64" : kv == 1 ? "f64dma" : "f64x2") : "flash2", err, mx, err < 0.02 * mx + 0.01 ? "OK" : "MISMATCH");
       }
       CK(hipFree(ref));
     }
     struct V { const char* name; int exp; };  // exp < 0: v1
-    const V vars[] = {{"v1", -1}, {"flash2", 0}, {"flash64", -2}, {"f64dma-occ2", -3}, {"f64dma-occ4", -4}};
+    const V vars[] = {{"v1", -1}, {"flash2", 0}, {"flash64", -2}, {"f64dma", -3}, {"f64x2", -5}};
     constexpr int NV = sizeof(vars) / sizeof(vars[0]);
     float best[NV];
     for (int vi = 0; vi < NV; ++vi) best[vi] = 1e30f;
@@ -124,8 +125,8 @@ int main() {
         if (vars[vi].exp <= -3 && c.D != 64) continue;
         auto run = [&]() {
           if (vars[vi].exp == -2) { if (c.D == 64) shai::launch_flash64(a, 0); }
-          else if (vars[vi].exp == -3) shai::launch_flash64_dma(a, 2, 0);
-          else if (vars[vi].exp == -4) shai::launch_flash64_dma(a, 4, 0);
+          else if (vars[vi].exp == -3) shai::launch_flash64_dma(a, 0);
+          else if (vars[vi].exp == -5) shai::launch_flash64_x2(a, 0);
           else if (vars[vi].exp < 0) shai::launch_flash_attn(a, 0);
           else shai::launch_flash2_exp(a, vars[vi].exp, 0);
         };
