@@ -153,29 +153,7 @@ def create_app(engine=None, env: Optional[ServerEnv] = None, max_batch: Optional
     app = base_app(env, f"{env.model_id} SD2.1{title_suffix}", spaced=False)
     app.state.engine, app.state.worker = engine, worker
 
-    @app.get("/")
-    def read_main():
-        return {"message": "This is" + env.model_id + " pod " + env.pod_name + " in AWS EC2 " + env.device +
-                " instance; try /load/{n_runs}/infer/{n_inf}; /genimage http post with user prompt "}
-
-    @app.get("/load/{n_runs}/infer/{n_inf}")
-    def load(n_runs: int, n_inf: int):
-        _check(LOAD_PROMPT, n_inf)
-        t0 = time.time()
-        report = benchmark(n_runs, "stable_diffusion_512",
-                           lambda: worker.submit_batched(n_inf, LOAD_PROMPT).result(), env.pod_name)
-        METRICS.request_done(env, time.time() - t0)
-        return {"message": "benchmark report:" + report}
-
-    @app.post("/genimage")
-    def generate_image_post(request: dict):
-        prompt = request.get("prompt")
-        _check(prompt, env.num_inference_steps)
-        img, latency = text2img(prompt)
-        METRICS.request_done(env, float(latency))
-        return {"prompt": prompt, "response": png_b64(img), "latency": latency}
-
-    mount_ui(app, f"{env.model_id} on MI355X; pod {env.pod_name}", "/genimage", "{prompt: p}", output="image")
+    _routes(app, env, text2img, lambda n_inf: worker.submit_batched(n_inf, LOAD_PROMPT).result())
     return app
 
 

@@ -23,8 +23,11 @@ a heartbeat every ``HEARTBEAT_S`` seconds.
 
 Failure handling (a TP group is one unit: it serves or it is restarted whole):
 
-* a follower whose call fails with anything but a mirrored input error (``MIRRORED``: the leader raises the
-  same exception on the same inputs and reports it to its client) reports the failure to the leader on a
+* after every CALL the leader broadcasts its outcome (ok, or the type of the exception it raised); a follower
+  whose call fails stays in the group only when its exception is a mirrored input error (``MIRRORED``) AND the
+  leader raised the same type -- a rank-local ``KeyError`` thrown after a collective is not excused by the
+  leader's success -- and so does a follower whose call succeeded where the leader's failed with anything but a
+  mirrored error.  Any other follower failure is reported to the leader on a
   second gloo group and exits non-zero; ``torch.distributed.run`` then stops the other ranks and the
   supervisor relaunches the group.  The leader's status listener marks the process broken
   (``utils.liveness.mark_broken``: ``/health`` 503) the moment the report -- or the lost connection of a
@@ -50,7 +53,7 @@ from ..utils.logging import get_logger
 
 _log = get_logger("tp-serving")
 
-CALL, STEP, NOOP, STOP = 1, 2, 3, 4
+CALL, STEP, NOOP, STOP, OUTCOME = 1, 2, 3, 4, 5
 HEARTBEAT_S = float(os.environ.get("SHAI_TP_HEARTBEAT_S", "20"))
 LEADER_TIMEOUT_S = float(os.environ.get("SHAI_TP_LEADER_TIMEOUT_S", str(2 * HEARTBEAT_S + 5)))
 # exceptions a follower treats as mirrored on the leader (same inputs, same code -> the leader's client gets
@@ -147,8 +150,13 @@ class SPMDProxy:
         def call(*args, **kwargs):
             from ..parallel.comm import raise_if_p2p_error
             self._channel.send(CALL, (name, args, kwargs))
-            out = attr(*args, **kwargs)
-            raise_if_p2p_error()
+            try:
+                out = attr(*args, **kwargs)
+                raise_if_p2p_error()
+            except BaseException as e:
+                self._channel.send(OUTCOME, type(e).__name__)
+                raise
+            self._channel.send(OUTCOME, "")
             return out
         return call
 
@@ -190,12 +198,24 @@ class _LeaderWatchdog:
 
 def follow(target, channel: TPChannel, step_fn=None, leader_timeout_s: Optional[float] = None) -> int:
     """Follower main loop: execute the leader's calls until STOP.  ``step_fn(payload)`` handles STEP
-    messages (the LLM engine loop).  A CALL that raises a ``MIRRORED`` (input) error is logged and skipped --
-    the leader hits the same exception on the same inputs and reports it to its client.  Any other failure is
-    rank-local: it is reported to the leader and the process exits non-zero, so the group is restarted whole
-    instead of running on with mismatched collectives.  Returns the number of calls run."""
+    messages (the LLM engine loop).  After a CALL the follower waits for the leader's OUTCOME: a ``MIRRORED``
+    (input) error that the leader raised too is logged and skipped -- the leader reports it to its client.  Any
+    other divergence (a follower error the leader did not share, or a leader failure outside ``MIRRORED`` the
+    follower did not share) is rank-local: it is reported to the leader and the process exits non-zero, so the
+    group is restarted whole instead of running on with mismatched collectives.  Returns the number of calls."""
     n = 0
     dog = _LeaderWatchdog(LEADER_TIMEOUT_S if leader_timeout_s is None else leader_timeout_s)
+
+    def leader_outcome() -> str:
+        while True:  # heartbeats may land between the call and its outcome
+            dog.idle_since = time.monotonic()
+            kind, payload = channel.recv()
+            dog.idle_since = None
+            if kind == OUTCOME:
+                return payload or ""
+            if kind != NOOP:
+                raise RuntimeError(f"TP protocol: expected the leader's call outcome, got message kind {kind}")
+
     try:
         while True:
             dog.idle_since = time.monotonic()
@@ -203,8 +223,9 @@ def follow(target, channel: TPChannel, step_fn=None, leader_timeout_s: Optional[
             dog.idle_since = None
             if kind == STOP:
                 return n
-            if kind == NOOP:
+            if kind in (NOOP, OUTCOME):
                 continue
+            err = None
             try:
                 with torch.inference_mode():
                     if kind == CALL:
@@ -214,13 +235,26 @@ def follow(target, channel: TPChannel, step_fn=None, leader_timeout_s: Optional[
                         raise_if_p2p_error()
                     elif kind == STEP and step_fn is not None:
                         step_fn(payload)
-            except MIRRORED as e:
-                if kind != CALL:
+            except Exception as e:  # noqa: BLE001 -- classified against the leader's outcome below
+                err = e
+            if kind != CALL:
+                if err is not None:
+                    _fail(channel, err)
+            else:
+                try:
+                    lead = leader_outcome()
+                except Exception as e:  # noqa: BLE001
                     _fail(channel, e)
-                _log.warning("follower call failed (mirrored on the leader)",
-                             extra={"event": "follower_error", "detail": repr(e)[:300]})
-            except Exception as e:  # noqa: BLE001 -- rank-local: the group cannot continue
-                _fail(channel, e)
+                mine = type(err).__name__ if err is not None else ""
+                mirrored = {c.__name__ for c in MIRRORED}
+                if mine != lead and not (err is None and lead in mirrored):
+                    _fail(channel, err if err is not None else
+                          RuntimeError(f"leader failed with {lead} where this rank succeeded"))
+                if err is not None:
+                    if mine not in mirrored:
+                        _fail(channel, err)
+                    _log.warning("follower call failed (mirrored on the leader)",
+                                 extra={"event": "follower_error", "detail": repr(err)[:300]})
             n += 1
     finally:
         dog.stop()
