@@ -62,14 +62,19 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+// Activations divide with v_rcp_f32 (1 ulp): a plain '/' or __frcp_rn expands to the correctly rounded
+// v_div_scale / v_div_fmas / v_div_fixup sequence (~10 instructions), which made the GEGLU epilogue of the
+// W-stationary GEMM VALU-bound (120 such sequences per tile step).
+__device__ __forceinline__ float rcp_f(float x) { return __builtin_amdgcn_rcpf(x); }
+
+__device__ __forceinline__ float silu_f(float x) { return x * rcp_f(1.0f + __expf(-x)); }
 
 // erf via Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7, far below bf16 resolution): one exp, one
 // reciprocal and a degree-5 Horner chain instead of the libm erff polynomial + branches, which
 // made GEGLU epilogues VALU-bound.
 __device__ __forceinline__ float erf_fast(float x) {
   const float ax = fabsf(x);
-  const float t = __frcp_rn(fmaf(0.3275911f, ax, 1.0f));
+  const float t = rcp_f(fmaf(0.3275911f, ax, 1.0f));
   float y = fmaf(1.061405429f, t, -1.453152027f);
   y = fmaf(y, t, 1.421413741f);
   y = fmaf(y, t, -0.284496736f);
@@ -78,17 +83,30 @@ __device__ __forceinline__ float erf_fast(float x) {
   return copysignf(y, x);
 }
 
-__device__ __forceinline__ float gelu_erf_f(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
+// gelu(x) = x/2 + |x|/2 * erf(|x| / sqrt 2), the same 7.1.26 erf written for the GELU argument directly: the
+// 1/sqrt 2 and log2 e factors folded into the constants, the sign handled by the |x|/2 form (no copysign):
+// 13 VALU, 2 of them transcendental.
+__device__ __forceinline__ float gelu_erf_f(float x) {
+  const float hx = 0.5f * x;
+  const float t = rcp_f(fmaf(0.23164189f, fabsf(x), 1.0f));  // 0.3275911 / sqrt 2
+  const float e = __builtin_amdgcn_exp2f(x * x * -0.72134752f);  // exp(-x^2 / 2)
+  float y = fmaf(1.061405429f, t, -1.453152027f);
+  y = fmaf(y, t, 1.421413741f);
+  y = fmaf(y, t, -0.284496736f);
+  y = fmaf(y, t, 0.254829592f);
+  const float erf_abs = fmaf(-(y * t), e, 1.0f);
+  return fmaf(fabsf(hx), erf_abs, hx);
+}
 
 // tanh(u) = 1 - 2 / (1 + e^{2u}) (saturates correctly at +-1 for large |u|)
 __device__ __forceinline__ float gelu_tanh_f(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float u = k0 * fmaf(k1 * x, x * x, x);
-  const float th = 1.0f - 2.0f * __frcp_rn(1.0f + __expf(2.0f * u));
+  const float th = 1.0f - 2.0f * rcp_f(1.0f + __expf(2.0f * u));
   return 0.5f * x * (1.0f + th);
 }
 
-__device__ __forceinline__ float quick_gelu_f(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+__device__ __forceinline__ float quick_gelu_f(float x) { return x * rcp_f(1.0f + __expf(-1.702f * x)); }
 
 // smallest bf16-representable float >= x (finite x; -inf stays -inf): flash attention keeps its running max on
 // the bf16 grid so that -m can enter the score MFMA exactly as a bf16 operand
