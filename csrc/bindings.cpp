@@ -88,17 +88,22 @@ std::string gemm_bucket_key(const shai::GemmArgs& g) {
 }
 
 // exact key first, then the M bucket (a bucket hit is filed under the exact key too).  Caller holds no lock.
+bool lib_enabled();
+constexpr int kLibCfgId = 2000;  // = kLibCfg (below)
+
 bool lookup_choice(const shai::GemmArgs& g, const std::string& key, Choice* out) {
   std::lock_guard<std::mutex> lk(g_tune_mu);
+  // a cached library choice counts as untuned while the library path is off (the tuner races it afresh)
+  auto usable = [](const Choice& c) { return c.cfg != kLibCfgId || lib_enabled(); };
   auto it = g_tuned.find(key);
-  if (it != g_tuned.end()) {
+  if (it != g_tuned.end() && usable(it->second)) {
     *out = it->second;
     return true;
   }
   const std::string bk = gemm_bucket_key(g);
   if (bk.empty()) return false;
   it = g_tuned.find(bk);
-  if (it == g_tuned.end()) return false;
+  if (it == g_tuned.end() || !usable(it->second)) return false;
   *out = it->second;
   g_tuned[key] = it->second;
   return true;
@@ -127,10 +132,11 @@ bool autotune_enabled() {
   return on;
 }
 
-bool lib_enabled() {  // SHAI_GEMM_LIB=0 keeps every GEMM on the hand-written kernels
+bool lib_enabled() {  // off by default: every GEMM runs on the hand-written kernels; SHAI_GEMM_LIB=1 lets the
+                      // tuner race hipBLASLt again (A/B) and honours cached library choices
   static const bool on = [] {
     const char* e = getenv("SHAI_GEMM_LIB");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }
@@ -197,7 +203,7 @@ void launch_skinny_choice(const shai::GemmArgs& g, const Tensor& like, int kg, b
 // Choice.cfg of the library path: plain GEMMs (no fused epilogue beyond a bias or an unscaled residual) may
 // go to hipBLASLt through at::mm_out / at::addmm_out when the autotuner measures it faster than the tile
 // configs -- the hand-written kernels keep every fused-epilogue / conv / GLU / gated problem.
-constexpr int kLibCfg = 2000;
+constexpr int kLibCfg = kLibCfgId;
 
 
 void launch_lib(const shai::GemmArgs& g, const Tensor& like) {

@@ -596,6 +596,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
                 for (int ii = 0; ii < IG; ++ii) {
                   const int i = i0 + ii;
                   bf16_t* crow = C + (long)(m0 + wm * 128 + i * 16 + fr) * p.ldc + ((n0 + wn * WC) >> 1);
+                  uint32_t wq[NP][2];
 #pragma unroll
                   for (int q = 0; q < NP; ++q) {
                     float o[4];
@@ -609,10 +610,28 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
                       o[0] += bf2f(rr[ii][q][0] & 0xffff) * p.res_alpha; o[1] += bf2f(rr[ii][q][0] >> 16) * p.res_alpha;
                       o[2] += bf2f(rr[ii][q][1] & 0xffff) * p.res_alpha; o[3] += bf2f(rr[ii][q][1] >> 16) * p.res_alpha;
                     }
+                    wq[q][0] = pack2(o[0], o[1]);
+                    wq[q][1] = pack2(o[2], o[3]);
+                  }
+                  // column groups (2k, 2k + 1): lane quad fq holds outputs 4 fq .. of both; one v_permlane16_swap per
+                  // dword gives quads (0, 2) group 2k's and quads (1, 3) group 2k + 1's 8 consecutive outputs -> one
+                  // 16-B store per lane instead of two 8-B ones (the GEGLU epilogue is store-issue bound)
+#pragma unroll
+                  for (int q = 0; q + 1 < NP; q += 2) {
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                      const auto r = __builtin_amdgcn_permlane16_swap(wq[q][e], wq[q + 1][e], false, false);
+                      wq[q][e] = r[0];
+                      wq[q + 1][e] = r[1];
+                    }
+                    *reinterpret_cast<uint4_*>(crow + q * 16 + 16 * (fq & 1) + 8 * (fq >> 1)) =
+                        uint4_{wq[q][0], wq[q][1], wq[q + 1][0], wq[q + 1][1]};
+                  }
+                  if constexpr ((NP & 1) != 0) {
                     uint2_ w;
-                    w[0] = pack2(o[0], o[1]);
-                    w[1] = pack2(o[2], o[3]);
-                    *reinterpret_cast<uint2_*>(crow + q * 16 + 4 * fq) = w;
+                    w[0] = wq[NP - 1][0];
+                    w[1] = wq[NP - 1][1];
+                    *reinterpret_cast<uint2_*>(crow + (NP - 1) * 16 + 4 * fq) = w;
                   }
                   if constexpr (TAIL) {
                     float o0 = (acc[i][NJ - 1][0] * p.alpha + bt[0]) * apply_act<ACT>(acc[i][NJ - 1][1] * p.alpha + bt[1]);

@@ -324,6 +324,72 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(const GemmArgs p, int s
     }
   };
 
+  // ---- GLU epilogue unit rb of the i-th tile (BM = 64: RB = 4 units): the row block's three column groups, stored
+  // 16 B per lane.  Column groups 0 and 1 give each lane 4 + 4 outputs that are not adjacent; one v_permlane16_swap
+  // per dword pairs lane quads (0, 1) and (2, 3) so each lane holds 8 consecutive outputs of one group (quad fq: group
+  // fq & 1, outputs 8 (fq >> 1) ..).  Group 2 gives each lane one dword (2 outputs) per row block: they are parked in
+  // d2[rb] and, after the last unit, a 4 x 4 transpose across the lane quads (v_permlane32_swap, then 16) leaves lane
+  // quad fq with row block fq's 8 outputs.  RB + 1 store instructions per tile instead of 3 RB of 8 / 4 bytes: the
+  // GEGLU epilogue was store-issue bound.
+  auto epi_glu_unit = [&](const float4_ (&acc)[RB][WS_NB], int rb, int i, uint32_t (&d2)[RB]) {
+    const int m0 = (slot + S * i) * BM;
+    const long m = (long)m0 + 16 * rb + fr;
+    uint32_t w[3][2];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const LnPre ln = epi_pre(3 * rb + q, i);
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[rb][q < 2 ? 2 * q : 4][e];
+        v[4 + e] = q < 2 ? acc[rb][2 * q + 1][e] : 0.f;
+      }
+      if constexpr (LNF) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = ln.rstd * fmaf(-ln.mean, ln.sc[e], v[e]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaf(v[e], p.alpha, bq[q][e]);
+      if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) asm volatile("" ::"v"(v[e]));
+      }
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = v[2 * e] * apply_act<ACT>(v[2 * e + 1]);
+      w[q][0] = ws_pk(o[0], o[1]);
+      w[q][1] = ws_pk(o[2], o[3]);
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const auto r = __builtin_amdgcn_permlane16_swap(w[0][e], w[1][e], false, false);
+      w[0][e] = r[0];
+      w[1][e] = r[1];
+    }
+    const int ob = (n0 + cw) >> 1;  // the wave's first output column
+    if (m < p.M && !(ABL & 1))
+      *reinterpret_cast<uint4_*>(p.C + m * p.ldc + ob + 16 * (fq & 1) + 8 * (fq >> 1)) =
+          uint4_{w[0][0], w[0][1], w[1][0], w[1][1]};
+    d2[rb] = w[2][0];
+    if (rb == RB - 1) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const auto r = __builtin_amdgcn_permlane32_swap(d2[e], d2[2 + e], false, false);
+        d2[e] = r[0];
+        d2[2 + e] = r[1];
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const auto r = __builtin_amdgcn_permlane16_swap(d2[2 * e], d2[2 * e + 1], false, false);
+        d2[2 * e] = r[0];
+        d2[2 * e + 1] = r[1];
+      }
+      const long m2 = (long)m0 + 16 * fq + fr;
+      if (m2 < p.M && !(ABL & 1))
+        *reinterpret_cast<uint4_*>(p.C + m2 * p.ldc + ob + 32) = uint4_{d2[0], d2[1], d2[2], d2[3]};
+    }
+  };
+
   // ---- LNO epilogue of the i-th tile (residual builds, no activation): y = acc + bias + res_alpha R stored to C,
   // then the row moments of the stored bf16 y across the 4 waves (LDS, raw barriers: an LDS-DMA prefetch is in
   // flight) and C2 = LayerNorm(y) gamma + beta
@@ -449,9 +515,12 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(const GemmArgs p, int s
   // chunks run between this tile's MFMA groups.  Otherwise (plain / bias / residual: a few VALU per output) each tile's
   // epilogue follows its own MFMAs, which measured faster there (round-5 lab: no second accumulator set to keep).
   constexpr bool IL = GLU;
+  static_assert(!GLU || RB == 4, "the GLU epilogue's lane-quad transpose assumes 4 row blocks");
+  constexpr int NU = GLU ? RB : T::NCH;        // epilogue units per tile
+  constexpr int NST = GLU ? RB + 1 : T::NST;   // store instructions per wave per full tile
   auto tile = [&](float4_ (&acc)[RB][WS_NB], const float4_ (&prev)[RB][WS_NB], int i) {
     // outstanding after tile i's DMA: tile i + 1's DMA and the stores of tiles i - 2 and i - 1
-    if (i >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T::DMA + 2 * T::NST) : "memory");
+    if (i >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T::DMA + 2 * NST) : "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T::DMA) : "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slots restaged next are done
     __builtin_amdgcn_sched_barrier(0);
@@ -466,6 +535,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(const GemmArgs p, int s
     // the previous tile's accumulators (consumed by the epilogue chunks in the first half of the steps) and this
     // tile's share registers: at most 1.5 accumulator sets are live.
     constexpr int NSTEP = RB * KS;
+    uint32_t d2[RB];  // GLU: group-2 dwords of the previous tile's row blocks, stored after its last unit
     wsbf16x8 xr[3];
     xr[0] = *reinterpret_cast<const wsbf16x8*>(sa + xaddr(0, 0));
     xr[1] = *reinterpret_cast<const wsbf16x8*>(sa + xaddr(1 / KS, 1 % KS));
@@ -473,11 +543,6 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(const GemmArgs p, int s
     for (int st = 0; st < NSTEP; ++st) {
       const int rb = st / KS, s = st % KS;
       if (st + 2 < NSTEP) xr[(st + 2) % 3] = *reinterpret_cast<const wsbf16x8*>(sa + xaddr((st + 2) / KS, (st + 2) % KS));
-      // LayerNorm constants of the chunk placed after this step's MFMAs: read now, used after them
-      LnPre lpre[T::NCH > 0 ? 1 : 1];
-#pragma unroll
-      for (int c = 0; c < T::NCH; ++c)
-        if (IL && LNF && st == (c * (NSTEP / 2)) / T::NCH && has_prev) lpre[0] = epi_pre(c, i - 1);
       __builtin_amdgcn_sched_barrier(0);  // the read two steps ahead goes out before this step's MFMAs
       const wsbf16x8& xc = xr[st % 3];
 #pragma unroll
@@ -492,13 +557,15 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(const GemmArgs p, int s
           asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[rb][j]) : "a"(wf[j][s]), "v"(xc));
       }
       asm volatile("s_nop 1" ::: "memory");  // WAR margin: a later read may land in this step's X registers
-      // epilogue chunks of the previous tile, spread over the first half of the steps
+      // epilogue units of the previous tile, spread over the first half of the steps
+      if constexpr (IL) {
 #pragma unroll
-      for (int c = 0; c < T::NCH; ++c) {
-        if (IL && st == (c * (NSTEP / 2)) / T::NCH) {
-          __builtin_amdgcn_sched_barrier(0);
-          if (IL && has_prev) epi_chunk(prev, c, i - 1, lpre[0]);
-          __builtin_amdgcn_sched_barrier(0);
+        for (int c = 0; c < NU; ++c) {
+          if (st == (c * (NSTEP / 2)) / NU) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (has_prev) epi_glu_unit(prev, c, i - 1, d2);
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
       }
     }
@@ -524,12 +591,15 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(const GemmArgs p, int s
   }
   // the last tile's epilogue (its MFMA results: s_nops for the VALU reads)
   asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-  if (IL && i_end > 0) {
-    const int il = i_end - 1;
+  if constexpr (IL) {
+    if (i_end > 0) {
+      const int il = i_end - 1;
+      uint32_t d2[RB];
 #pragma unroll
-    for (int c = 0; c < T::NCH; ++c) {
-      if (il & 1) epi_chunk(accB, c, il, epi_pre(c, il));
-      else epi_chunk(accA, c, il, epi_pre(c, il));
+      for (int c = 0; c < NU; ++c) {
+        if (il & 1) epi_glu_unit(accB, c, il, d2);
+        else epi_glu_unit(accA, c, il, d2);
+      }
     }
   }
   // every LDS-DMA of this workgroup (prefetches past the end included) lands before the LDS is released
