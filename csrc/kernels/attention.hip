@@ -525,7 +525,8 @@ void launch_flash64(const AttnArgs& a, hipStream_t s) {
   }();
   if (dma && flash64_dma_supported(a)) {
     // two 32-query groups per wave when the 256-query grid still fills the chip several times over
-    if ((long)((a.Sq + 255) / 256) * a.Hq * a.B >= 1024) launch_flash64_x2(a, s);
+    // (short key ranges -- SD2.1 cross-attention over 77 text tokens -- stay on the 128-query kernel: 123 vs 142 us)
+    if ((long)((a.Sq + 255) / 256) * a.Hq * a.B >= 1024 && a.Skv >= 512) launch_flash64_x2(a, s);
     else launch_flash64_dma(a, s);
     return;
   }

@@ -237,11 +237,13 @@ __global__ void __launch_bounds__(256, OCC) flash64_dma_kernel(const AttnArgs p)
   }
 }
 
-// flash64x2: the same K/V pipeline with TWO groups of 32 queries per wave (64 per wave, 256 per workgroup).  Each K /
-// V fragment read out of LDS feeds both groups' MFMAs (half the LDS traffic per FLOP), and the two groups' chains are
-// independent: group B's score MFMAs are in the matrix pipe while group A's softmax runs on the VALU, and A's P.V
-// MFMAs beside B's softmax -- the overlap a single 32-query chain (QK -> softmax -> PV, each waiting on the last)
-// can only get from other waves.  2 waves / SIMD (<= 256 registers).
+// flash64x2: the same K/V pipeline with TWO groups of 32 queries per wave (64 per wave, 256 per workgroup).  The two
+// groups' chains are independent: group B's score MFMAs are in the matrix pipe while group A's exponentials run on the
+// VALU, and A's P.V MFMAs beside B's exponentials (each V fragment read once for both) -- the overlap a single
+// 32-query chain (QK -> softmax -> PV, each waiting on the last) can only get from other waves.  The softmax fast path
+// is branch-free (the mask and the lazy-max rescale run after it, on a wave-uniform branch), which keeps each pair in
+// one basic block: round-5 lab, same box, 1397 vs 1443 us at B64 H5 S4096 and 209 vs 225 us at B64 H10 S1024 for
+// the branchy order (QK both -> softmax A -> PV A -> softmax B -> PV B).  2 waves / SIMD (<= 256 registers).
 template <bool CAUSAL>
 __global__ void __launch_bounds__(256, 2) flash64x2_kernel(const AttnArgs p) {
   constexpr int D = 64, KT = 64, NS = 4, ND = 2, G = 2;
@@ -358,25 +360,30 @@ __global__ void __launch_bounds__(256, 2) flash64x2_kernel(const AttnArgs p) {
       }
     return (ls4[0] + ls4[1]) + (ls4[2] + ls4[3]);
   };
-  // softmax of group g on its scores (lazy max: rescale only when the tile's row sum would exceed 2^8)
-  auto softmax = [&](int g, int key0) {
-    if ((key0 + KT > kv_len) || (CAUSAL && key0 + KT - 1 > q0 + c_off)) {
+  // the slow path of group g's softmax for the tile at key0 (lazy max: rescale only when the tile's row sum would
+  // exceed 2^8), after a branch-free fast path (ls_fast, pf[g] already computed): masking and the rescale only here,
+  // so the fast path's exponentials share a basic block with the other group's MFMAs and the scheduler can
+  // interleave them
+  auto check = [&](int g, int key0, float ls_fast) {
+    const bool mask = (key0 + KT > kv_len) || (CAUSAL && key0 + KT - 1 > q0 + wid * 64 + 32 * g + c_off);
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+    for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-          const bool bad = key >= kv_len || (CAUSAL && key > qi[g] + c_off);
-          sacc[g][kb][r] = bad ? -INFINITY : sacc[g][kb][r];
-        }
-    }
-    float ls = 0.f;
-    bool slow = __any(m_run[g] == -INFINITY);
-    if (!slow) {
-      ls = expo(g, 0.f, std::false_type{});
-      slow = __any(!(ls <= kSumThr));
-    }
-    if (slow) {
+      for (int s2 = 0; s2 < 2; ++s2) asm volatile("" ::"v"(pf[g][kb][s2]));
+    asm volatile("" ::"v"(ls_fast));
+    const uint64_t slow_lanes = __ballot(m_run[g] == -INFINITY) | __ballot(!(ls_fast <= kSumThr));
+    float ls = ls_fast;
+    if (mask | (slow_lanes != 0)) {
+      if (mask) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+            const bool bad = key >= kv_len || (CAUSAL && key > qi[g] + c_off);
+            sacc[g][kb][r] = bad ? -INFINITY : sacc[g][kb][r];
+          }
+      }
       float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
@@ -403,6 +410,18 @@ __global__ void __launch_bounds__(256, 2) flash64x2_kernel(const AttnArgs p) {
     }
     l_run[g] += ls;
   };
+  auto qk1 = [&](int g, const bf16_t* ks) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const float16_ z = {};
+      sacc[g][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, b_negm[g], z, 0, 0, 0);
+#pragma unroll
+      for (int s2 = 0; s2 < NS; ++s2) {
+        const f3bf16x8 kf = *reinterpret_cast<const f3bf16x8*>(ks + koff[s2] + kb * 2048);
+        sacc[g][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[g][s2], sacc[g][kb], 0, 0, 0);
+      }
+    }
+  };
 
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
@@ -412,48 +431,37 @@ __global__ void __launch_bounds__(256, 2) flash64x2_kernel(const AttnArgs p) {
     if (t + 1 < ntiles) dma(cur ^ 1, t + 1);
     const bf16_t* ks = smem + cur * 2 * KT * D;
     const bf16_t* vs = ks + KT * D;
-    // scores of both groups: each K fragment feeds both
+    {
+      // QK_A; then QK_B beside A's exponentials; A's P.V beside B's exponentials; B's P.V
+      const int key0 = t * KT;
+      qk1(0, ks);
+      qk1(1, ks);
+      const float ls0 = expo(0, 0.f, std::false_type{});
+      check(0, key0, ls0);
+      f3bf16x8 vf[ND][2][2];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const float16_ z = {};
+      for (int d = 0; d < ND; ++d)
 #pragma unroll
-      for (int g = 0; g < G; ++g) sacc[g][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, b_negm[g], z, 0, 0, 0);
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const f3bf16x8 kf = *reinterpret_cast<const f3bf16x8*>(ks + koff[s] + kb * 2048);
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const bf16_t* a0 = vs + voff[d] + kb * 2048 + s2 * 1024;
+            const f3s4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) f3s4v*)(a0));
+            const f3s4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) f3s4v*)(a0 + 512));
+            vf[d][kb][s2] = __builtin_bit_cast(f3bf16x8, __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7));
+            o[0][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[d][kb][s2], pf[0][kb][s2], o[0][d], 0, 0, 0);
+          }
+      const float ls1 = expo(1, 0.f, std::false_type{});
+      check(1, key0, ls1);
 #pragma unroll
-        for (int g = 0; g < G; ++g)
-          sacc[g][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[g][s], sacc[g][kb], 0, 0, 0);
-      }
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2)
+            o[1][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[d][kb][s2], pf[1][kb][s2], o[1][d], 0, 0, 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    const int key0 = t * KT;
-    softmax(0, key0);
-    // group A's P.V (its MFMAs beside group B's softmax), then group B's; V fragments read once for both
-    f3bf16x8 vf[ND][2][2];
-#pragma unroll
-    for (int d = 0; d < ND; ++d)
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const bf16_t* a0 = vs + voff[d] + kb * 2048 + s * 1024;
-          const f3s4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) f3s4v*)(a0));
-          const f3s4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) f3s4v*)(a0 + 512));
-          short8 vv;
-          vv[0] = t0[0]; vv[1] = t0[1]; vv[2] = t0[2]; vv[3] = t0[3];
-          vv[4] = t1[0]; vv[5] = t1[1]; vv[6] = t1[2]; vv[7] = t1[3];
-          vf[d][kb][s] = __builtin_bit_cast(f3bf16x8, vv);
-          o[0][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[d][kb][s], pf[0][kb][s], o[0][d], 0, 0, 0);
-        }
-    softmax(1, key0);
-#pragma unroll
-    for (int d = 0; d < ND; ++d)
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-          o[1][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[d][kb][s], pf[1][kb][s], o[1][d], 0, 0, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
 
 #pragma unroll
