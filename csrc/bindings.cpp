@@ -394,6 +394,15 @@ void launch_final(shai::GemmArgs g, const Tensor& like, const Choice& c, const O
       g.row_part = rp.data_ptr<float>();
     }
   }
+  // a split-K v2 tile choice: its fold kernel writes the GroupNorm partials (no pass over the output;
+  // SHAI_FOLD_GN=0: the separate col_partials pass)
+  static const bool fold_gn = [] {
+    const char* e = getenv("SHAI_FOLD_GN");
+    return !(e && e[0] == '0');
+  }();
+  if (fold_gn && !v4 && st->gn_part && c.splits > 1 && c.cfg >= 0 && c.cfg < 5 && shai::gemm2_cfg_supported(g, c.cfg) &&
+      shai::splitk_reduce_gn_ok(g) && !g.row_mr)
+    g.col_part = st->gn_part;
   launch_choice(g, like, c);
   if (st->gn_part && g.col_part == nullptr) shai::launch_col_partials(g.C, g.M, g.N, g.ldc, st->gn_part, stream());
   if (st->ln_mr) {
@@ -863,12 +872,17 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
     return;
   }
   if (ln_mr.has_value() || gn_part.has_value() || ln_stats.has_value()) {
-    SHAI_CHECK(!batched && g.gate == nullptr && (force_cfg < 0 || force_cfg < shai::gemm2_num_cfgs()),
+    SHAI_CHECK(!batched && g.gate == nullptr &&
+                   (force_cfg < 0 || force_cfg < shai::gemm2_num_cfgs() || (force_cfg >= 3000 && force_cfg < 4000)),
                "folded LayerNorm / output statistics: 2D, ungated GEMMs on the tile kernels");
     SHAI_CHECK(!glu || (!gn_part.has_value() && !ln_stats.has_value()), "output statistics of a GLU GEMM");
     OutStats st;
     attach_norm_io(g, ln_mr, ln_s, gn_part, ln_stats, ln_eps, &st);
-    if (force_cfg >= 0) {
+    if (force_cfg >= 3000) {  // tests: a split-K tile choice (the fold writes the GroupNorm partials)
+      const int cfg = (int)((force_cfg - 3000) % 100), splits = (int)((force_cfg - 3000) / 100);
+      SHAI_CHECK(cfg < shai::gemm2_num_cfgs() && shai::gemm2_cfg_supported(g, cfg) && splits >= 1, "bad forced split");
+      launch_final(g, a, Choice{cfg, splits}, &st);
+    } else if (force_cfg >= 0) {
       SHAI_CHECK(shai::gemm2_cfg_supported(g, force_cfg), "bad force_cfg");
       launch_final(g, a, Choice{(int)force_cfg, 1}, &st);
     } else {

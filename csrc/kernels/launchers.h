@@ -47,6 +47,7 @@ void launch_groupnorm_apply(const GroupNormArgs& a, hipStream_t s);
 // Norm statistics produced by a GEMM epilogue (GemmArgs::col_part / row_part) and their fallback passes:
 //   col partials [M / 128, N, 2] (sum, sum of squares per 128-row block and column) of x [M, N] (row stride ldx)
 void launch_col_partials(const bf16_t* x, long M, int N, long ldx, float* part, hipStream_t s);
+
 //   GroupNorm (scale, shift) [Nimg, C1 + C2] from the col partials of x (C1 channels) and optional x2 (C2)
 void launch_gn_from_partials(const float* part1, int C1, const float* part2, int C2, int Nimg, int HW, int G,
                              const bf16_t* gamma, const bf16_t* beta, float eps, float* scale, float* shift,
@@ -177,6 +178,8 @@ void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipS
 // v4: 8-phase ping-pong 256x256 / 256x320 LDS-DMA GEMM / conv (gemm_8ph.hip); config indices
 // gemm2_num_cfgs() - 2 (bn 256) and - 1 (bn 320)
 bool gemm4_supported(const GemmArgs& a);
+// the split-K fold of the v2 tiles writes GemmArgs::col_part itself when this holds (plain epilogue, M % 128 == 0)
+bool splitk_reduce_gn_ok(const GemmArgs& a);
 // every tile of this problem takes the v4 wide epilogue (the only path that writes col_part / row_part)
 bool gemm4_stats_ok(const GemmArgs& a, int bn);
 void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t s, bool persist = false);
