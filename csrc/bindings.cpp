@@ -394,15 +394,6 @@ void launch_final(shai::GemmArgs g, const Tensor& like, const Choice& c, const O
       g.row_part = rp.data_ptr<float>();
     }
   }
-  // a split-K v2 tile choice: its fold kernel writes the GroupNorm partials (no pass over the output;
-  // SHAI_FOLD_GN=0: the separate col_partials pass)
-  static const bool fold_gn = [] {
-    const char* e = getenv("SHAI_FOLD_GN");
-    return !(e && e[0] == '0');
-  }();
-  if (fold_gn && !v4 && st->gn_part && c.splits > 1 && c.cfg >= 0 && c.cfg < 5 && shai::gemm2_cfg_supported(g, c.cfg) &&
-      shai::splitk_reduce_gn_ok(g) && !g.row_mr)
-    g.col_part = st->gn_part;
   launch_choice(g, like, c);
   if (st->gn_part && g.col_part == nullptr) shai::launch_col_partials(g.C, g.M, g.N, g.ldc, st->gn_part, stream());
   if (st->ln_mr) {

@@ -502,7 +502,9 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
                 for (int ii = 0; ii < IG; ++ii) {
                   const int i = i0 + ii;
                   bf16_t* crow = C + (long)(m0 + wm * 128 + i * 16 + fr) * p.ldc + n0 + wn * WC;
-                  float rs = 0.f, rq = 0.f;  // row statistics of this lane's columns
+                  // row statistics of this lane's columns, shifted by the row's first stored value in this
+                  // slot (lane fq = 0, column 0): (mean, M2) per slot, combined exactly by the finalizer
+                  float rs = 0.f, rq = 0.f, rk = 0.f;
 #pragma unroll
                   for (int q = 0; q < NP; ++q) {
                     float v[8];
@@ -523,10 +525,12 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
                     if (rowp) {  // moments of the stored (bf16-rounded) values: what the consumer reads
                       float f[8];
                       unpack8(pv, f);
+                      if (q == 0) rk = __shfl(f[0], fr, 64);
 #pragma unroll
                       for (int e = 0; e < 8; ++e) {
-                        rs += f[e];
-                        rq = fmaf(f[e], f[e], rq);
+                        const float d = f[e] - rk;
+                        rs += d;
+                        rq = fmaf(d, d, rq);
                       }
                     }
                   }
@@ -547,8 +551,9 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
                       const float f[4] = {bf2f(o[0] & 0xffff), bf2f(o[0] >> 16), bf2f(o[1] & 0xffff), bf2f(o[1] >> 16)};
 #pragma unroll
                       for (int e = 0; e < 4; ++e) {
-                        rs += f[e];
-                        rq = fmaf(f[e], f[e], rq);
+                        const float d = f[e] - rk;
+                        rs += d;
+                        rq = fmaf(d, d, rq);
                       }
                     }
                   }
@@ -560,7 +565,9 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
                     if (fq == 0) {
                       const long m = m0 + wm * 128 + i * 16 + fr;
                       const int slot = (n0 / BN) * 4 + wn;
-                      *reinterpret_cast<float2*>(rowp + (m * p.row_part_slots + slot) * 2) = make_float2(rs, rq);
+                      constexpr float inv_wc = 1.f / WC;  // the slot's column count
+                      *reinterpret_cast<float2*>(rowp + (m * p.row_part_slots + slot) * 2) =
+                          make_float2(rk + rs * inv_wc, fmaxf(rq - rs * rs * inv_wc, 0.f));
                     }
                   }
                 }

@@ -441,84 +441,6 @@ __global__ void gemm_splitk_reduce(const GemmArgs p, const float* __restrict__ w
   }
 }
 
-// The same fold when the output feeds a GroupNorm (GemmArgs::col_part set by the host: the split-K v2 tiles, whose
-// epilogue writes no statistics): the GroupNorm partials [M / 128, N, 2] of the stored (bf16) output come out of the
-// fold instead of a separate col_partials pass over it.  Block = one 128-row block x 64 columns: 16 column quads x
-// 16 row lanes of 8 rows, each lane's 4 rows x 4 slabs of loads issued together (a serial row loop per thread was
-// latency-bound); plain (non-GLU) epilogues, M % 128 == 0, N % 8 == 0.
-template <int ACT>
-__global__ void __launch_bounds__(256) gemm_splitk_reduce_gn(const GemmArgs p, const float* __restrict__ ws,
-                                                             int splits) {
-  __shared__ float4_ red[16][16][2];
-  const int t = threadIdx.x, c4 = t & 15, rl = t >> 4;
-  const int n = blockIdx.y * 64 + 4 * c4;
-  const long r0 = (long)blockIdx.x * 128 + rl * 8;
-  const long slab = (long)p.M * p.N;
-  float4_ s = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
-  if (n < p.N) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float v[4][4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[r][e] = 0.f;
-      for (int s0 = 0; s0 < splits; s0 += 4) {
-        float4_ x[4][4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            x[r][u] = s0 + u < splits ? *reinterpret_cast<const float4_*>(ws + (s0 + u) * slab + (r0 + 4 * h + r) * p.N + n)
-                                      : float4_{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[r][e] += x[r][u][e];
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const long m = r0 + 4 * h + r;
-        if (p.rms) {
-          const float* ss = ws + (long)splits * p.M * p.N;
-          float tt = 0.f;
-          for (int k = 0; k < splits; ++k) tt += ss[(long)k * p.M + m];
-          const float rr = rsqrtf(tt / p.K + p.rms_eps);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[r][e] *= rr;
-        }
-        epilogue4<false, ACT>(p, p.C, p.residual, (int)m, n, v[r]);  // v <- the stored values before rounding
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float f = bf2f(f2bf(v[r][e]));  // moments of the stored bf16 output: what the consumer reads
-          s[e] += f;
-          q[e] = fmaf(f, f, q[e]);
-        }
-      }
-    }
-  }
-  red[rl][c4][0] = s;
-  red[rl][c4][1] = q;
-  __syncthreads();
-  if (rl == 0 && n < p.N) {
-#pragma unroll
-    for (int l = 1; l < 16; ++l) {
-      s += red[l][c4][0];
-      q += red[l][c4][1];
-    }
-    float4_* dst = reinterpret_cast<float4_*>(p.col_part + ((long)blockIdx.x * p.N + n) * 2);
-    dst[0] = float4_{s[0], q[0], s[1], q[1]};
-    dst[1] = float4_{s[2], q[2], s[3], q[3]};
-  }
-}
-
-bool splitk_reduce_gn_ok(const GemmArgs& a) {
-  return !a.glu && a.gate == nullptr && a.M % 128 == 0 && a.N % 8 == 0 && a.N <= 2048 && (a.ldc & 3) == 0 &&
-         (a.residual == nullptr || (a.ldr & 3) == 0) && a.batch <= 1;
-}
-
 // ---------------------------------------------------------------------------- dispatch
 static int g_stages() {
   static int st = [] {
@@ -581,12 +503,6 @@ static void launch_tiles(const GemmArgs& a, int cfg, float* ws, int splits, int 
 
 template <bool GLU, int ACT>
 static void launch_reduce(const GemmArgs& a, const float* ws, int splits, hipStream_t s) {
-  if constexpr (!GLU) {
-    if (a.col_part != nullptr && splitk_reduce_gn_ok(a)) {
-      gemm_splitk_reduce_gn<ACT><<<dim3((unsigned)(a.M / 128), (unsigned)((a.N + 63) / 64)), 256, 0, s>>>(a, ws, splits);
-      return;
-    }
-  }
   const long total = (long)a.M * ((a.N + 3) / 4);
   long blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
@@ -661,8 +577,7 @@ static void launch_all(const GemmArgs& a, float* ws, int cfg, int splits, hipStr
   }();
   unsigned* cnt = nullptr;
   // (not at 128 x 128: the fixup's registers would halve that config's occupancy)
-  if (splits > 1 && (cfg == 2 || cfg == 4) && fixup_on && !a.rms && a.col_part == nullptr &&
-      (long)splits * a.M * a.N * 4 < 0x7fffffffL) {
+  if (splits > 1 && (cfg == 2 || cfg == 4) && fixup_on && !a.rms && (long)splits * a.M * a.N * 4 < 0x7fffffffL) {
     const int bm = cfg == 2 ? 256 : 128, bn = cfg == 4 ? 64 : 128;
     const long tiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
     if (tiles <= 4096) cnt = skinny_ticket_slice(s, (int)tiles);

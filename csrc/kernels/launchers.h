@@ -178,8 +178,6 @@ void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipS
 // v4: 8-phase ping-pong 256x256 / 256x320 LDS-DMA GEMM / conv (gemm_8ph.hip); config indices
 // gemm2_num_cfgs() - 2 (bn 256) and - 1 (bn 320)
 bool gemm4_supported(const GemmArgs& a);
-// the split-K fold of the v2 tiles writes GemmArgs::col_part itself when this holds (plain epilogue, M % 128 == 0)
-bool splitk_reduce_gn_ok(const GemmArgs& a);
 // every tile of this problem takes the v4 wide epilogue (the only path that writes col_part / row_part)
 bool gemm4_stats_ok(const GemmArgs& a, int bn);
 void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t s, bool persist = false);

@@ -654,15 +654,18 @@ __global__ void __launch_bounds__(256) row_moments_part_kernel(const float* __re
                                                                float inv_n, float eps, float* __restrict__ mr) {
   const long m = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (m >= M) return;
+  // slot k holds (mean_k, M2_k) of its N / slots columns (equal counts): Chan's combination, no E[x^2] - mean^2
   const float2* src = reinterpret_cast<const float2*>(part) + m * slots;
-  float a = 0.f, b = 0.f;
+  float a = 0.f;
+  for (int k = 0; k < slots; ++k) a += src[k].x;
+  const float mean = a / slots;
+  float m2 = 0.f;
   for (int k = 0; k < slots; ++k) {
     const float2 v = src[k];
-    a += v.x;
-    b += v.y;
+    const float d = v.x - mean;
+    m2 += v.y + d * d * (1.f / (inv_n * slots));  // n_k = N / slots
   }
-  const float mean = a * inv_n;
-  const float var = fmaxf(b * inv_n - mean * mean, 0.f);
+  const float var = fmaxf(m2 * inv_n, 0.f);
   *reinterpret_cast<float2*>(mr + 2 * m) = make_float2(mean, rsqrtf(var + eps));
 }
 
@@ -678,14 +681,17 @@ __global__ void __launch_bounds__(256) row_moments_kernel(const bf16_t* __restri
   const long m = blockIdx.x * 4L + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (m >= M) return;
+  // sums shifted by the row's first value: no catastrophic cancellation for rows with |mean| >> std
+  const float k0 = bf2f(x[m * ldx]);
   float a = 0.f, b = 0.f;
   for (int c = lane * 8; c < N; c += 512) {
     float f[8];
     unpack8(*reinterpret_cast<const uint4_*>(x + m * ldx + c), f);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      a += f[e];
-      b = fmaf(f[e], f[e], b);
+      const float d = f[e] - k0;
+      a += d;
+      b = fmaf(d, d, b);
     }
   }
 #pragma unroll
@@ -694,9 +700,9 @@ __global__ void __launch_bounds__(256) row_moments_kernel(const bf16_t* __restri
     b += __shfl_xor(b, o, 64);
   }
   if (lane == 0) {
-    const float mean = a / N;
-    const float var = fmaxf(b / N - mean * mean, 0.f);
-    *reinterpret_cast<float2*>(mr + 2 * m) = make_float2(mean, rsqrtf(var + eps));
+    const float ms = a / N;
+    const float var = fmaxf(b / N - ms * ms, 0.f);
+    *reinterpret_cast<float2*>(mr + 2 * m) = make_float2(k0 + ms, rsqrtf(var + eps));
   }
 }
 

@@ -36,28 +36,22 @@ def test_gemm_gn_partials(cuda, cfg, M, N, K):
     assert rel(part, ref.col_partials(y)) < 1e-5
 
 
-@pytest.mark.parametrize("force", [3204, 3302, 3503])
-@pytest.mark.parametrize("M,N,K,act", [(4096, 320, 640, None), (1024, 1280, 2560, "silu"), (512, 2048, 1024, None)])
-def test_splitk_fold_gn_partials(cuda, force, M, N, K, act):
-    """Split-K v2 tiles (forced: 3000 + 100 splits + cfg): the fold kernel writes the GroupNorm partials of the
-    stored output (bias, residual, activation in its epilogue) instead of a separate col_partials pass."""
-    torch.manual_seed(7)
-    x, w, b, r = rnd(M, K), rnd(N, K, scale=0.05), rnd(N), rnd(M, N)
-    y, part = ops.linear_stats(x, w, b, residual=r, act=act, stats="gn", force_cfg=force)
-    assert rel(y, ref.linear(x, w, b, act, r)) < 1e-2
-    assert part.shape == (M // 128, N, 2)
-    assert rel(part, ref.col_partials(y)) < 1e-5
-
-
+@pytest.mark.parametrize("dc", [0.0, 100.0])
 @pytest.mark.parametrize("cfg", [9, 10, 11, 12, 0])
 @pytest.mark.parametrize("M,N,K", [(4096, 320, 320), (3000, 640, 320)])
-def test_gemm_ln_moments(cuda, cfg, M, N, K):
+def test_gemm_ln_moments(cuda, cfg, M, N, K, dc):
+    """LayerNorm moments of a GEMM output from the v4 epilogue (per-slot shifted (mean, M2), Chan-combined) or the
+    fallback pass (sums shifted by the row's first value); dc = a large per-row offset (|mean| / std ~ 100), where
+    E[x^2] - mean^2 in fp32 would lose the variance.  Reference: float64 moments of the stored bf16 output."""
     torch.manual_seed(1)
-    x, w, b, r = rnd(M, K), rnd(N, K, scale=0.05), rnd(N), rnd(M, N)
+    x, w, b = rnd(M, K), rnd(N, K, scale=0.05), rnd(N)
+    r = (torch.randn(M, N, device="cuda") + dc * torch.randn(M, 1, device="cuda").sign()).bfloat16()
     y, mr = ops.linear_stats(x, w, b, residual=r, stats="ln", eps=1e-5, force_cfg=cfg)
     assert mr.shape == (M, 2)
-    want = ref.row_moments(y, 1e-5)
-    assert rel(mr[:, 0], want[:, 0]) < 1e-4 and rel(mr[:, 1], want[:, 1]) < 1e-4
+    yd = y.double()
+    mean = yd.mean(1)
+    rstd = torch.rsqrt(yd.var(1, unbiased=False) + 1e-5)
+    assert rel(mr[:, 0], mean) < 1e-5 and rel(mr[:, 1], rstd) < 1e-4
 
 
 @pytest.mark.parametrize("cfg", [9, 10, 11, 12, -1])
