@@ -38,6 +38,8 @@ KERNEL_SRCS = ["kernels/norm.hip", "kernels/gemm.hip", "kernels/gemm_lds.hip", "
 # per-source extra hipcc flags: gemm_w4's epilogue (256 accumulators x an activation) is larger than LLVM's
 # default pragma-unroll budget; partially unrolled it would index the accumulators at run time (scratch)
 EXTRA_KFLAGS = {"kernels/attention3.hip": "-mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize",
+                # flash2 (d128): +0.5-1.2 % at the Flux / LLM-prefill shapes with the same flags (attention lab A/B)
+                "kernels/attention2.hip": "-mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize",
                 "kernels/gemm_w4.hip": "-mllvm -pragma-unroll-threshold=100000",
                 "kernels/gemm_ws.hip": "-mllvm -pragma-unroll-threshold=100000 -fno-slp-vectorize"}
 BINDING_SRCS = ["bindings.cpp"]

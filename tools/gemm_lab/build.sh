@@ -11,7 +11,7 @@ for src in gemm_lds gemm_8ph gemm_w4 gemm_ws gemv attention attention2 attention
     extra=""
     { [ "$src" = gemm_w4 ] || [ "$src" = gemm_ws ]; } && extra="-mllvm -pragma-unroll-threshold=100000"
     [ "$src" = gemm_ws ] && extra="$extra -fno-slp-vectorize"   # as csrc/build.py EXTRA_KFLAGS
-    [ "$src" = attention3 ] && extra="-mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize"
+    { [ "$src" = attention3 ] || [ "$src" = attention2 ]; } && extra="-mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize"
     hipcc $FLAGS $extra -c "$ROOT/csrc/kernels/$src.hip" -o "$OUT/$src.o" &
   fi
 done
@@ -23,9 +23,10 @@ mkdir -p "$ROOT/tools/gemm_lab/bin"
 hipcc --offload-arch=gfx950 "$OUT"/gemm_lab.o "$OUT"/gemm_lds.o "$OUT"/gemm_8ph.o "$OUT"/gemm_w4.o "$OUT"/gemm_ws.o "$OUT"/gemv.o \
   -o "$ROOT/tools/gemm_lab/bin/gemm_lab"
 hipcc --offload-arch=gfx950 "$OUT"/attn_lab.o "$OUT"/attention.o "$OUT"/attention2.o "$OUT"/attention3.o -o "$ROOT/tools/gemm_lab/bin/attn_lab"
-# ATTN3_FLAGS="...": a second attention lab whose attention3.hip is built with extra compiler flags (A/B of codegen)
-if [ -n "${ATTN3_FLAGS:-}" ]; then
-  hipcc $FLAGS $ATTN3_FLAGS -c "$ROOT/csrc/kernels/attention3.hip" -o "$OUT/attention3_x.o"
-  hipcc --offload-arch=gfx950 "$OUT"/attn_lab.o "$OUT"/attention.o "$OUT"/attention2.o "$OUT"/attention3_x.o -o "$ROOT/tools/gemm_lab/bin/attn_lab_x"
+# ATTN2_FLAGS="...": a second attention lab whose attention2.hip (flash2) is built with extra compiler flags (A/B of
+# codegen; attention3.hip's flags came out of the same A/B)
+if [ -n "${ATTN2_FLAGS:-}" ]; then
+  hipcc $FLAGS $ATTN2_FLAGS -c "$ROOT/csrc/kernels/attention2.hip" -o "$OUT/attention2_x.o"
+  hipcc --offload-arch=gfx950 "$OUT"/attn_lab.o "$OUT"/attention.o "$OUT"/attention2_x.o "$OUT"/attention3.o -o "$ROOT/tools/gemm_lab/bin/attn_lab_x"
 fi
 echo "built tools/gemm_lab/bin/gemm_lab tools/gemm_lab/bin/attn_lab"
