@@ -23,6 +23,12 @@ mkdir -p "$ROOT/tools/gemm_lab/bin"
 hipcc --offload-arch=gfx950 "$OUT"/gemm_lab.o "$OUT"/gemm_lds.o "$OUT"/gemm_8ph.o "$OUT"/gemm_w4.o "$OUT"/gemm_ws.o "$OUT"/gemv.o \
   -o "$ROOT/tools/gemm_lab/bin/gemm_lab"
 hipcc --offload-arch=gfx950 "$OUT"/attn_lab.o "$OUT"/attention.o "$OUT"/attention2.o "$OUT"/attention3.o -o "$ROOT/tools/gemm_lab/bin/attn_lab"
+# G8_FLAGS="...": a second GEMM lab whose gemm_8ph.hip (v4) is built with extra compiler flags (A/B of codegen)
+if [ -n "${G8_FLAGS:-}" ]; then
+  hipcc $FLAGS -DSHAI_GEMM_LAB $G8_FLAGS -c "$ROOT/csrc/kernels/gemm_8ph.hip" -o "$OUT/gemm_8ph_x.o"
+  hipcc --offload-arch=gfx950 "$OUT"/gemm_lab.o "$OUT"/gemm_lds.o "$OUT"/gemm_8ph_x.o "$OUT"/gemm_w4.o "$OUT"/gemm_ws.o "$OUT"/gemv.o \
+    -o "$ROOT/tools/gemm_lab/bin/gemm_lab_x"
+fi
 # ATTN2_FLAGS="...": a second attention lab whose attention2.hip (flash2) is built with extra compiler flags (A/B of
 # codegen; attention3.hip's flags came out of the same A/B)
 if [ -n "${ATTN2_FLAGS:-}" ]; then
