@@ -412,6 +412,11 @@ void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_
   if (!use_v2(g, a_bytes, w_bytes, a2_bytes)) {
     SHAI_CHECK(g.gate == nullptr, "gated GEMM epilogue needs the v2 kernel (operands < 2 GiB, SHAI_GEMM_V1 unset)");
     SHAI_CHECK(g.row_mr == nullptr, "folded LayerNorm needs the v4 kernel (operands < 2 GiB, SHAI_GEMM_V1 unset)");
+    if (g.conv) {  // the v1 conv instantiations: activation none / silu, silu only with 64-channel sources
+      const bool fast = g.Cin % 64 == 0 && (g.A2 == nullptr || g.Cin1 % 64 == 0);
+      SHAI_CHECK(!g.glu && (g.act == 0 || (g.act == 1 && fast)), "conv2d output activation ", g.act,
+                 " is not implemented for this input layout");
+    }
     shai::launch_gemm(g, stream());
     if (st && st->any()) {  // v1 writes no statistics
       if (st->gn_part) shai::launch_col_partials(g.C, g.M, g.N, g.ldc, st->gn_part, stream());

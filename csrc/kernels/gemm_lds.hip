@@ -636,10 +636,15 @@ void launch_gemm2_cfg(const GemmArgs& a, float* ws, int cfg, int splits, hipStre
 
 // Split-K fold + full epilogue for fp32 partials laid out [splits][M][N] (also used by the skinny kernel).
 void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipStream_t s) {
-  if (a.glu) {
-    if (a.act == ACT_SILU) launch_reduce<true, ACT_SILU>(a, ws, splits, s);
-    else if (a.act == ACT_GELU_TANH) launch_reduce<true, ACT_GELU_TANH>(a, ws, splits, s);
-    else launch_reduce<true, ACT_GELU>(a, ws, splits, s);
+  if (a.glu) {  // every activation: the skinny kernels (any GLU activation) fold through here too
+    switch (a.act) {
+      case ACT_SILU: launch_reduce<true, ACT_SILU>(a, ws, splits, s); break;
+      case ACT_GELU: launch_reduce<true, ACT_GELU>(a, ws, splits, s); break;
+      case ACT_GELU_TANH: launch_reduce<true, ACT_GELU_TANH>(a, ws, splits, s); break;
+      case ACT_QUICK_GELU: launch_reduce<true, ACT_QUICK_GELU>(a, ws, splits, s); break;
+      case ACT_RELU: launch_reduce<true, ACT_RELU>(a, ws, splits, s); break;
+      default: launch_reduce<true, ACT_NONE>(a, ws, splits, s); break;
+    }
     return;
   }
   switch (a.act) {
@@ -662,6 +667,8 @@ bool gemm2_cfg_candidate(int cfg) { return !(cfg >= kNumCfgs && cfg < kV4Cfg) &&
 bool gemm2_cfg_splittable(int cfg) { return cfg != kW4Cfg && cfg != kW4Cfg + 1 && cfg != kWsCfg; }
 
 bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
+  // an epilogue activation no tile kernel instantiates is never accepted (it would run as another one)
+  if (!tile_act_supported(a)) return false;
   // folded LayerNorm (row_mr): only the v4 kernel's epilogue applies it, and only unsplit, batch 1
   if (a.row_mr != nullptr)
     return cfg == kWsCfg ? gemm_ws_supported(a) : cfg >= kV4Cfg && cfg < kV4Cfg + 4 && a.batch <= 1 && gemm4_supported(a);

@@ -615,7 +615,18 @@ bool gemm_ws_supported(const GemmArgs& a) {
   const auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
   if (!al(a.A) || !al(a.W) || !al(a.C) || (a.residual && !al(a.residual))) return false;
   if ((long)a.M * a.lda * 2 >= 0x7fffffffL || (a.residual && (long)a.M * a.ldr * 2 >= 0x7fffffffL)) return false;
-  if (a.row_mr && (a.col_s == nullptr || (!a.glu && a.act != ACT_NONE))) return false;  // the instantiated folds
+  // exactly the variants launch_gemm_ws instantiates -- anything else would run as another activation (or drop
+  // the folded LayerNorm) without an error:
+  //   GLU:     SILU / GELU / GELU_TANH; the folded LayerNorm (row_mr) only with GELU
+  //   non-GLU: NONE / SILU / GELU;      the folded LayerNorm only with NONE
+  if (a.glu) {
+    if (a.act != ACT_SILU && a.act != ACT_GELU && a.act != ACT_GELU_TANH) return false;
+    if (a.row_mr && a.act != ACT_GELU) return false;
+  } else {
+    if (a.act != ACT_NONE && a.act != ACT_SILU && a.act != ACT_GELU) return false;
+    if (a.row_mr && a.act != ACT_NONE) return false;
+  }
+  if (a.row_mr && a.col_s == nullptr) return false;
   return true;
 }
 

@@ -138,9 +138,19 @@ struct GemmArgs {
   // output statistics for the NEXT norm, written by the v4 wide epilogue (gemm4_stats_ok); other kernels leave
   // them to the fallback passes of launch_out_stats
   float* col_part;          // [M / 128, N, 2]: per 128-row block and column (sum, sum of squares) -> GroupNorm
-  float* row_part;          // [M, row_part_slots, 2]: per row (sum, sum of squares) of each wave's column slice
-  int row_part_slots;       //   -> LayerNorm; slots = 4 * column tiles
+  float* row_part;          // [M, row_part_slots, 2]: per row and slot (mean, M2) of that slot's columns, shifted
+  int row_part_slots;       //   by the row's first value -> LayerNorm (Chan's combine in row_moments_part_kernel
+                            //   assumes equal column counts: every slot covers N / slots columns);
+                            //   slots = 4 * column tiles
 };
+// (conv, GLU, activation) epilogue variants the tile kernels (v2 / v4 / four-wave / W-stationary / halo conv)
+// instantiate: convolutions NONE / SILU, GLU SILU / GELU / GELU_TANH, plain GEMMs every activation.  Any other
+// combination is rejected by every tile config (gemm2_cfg_supported), never run as a neighbouring variant.
+inline bool tile_act_supported(const GemmArgs& a) {
+  if (a.conv) return !a.glu && (a.act == 0 || a.act == 1);       // ACT_NONE, ACT_SILU
+  if (a.glu) return a.act == 1 || a.act == 2 || a.act == 3;      // ACT_SILU, ACT_GELU, ACT_GELU_TANH
+  return true;
+}
 void launch_dequant_fp8_rows(const uint8_t* w8, const float* scale, bf16_t* out, long N, int K, hipStream_t s);
 // fp8 e4m3 MFMA GEMM (gemm_f8.hip): C = epi(a_scale[m] w_scale[n] A8 W8^T); A8 / W8 are e4m3 bytes, lda / ldw in
 // bytes; cfg 0 = 256 x 128 tile, 1 = 128 x 128

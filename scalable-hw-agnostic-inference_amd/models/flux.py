@@ -166,7 +166,7 @@ def _gated_out(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], resi
     # per slab reduces and applies the gated residual in place
     nrows = x.numel() // x.shape[-1]
     if comm.row_parallel_reduce(x, w, b, residual, gate=gate, rows_per_gate=rows, out=residual,
-                                chunks=comm.overlap_chunks(nrows)) is not None:
+                                chunks=comm.overlap_chunks(nrows, w.shape[0])) is not None:
         return
     y = ops.linear(x, w, None)
     comm.all_reduce(y)

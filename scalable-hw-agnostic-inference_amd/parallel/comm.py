@@ -82,8 +82,10 @@ def all_reduce(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> to
 # bias / AdaLN gate / residual epilogue fused) runs on a side stream while slab i + 1's GEMM runs on the compute
 # stream.  Fork / join by events, so it is HIP-graph capturable; every slab is its own collective, issued in the
 # same order on every rank.
-OVERLAP_CHUNKS = int(os.environ.get("SHAI_TP_OVERLAP_CHUNKS", "2"))
+_env_chunks = os.environ.get("SHAI_TP_OVERLAP_CHUNKS")
+OVERLAP_CHUNKS: Optional[int] = int(_env_chunks) if _env_chunks else None   # None: by rows and message size
 OVERLAP_MIN_ROWS = int(os.environ.get("SHAI_TP_OVERLAP_MIN_ROWS", "1024"))
+OVERLAP_MIN_BYTES = int(os.environ.get("SHAI_TP_OVERLAP_MIN_BYTES", str(2 << 20)))
 _SIDE: dict = {}
 
 
@@ -94,11 +96,21 @@ def _side_stream(device: torch.device) -> "torch.cuda.Stream":
     return _SIDE[idx]
 
 
-def overlap_chunks(rows: int) -> int:
-    """How many row slabs a row-parallel GEMM of ``rows`` rows is split into (1: no overlap)."""
-    if tp().size == 1 or OVERLAP_CHUNKS <= 1 or rows < OVERLAP_MIN_ROWS:
+def overlap_chunks(rows: int, cols: int = 0, elem_bytes: int = 2) -> int:
+    """How many row slabs a row-parallel GEMM of ``rows`` x ``cols`` outputs is split into (1: no overlap).
+
+    Only the LAST slab's reduce is exposed after the GEMM, so the exposed share of the message is 1 / slabs, while
+    every slab GEMM must still fill the chip: 4 slabs from 4096 rows (Flux 1024^2: 4608 rows, 27 MiB per call at
+    TP8 -> ~6.8 MiB exposed instead of 13.5 with 2), 2 from OVERLAP_MIN_ROWS (1024: Flux 512^2, LLM prefill
+    chunks), none below it or for messages under OVERLAP_MIN_BYTES (latency-bound reduces: a split only adds
+    launches).  SHAI_TP_OVERLAP_CHUNKS (or setting ``OVERLAP_CHUNKS``) pins the count for every large message."""
+    if tp().size == 1 or rows < OVERLAP_MIN_ROWS:
         return 1
-    return max(1, min(OVERLAP_CHUNKS, rows))
+    if OVERLAP_CHUNKS is not None:
+        return max(1, min(OVERLAP_CHUNKS, rows))
+    if cols and rows * cols * elem_bytes < OVERLAP_MIN_BYTES:
+        return 1
+    return 4 if rows >= 4096 else 2
 
 
 def row_slabs(rows: int, chunks: int):
@@ -124,6 +136,50 @@ def _epilogue_rows(y: torch.Tensor, out: torch.Tensor, bias, residual, gate, row
 
 def _al16(t: Optional[torch.Tensor]) -> bool:
     return t is None or t.data_ptr() % 16 == 0
+
+
+def _staged_ok(p, x, rows, n, w_scale, residual, out, bias, gate2) -> bool:
+    """Whether the fused staged P2P reduce (GEMM into the IPC slot + one reduce/epilogue kernel) takes a message."""
+    if p is None or not P2P_STAGED or x.dtype != torch.bfloat16:
+        return False
+    if n % 8 or rows * n * 2 > p.max_bytes or (w_scale is not None and rows > 64):
+        return False
+    for t in (residual, out, bias):
+        if t is not None and (t.dtype != torch.bfloat16 or not _al16(t)):
+            return False
+    if bias is not None and (not bias.is_contiguous() or bias.numel() != n):
+        return False
+    if gate2 is not None and (gate2.dtype != torch.bfloat16 or gate2.stride(-1) != 1 or gate2.shape[-1] < n
+                              or gate2.stride(0) % 8 or not _al16(gate2)):
+        return False
+    return True
+
+
+def _generic_slabs(x, x2, weight, bias, residual, w_scale, gate2, rows_per_gate, out, bounds):
+    """Overlapped row-parallel stage without the staged P2P reduce (no P2P group, a message above its capacity,
+    fp8 prefill): slab i's GEMM runs on the compute stream while slab i - 1's all-reduce (RCCL, or the unstaged P2P
+    kernels) and its bias / gate / residual epilogue run on the side stream."""
+    from .. import ops
+    n = weight.shape[0]
+    rows = x2.shape[0]
+    if out is None:
+        out = torch.empty(*x.shape[:-1], n, dtype=x.dtype, device=x.device)
+    o2 = out.view(rows, n)
+    r2 = residual.reshape(rows, n) if residual is not None else None
+    cur = torch.cuda.current_stream(x.device)
+    side = _side_stream(x.device)
+    side.wait_stream(cur)
+    for r0, r1 in bounds:
+        ys = ops.linear(x2[r0:r1], weight, None, w_scale=w_scale)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        side.wait_event(ev)
+        ys.record_stream(side)   # allocated on the compute stream, consumed on the side stream
+        with torch.cuda.stream(side):
+            all_reduce(ys)
+            _epilogue_rows(ys, o2[r0:r1], bias, r2[r0:r1] if r2 is not None else None, gate2, rows_per_gate, r0)
+    cur.wait_stream(side)
+    return out
 
 
 def row_parallel_reduce(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
@@ -158,19 +214,13 @@ def row_parallel_reduce(x: torch.Tensor, weight: torch.Tensor, bias: Optional[to
             _epilogue_rows(y, o2[r0:r1], bias, r2[r0:r1] if r2 is not None else None, gate2, rows_per_gate, r0)
         return out
     p = _P2P
-    if p is None or not P2P_STAGED or x.dtype != torch.bfloat16:
-        return None
-    nbytes = rows * n * 2
-    if n % 8 or nbytes > p.max_bytes or (w_scale is not None and rows > 64):
-        return None
-    for t in (residual, out, bias):
-        if t is not None and (t.dtype != torch.bfloat16 or not _al16(t)):
+    if not _staged_ok(p, x, rows, n, w_scale, residual, out, bias, gate2):
+        # no staged P2P reduce for this message: with several slabs, the generic overlapped slab loop (GEMM per
+        # slab on the compute stream, that slab's all-reduce + epilogue on the side stream); one slab -> the
+        # caller's serial GEMM -> all_reduce -> epilogue path
+        if len(bounds) == 1:
             return None
-    if bias is not None and (not bias.is_contiguous() or bias.numel() != n):
-        return None
-    if gate2 is not None and (gate2.dtype != torch.bfloat16 or gate2.stride(-1) != 1 or gate2.shape[-1] < n
-                              or gate2.stride(0) % 8 or not _al16(gate2)):
-        return None
+        return _generic_slabs(x, x2, weight, bias, residual, w_scale, gate2, rows_per_gate, out, bounds)
     from .. import ops
     stage = p.staging(rows, n, x.device)
     if out is None:

@@ -111,7 +111,7 @@ class RowParallelLinear(_ShardLoadMixin, nn.Module):
         # fused (GEMM into the IPC staging slot, one kernel reduces + adds bias / residual) and, at >= 1024 rows,
         # overlapped (row slab i's reduce runs beside slab i + 1's GEMM); CPU (gloo): the same slab schedule
         y = comm.row_parallel_reduce(x, self.weight, self.bias, residual, self.w_scale,
-                                     chunks=comm.overlap_chunks(rows))
+                                     chunks=comm.overlap_chunks(rows, self.out_features))
         if y is not None:
             return y.view(*x.shape[:-1], self.out_features)
         y = ops.linear(x, self.weight, None, w_scale=self.w_scale)

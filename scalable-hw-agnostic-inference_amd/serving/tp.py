@@ -27,7 +27,9 @@ Failure handling (a TP group is one unit: it serves or it is restarted whole):
   whose call fails stays in the group only when its exception is a mirrored input error (``MIRRORED``) AND the
   leader raised the same type -- a rank-local ``KeyError`` thrown after a collective is not excused by the
   leader's success -- and so does a follower whose call succeeded where the leader's failed with anything but a
-  mirrored error.  Any other follower failure is reported to the leader on a
+  mirrored error.  A follower error outside ``MIRRORED`` leaves at once, without waiting for the outcome (the
+  leader may be blocked in a collective the follower never joins).  Any other follower failure is reported to the
+  leader on a
   second gloo group and exits non-zero; ``torch.distributed.run`` then stops the other ranks and the
   supervisor relaunches the group.  The leader's status listener marks the process broken
   (``utils.liveness.mark_broken``: ``/health`` 503) the moment the report -- or the lost connection of a
@@ -154,7 +156,9 @@ class SPMDProxy:
                 out = attr(*args, **kwargs)
                 raise_if_p2p_error()
             except BaseException as e:
-                self._channel.send(OUTCOME, type(e).__name__)
+                # the follower compares the type NAME and requires both sides mirrored (a ValueError subclass such
+                # as JSONDecodeError raised on both ranks is as mirrored as a ValueError)
+                self._channel.send(OUTCOME, (type(e).__name__, isinstance(e, MIRRORED)))
                 raise
             self._channel.send(OUTCOME, "")
             return out
@@ -206,13 +210,14 @@ def follow(target, channel: TPChannel, step_fn=None, leader_timeout_s: Optional[
     n = 0
     dog = _LeaderWatchdog(LEADER_TIMEOUT_S if leader_timeout_s is None else leader_timeout_s)
 
-    def leader_outcome() -> str:
+    def leader_outcome():
+        """("", False) when the leader's call succeeded, else (its exception type name, whether mirrored)."""
         while True:  # heartbeats may land between the call and its outcome
             dog.idle_since = time.monotonic()
             kind, payload = channel.recv()
             dog.idle_since = None
             if kind == OUTCOME:
-                return payload or ""
+                return tuple(payload) if payload else ("", False)
             if kind != NOOP:
                 raise RuntimeError(f"TP protocol: expected the leader's call outcome, got message kind {kind}")
 
@@ -237,21 +242,22 @@ def follow(target, channel: TPChannel, step_fn=None, leader_timeout_s: Optional[
                         step_fn(payload)
             except Exception as e:  # noqa: BLE001 -- classified against the leader's outcome below
                 err = e
-            if kind != CALL:
+            if kind != CALL or (err is not None and not isinstance(err, MIRRORED)):
+                # a rank-local failure (OOM, device fault, shard-specific error) leaves AT ONCE: the leader may be
+                # blocked in a collective this rank will never join, so waiting for its OUTCOME could hang the
+                # group until the collective's timeout while the heartbeats keep this rank's watchdog quiet
                 if err is not None:
                     _fail(channel, err)
             else:
                 try:
-                    lead = leader_outcome()
+                    lead, lead_mirrored = leader_outcome()
                 except Exception as e:  # noqa: BLE001
                     _fail(channel, e)
-                mine = type(err).__name__ if err is not None else ""
-                mirrored = {c.__name__ for c in MIRRORED}
-                if mine != lead and not (err is None and lead in mirrored):
-                    _fail(channel, err if err is not None else
-                          RuntimeError(f"leader failed with {lead} where this rank succeeded"))
-                if err is not None:
-                    if mine not in mirrored:
+                if err is None:
+                    if lead and not lead_mirrored:
+                        _fail(channel, RuntimeError(f"leader failed with {lead} where this rank succeeded"))
+                else:  # a mirrored error here: excused only when the leader raised the same type, also mirrored
+                    if not (lead == type(err).__name__ and lead_mirrored):
                         _fail(channel, err)
                     _log.warning("follower call failed (mirrored on the leader)",
                                  extra={"event": "follower_error", "detail": repr(err)[:300]})

@@ -91,6 +91,43 @@ def test_ws_folded_layernorm(cuda, glu, res):
     assert _rel(y, want) < 2e-2
 
 
+_ACTS = {None: lambda t: t, "silu": torch.nn.functional.silu, "gelu": torch.nn.functional.gelu,
+         "gelu_tanh": lambda t: torch.nn.functional.gelu(t, approximate="tanh"),
+         "quick_gelu": lambda t: t * torch.sigmoid(1.702 * t), "relu": torch.relu}
+
+
+@pytest.mark.parametrize("act,glu", [("relu", False), ("gelu_tanh", False), ("quick_gelu", False), ("relu", True),
+                                     ("quick_gelu", True), (None, True)])
+def test_ws_rejects_uninstantiated_act(cuda, act, glu):
+    """gemm_ws_supported() admits exactly the activation variants launch_gemm_ws instantiates: forcing config 15 on
+    any other (act, glu) pair raises instead of silently running another activation."""
+    M, K, N = 1024, 320, 640
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
+    out = torch.empty(M, N // 2 if glu else N, device=cuda, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="bad force_cfg"):
+        ops.gemm_into(a, w, out, None, act=act, glu=glu, force_cfg=WS)
+
+
+@pytest.mark.parametrize("act,glu", [("relu", False), ("gelu_tanh", False), ("quick_gelu", False), ("relu", True),
+                                     ("quick_gelu", True), ("silu", True)])
+def test_ws_shape_autotuned_any_act(cuda, act, glu):
+    """The same K = 320 shapes autotuned (config 15 is a candidate only where supported, and a cached choice of
+    another activation's problem falls back) match fp32 for every activation."""
+    M, K, N = 8192, 320, 1280
+    torch.manual_seed(5)
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device=cuda).bfloat16()
+    # prime the tuning cache with the plain problem of this shape (config 15 may win it)
+    ops.linear(a, w, b, act="gelu" if glu else None, glu=glu)
+    y = ops.linear(a, w, b, act=act, glu=glu)
+    f = _ACTS[act]
+    ref = a.float() @ w.float().t() + b.float()
+    want = ref[:, 0::2] * f(ref[:, 1::2]) if glu else f(ref)
+    assert _rel(y, want) < 1e-2
+
+
 @pytest.mark.parametrize("M", [262144, 1003])
 def test_ws_lnout(cuda, M):
     """ops.linear_lnout: y = x W^T + b + R and LayerNorm(y) gamma + beta from the W-stationary epilogue (row moments

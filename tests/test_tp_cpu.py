@@ -76,3 +76,26 @@ def _rs_no_alias_worker(rank, world, port):
 
 def test_reduce_scatter_seq_gloo_keeps_input():
     mp.spawn(_rs_no_alias_worker, args=(2, _port()), nprocs=2, join=True)
+
+
+def test_overlap_chunks_default_by_rows_and_bytes(monkeypatch):
+    """The default row-slab count of the overlapped row-parallel stage is a function of rows and message size
+    (comm.overlap_chunks): 4 slabs from 4096 rows (Flux 1024^2 TP8: 4608 rows, <= 1/4 of the 27 MiB reduce
+    exposed), 2 from 1024 rows (Flux 512^2: 1056), none below 1024 rows or under 2 MiB; the env/attribute pin
+    overrides it."""
+    import types
+    from shai_amd.parallel import comm
+    monkeypatch.setattr(comm, "tp", lambda: types.SimpleNamespace(size=8, rank=0, group=None))
+    monkeypatch.setattr(comm, "OVERLAP_CHUNKS", None)
+    monkeypatch.setattr(comm, "OVERLAP_MIN_ROWS", 1024)
+    assert comm.overlap_chunks(4608, 3072) == 4          # Flux 1024^2 single / dual image stream
+    assert comm.overlap_chunks(4096, 3072) == 4
+    assert comm.overlap_chunks(1056, 3072) == 2          # Flux 512^2
+    assert comm.overlap_chunks(1023, 3072) == 1
+    assert comm.overlap_chunks(2048, 256) == 1           # 1 MiB: latency-bound, no split
+    assert comm.overlap_chunks(2048) == 2                # width unknown: rows decide
+    assert [b - a for a, b in comm.row_slabs(4608, 4)] == [1152] * 4
+    monkeypatch.setattr(comm, "OVERLAP_CHUNKS", 3)
+    assert comm.overlap_chunks(4608, 3072) == 3 and comm.overlap_chunks(512, 3072) == 1
+    monkeypatch.setattr(comm, "tp", lambda: types.SimpleNamespace(size=1, rank=0, group=None))
+    assert comm.overlap_chunks(4608, 3072) == 1

@@ -52,6 +52,22 @@ def test_rank_local_keyerror_leaves_the_group():
     assert "leader notified: rank 1: KeyError" in out0, out0
 
 
+def test_mirrored_subclass_keeps_the_group():
+    """JSONDecodeError (a ValueError subclass) raised by both ranks is mirrored: the leader sends (type name,
+    isinstance(e, MIRRORED)) and the follower matches the name and the flag."""
+    (rc0, out0), (rc1, out1) = _run("subclass")
+    assert rc0 == 0 and "leader bad_json: JSONDecodeError" in out0, out0
+    assert rc1 == 0 and "follower survived 3" in out1, out1
+
+
+def test_follower_error_before_collective_leaves_at_once():
+    """A follower-only RuntimeError before a collective the leader enters: the follower must report and exit
+    without waiting for the leader's OUTCOME (which never comes: the leader is blocked in the all-reduce)."""
+    (rc0, out0), (rc1, out1) = _run("collective")
+    assert rc1 == tp.FOLLOWER_FAILED_EXIT, out1
+    assert "leader notified: rank 1: RuntimeError: out of memory" in out0, out0
+
+
 def test_leader_only_failure_leaves_the_group():
     (rc0, out0), (rc1, out1) = _run("leader")
     assert rc1 == tp.FOLLOWER_FAILED_EXIT, out1

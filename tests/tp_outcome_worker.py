@@ -30,6 +30,18 @@ class Target:
             raise RuntimeError("device fault")    # only the leader, not an input error: follower leaves
         return "ok"
 
+    def bad_json(self):
+        import json
+        json.loads("{not json")                   # both ranks: a ValueError SUBCLASS, still mirrored
+
+    def collective(self):
+        import torch
+        if self.rank == 1:
+            raise RuntimeError("out of memory")   # follower-only, BEFORE the collective the leader enters
+        t = torch.ones(1)
+        dist.all_reduce(t)                        # the leader blocks here: the follower must leave at once
+        return "ok"
+
 
 def main():
     case = sys.argv[1]
@@ -42,9 +54,11 @@ def main():
             print(f"leader notified: {detail}", flush=True)
             os._exit(0)
         ch.listen_for_failures(notified)
-        proxy = tp.SPMDProxy(target, ch, {"ok", "bad_input", "local_keyerror", "leader_runtime"})
+        proxy = tp.SPMDProxy(target, ch, {"ok", "bad_input", "local_keyerror", "leader_runtime", "bad_json",
+                                          "collective"})
         seq = {"mirrored": ["ok", "bad_input", "ok"], "local": ["ok", "local_keyerror"],
-               "leader": ["ok", "leader_runtime"]}[case]
+               "leader": ["ok", "leader_runtime"], "subclass": ["ok", "bad_json", "ok"],
+               "collective": ["ok", "collective"]}[case]
         for name in seq:
             try:
                 getattr(proxy, name)()

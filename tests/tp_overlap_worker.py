@@ -70,6 +70,38 @@ def run(rank, world, port):
         assert rel(yg) < 2e-2, rel(yg)
     assert not p2p.error()
     dist.barrier()
+    # the DEFAULT slab count (comm.overlap_chunks by rows and bytes) at both Flux sizes, asserted by launch counters:
+    # 1056 rows (512^2) -> 2 staged reduces, 4608 rows (1024^2; N = 1536 keeps the message under this group's
+    # 16 MiB staging cap) -> 4
+    comm.OVERLAP_CHUNKS, comm.OVERLAP_MIN_ROWS = None, 1024
+    for Md, Nd, want_slabs in ((1056, 3072, 2), (4608, 1536, 4)):
+        gd = torch.Generator().manual_seed(Md)
+        wd = (torch.randn(Nd, K, generator=gd) / K ** 0.5).bfloat16()
+        xd = torch.randn(Md, K, generator=gd).bfloat16()
+        rd = torch.randn(Md, Nd, generator=gd).bfloat16()
+        lind = RowParallelLinear(K, Nd, bias=False, input_is_parallel=False).cuda()
+        load_into(lind, {"weight": wd}, strict=True)
+        assert comm.overlap_chunks(Md, Nd) == want_slabs
+        c0 = p2p.launch_counts()
+        yd = lind(xd.cuda(), residual=rd.cuda())
+        torch.cuda.synchronize()
+        c1 = p2p.launch_counts()
+        assert c1["staged_two_shot"] - c0["staged_two_shot"] == want_slabs, (Md, c0, c1)
+        wantd = (xd.float() @ wd.float().t() + rd.float()).cuda()
+        assert ((yd.float() - wantd).norm() / wantd.norm()).item() < 2e-2
+        dist.barrier()
+        # the generic overlapped slab loop (no staged reduce: GEMM per slab, that slab's unstaged all-reduce +
+        # epilogue on the side stream) -- same slab count, same values
+        comm.P2P_STAGED = False
+        c0 = p2p.launch_counts()
+        yg2 = lind(xd.cuda(), residual=rd.cuda())
+        torch.cuda.synchronize()
+        c1 = p2p.launch_counts()
+        comm.P2P_STAGED = True
+        assert c1["two_shot"] - c0["two_shot"] == want_slabs, (Md, c0, c1)
+        assert c1["staged_two_shot"] == c0["staged_two_shot"], (c0, c1)
+        assert ((yg2.float() - wantd).norm() / wantd.norm()).item() < 2e-2
+        dist.barrier()
     comm.enable_p2p(None)
     p2p.close()
     dist.destroy_process_group()
