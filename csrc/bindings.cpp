@@ -26,6 +26,25 @@ namespace {
 
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// Halo-tiled conv routing (conv_halo.hip): 0 off, 1 GroupNorm-fused convs (default), 2 also plain 3x3 convs;
+// SHAI_HALO_CONV sets it, the set_halo_conv op changes it at run time (A/B in one process).  g_halo_waves: 0 = the
+// kernel's default wave layout (SHAI_HALO_WAVES), 4 / 8 pin one.
+int g_halo_mode = -1;
+int g_halo_waves = 0;
+int halo_conv_mode() {
+  if (g_halo_mode < 0) {
+    const char* e = getenv("SHAI_HALO_CONV");
+    g_halo_mode = e ? atoi(e) : 1;
+  }
+  return g_halo_mode;
+}
+int64_t set_halo_conv(int64_t mode, int64_t waves) {
+  const int prev = halo_conv_mode();
+  if (mode >= 0) g_halo_mode = (int)mode;
+  if (waves >= 0) g_halo_waves = (int)waves;
+  return prev;
+}
+
 // v2 GEMM (LDS-DMA) unless the problem needs v1 features (fused GN gather) or
 // exceeds the 2 GiB buffer-descriptor range.  SHAI_GEMM_V1=1 forces v1.
 bool use_v2(const shai::GemmArgs& g, long a_bytes, long w_bytes, long a2_bytes) {
@@ -992,15 +1011,48 @@ void conv2d(const Tensor& x, const optional<Tensor>& x2, const Tensor& w, const 
     SHAI_CHECK(in_shift.has_value(), "in_scale requires in_shift");
     check_f32(*in_scale, "in_scale");
     check_f32(*in_shift, "in_shift");
-    SHAI_CHECK(in_scale->numel() == (long)g.Nimg * g.Cin, "in_scale must be [N, Cin]");
+    SHAI_CHECK(in_scale->numel() == (long)g.Nimg * g.Cin && in_shift->numel() == (long)g.Nimg * g.Cin,
+               "in_scale / in_shift must be [N, Cin]");
     g.in_scale = in_scale->data_ptr<float>();
     g.in_shift = in_shift->data_ptr<float>();
     g.in_act = in_act;
   }
   OutStats st;
   attach_norm_io(g, ln_mr, ln_s, gn_part, ln_stats, ln_eps, &st);
-  run_gemm(g, x, xcat.defined() ? xcat.numel() * 2 : x.numel() * 2, w.numel() * 2,
-           (x2 && !xcat.defined()) ? x2->numel() * 2 : 0, &st);
+  // Halo-tiled conv (conv_halo.hip): GroupNorm(+SiLU) convs (SHAI_HALO_CONV >= 1, default) and, at mode 2, every
+  // 3x3 stride-1 conv it supports; the output's GroupNorm partials come from its epilogue.
+  const int hmode = halo_conv_mode();
+  if (hmode > 0 && g.row_mr == nullptr && st.ln_mr == nullptr && (g.in_scale != nullptr || hmode >= 2) &&
+      shai::conv_halo_supported(g)) {
+    g.col_part = st.gn_part;
+    shai::launch_conv_halo(g, stream(), g_halo_waves);
+    return;
+  }
+  Tensor xn;
+  if (g.in_scale != nullptr) {
+    // no fused kernel for this shape: the normalised input as one vectorised pass (fused concat read), then the
+    // tuned conv on it -- never the v1 kernel's per-tap in-gather normalisation
+    SHAI_CHECK(g.in_act == 0 || g.in_act == 1, "conv2d input norm activation must be none / silu");
+    xn = at::empty({(long)g.Nimg, (long)g.H, (long)g.Wd, (long)g.Cin}, x.options());
+    shai::GroupNormArgs a{};
+    a.x = g.A;
+    a.x2 = g.A2;
+    a.C1 = g.A2 ? g.Cin1 : g.Cin;
+    a.scale = const_cast<float*>(g.in_scale);
+    a.shift = const_cast<float*>(g.in_shift);
+    a.out = mptr(xn);
+    a.N = g.Nimg;
+    a.HW = g.H * g.Wd;
+    a.C = g.Cin;
+    a.silu = g.in_act == 1;
+    shai::launch_groupnorm_apply(a, stream());
+    g.A = cptr(xn);
+    g.A2 = nullptr;
+    g.Cin1 = g.Cin;
+    g.in_scale = g.in_shift = nullptr;
+  }
+  run_gemm(g, x, xn.defined() ? xn.numel() * 2 : (xcat.defined() ? xcat.numel() * 2 : x.numel() * 2),
+           w.numel() * 2, (g.A2 != nullptr) ? x2->numel() * 2 : 0, &st);
 }
 
 // ---------------------------------------------------------------- attention
@@ -1595,6 +1647,7 @@ TORCH_LIBRARY(shai, m) {
   m.def("layernorm_mod(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, int rows_per_mod, float eps) -> ()");
   m.def("qk_norm_rope(Tensor(a!) x, Tensor? q_w, Tensor? k_w, Tensor? cos, Tensor? sin, int H, int D, int S, float eps) -> ()");
   m.def("conv2d(Tensor x, Tensor? x2, Tensor w, Tensor(a!) out, Tensor? bias, Tensor? bias2d, Tensor? residual, Tensor? in_scale, Tensor? in_shift, int in_act, int kh, int kw, int stride, int pad, bool upsample, int act, float res_alpha, Tensor? ln_mr=None, Tensor? ln_s=None, Tensor(b!)? gn_part=None, Tensor(c!)? ln_stats=None, float ln_eps=1e-5) -> ()");
+  m.def("set_halo_conv(int mode, int waves=-1) -> int");
   m.def("flash_attn(Tensor q, Tensor k, Tensor v, Tensor(a!) o, float scale, bool causal, int causal_offset, Tensor? kv_lens, Tensor? q_lens, Tensor? bias, Tensor? block_table) -> ()");
   m.def("paged_attn_varlen(Tensor q, Tensor k_cache, Tensor v_cache, Tensor(a!) o, Tensor block_table, Tensor kv_lens, Tensor q_lens, Tensor q_start, int max_q, float scale, bool causal) -> ()");
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor(a!) o, Tensor block_table, Tensor ctx_lens, Tensor(b!) ws, int num_splits, float scale) -> ()");
@@ -1636,6 +1689,7 @@ TORCH_LIBRARY_IMPL(shai, CUDA, m) {
   m.impl("layernorm_mod", &layernorm_mod);
   m.impl("qk_norm_rope", &qk_norm_rope);
   m.impl("conv2d", &conv2d);
+  m.impl("set_halo_conv", &set_halo_conv);
   m.impl("flash_attn", &flash_attn);
   m.impl("paged_attn_varlen", &paged_attn_varlen);
   m.impl("decode_attn", &decode_attn);

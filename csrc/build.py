@@ -32,7 +32,7 @@ BUILD = os.path.join(ROOT, "build", "native")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
-KERNEL_SRCS = ["kernels/norm.hip", "kernels/gemm.hip", "kernels/gemm_lds.hip", "kernels/gemm_8ph.hip", "kernels/gemm_w4.hip", "kernels/gemm_ws.hip", "kernels/attention.hip", "kernels/attention2.hip", "kernels/attention3.hip", "kernels/elementwise.hip", "kernels/dit.hip",
+KERNEL_SRCS = ["kernels/norm.hip", "kernels/gemm.hip", "kernels/gemm_lds.hip", "kernels/gemm_8ph.hip", "kernels/gemm_w4.hip", "kernels/gemm_ws.hip", "kernels/conv_halo.hip", "kernels/attention.hip", "kernels/attention2.hip", "kernels/attention3.hip", "kernels/elementwise.hip", "kernels/dit.hip",
                "kernels/sampling.hip", "kernels/gemv.hip", "kernels/gemv2.hip",
                "kernels/gemm_f8.hip"]
 # per-source extra hipcc flags: gemm_w4's epilogue (256 accumulators x an activation) is larger than LLVM's
@@ -41,7 +41,8 @@ EXTRA_KFLAGS = {"kernels/attention3.hip": "-mllvm -amdgpu-mfma-vgpr-form -fno-sl
                 # flash2 (d128): +0.5-1.2 % at the Flux / LLM-prefill shapes with the same flags (attention lab A/B)
                 "kernels/attention2.hip": "-mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize",
                 "kernels/gemm_w4.hip": "-mllvm -pragma-unroll-threshold=100000",
-                "kernels/gemm_ws.hip": "-mllvm -pragma-unroll-threshold=100000 -fno-slp-vectorize"}
+                "kernels/gemm_ws.hip": "-mllvm -pragma-unroll-threshold=100000 -fno-slp-vectorize",
+                "kernels/conv_halo.hip": "-mllvm -pragma-unroll-threshold=100000"}
 BINDING_SRCS = ["bindings.cpp"]
 RUNTIME_SRCS = ["runtime/block_manager.cpp", "runtime/scheduler.cpp"]
 COMM_SRCS = ["comm/p2p_allreduce.hip"]

@@ -182,6 +182,12 @@ void launch_gemm_ws(const GemmArgs& a, hipStream_t s);
 bool gemm_ws_lnout_supported(const GemmArgs& a);
 void launch_gemm_ws_lnout(const GemmArgs& a, bf16_t* C2, const bf16_t* gamma, const bf16_t* beta, float eps,
                           hipStream_t s);
+// halo-tiled 3x3 conv (conv_halo.hip): stride 1 / pad 1, OW in {16, 32, 64}, Cin (and the concat split) multiples of
+// 64, N % 160 or N % 128 == 0; the input's GroupNorm + SiLU (in_scale / in_shift, one [2, N, Cin] allocation) applied
+// once per staged element in LDS; writes col_part (GroupNorm partials of the output) when set.  waves: 4 or 8 (0:
+// SHAI_HALO_WAVES, default 8)
+bool conv_halo_supported(const GemmArgs& a);
+void launch_conv_halo(const GemmArgs& a, hipStream_t s, int waves);
 // whether config cfg is raced by the autotuner (retired configs still run a cached choice, on their successor)
 bool gemm2_cfg_candidate(int cfg);
 void launch_splitk_epilogue(const GemmArgs& a, const float* ws, int splits, hipStream_t s);

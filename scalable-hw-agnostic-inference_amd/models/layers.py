@@ -144,16 +144,20 @@ class GroupNorm(nn.Module):
         """(scale, shift) fp32 [N, C]: fed to a consumer conv's fused prologue."""
         return ops.groupnorm_stats(x, self.weight, self.bias, self.groups, self.eps, x2=x2)
 
+    def scale_shift(self, x, x2=None, part=None, part2=None):
+        """(scale, shift) fp32 [N, C] of GroupNorm(cat([x, x2], -1)), from the producers' partials when given --
+        the ``norm=`` prologue of a consumer conv (``ops.conv2d``)."""
+        if part is not None and (x2 is None or part2 is not None):
+            return ops.groupnorm_stats_from_partials(part, self.weight, self.bias, self.groups, self.eps, x.shape[0],
+                                                     x.numel() // (x.shape[0] * x.shape[-1]),
+                                                     part2=part2 if x2 is not None else None)
+        return self.stats(x, x2)
+
     def forward(self, x, silu: bool = False, x2=None, part=None, part2=None):
         """GroupNorm of x, or of cat([x, x2], -1) without materialising the concat.  ``part`` / ``part2``:
         partials of x / x2 handed over by their producing GEMM (``conv2d(stats="gn")``), which replace the
         statistics pass over the input."""
-        if part is not None and (x2 is None or part2 is not None):
-            sc, sh = ops.groupnorm_stats_from_partials(part, self.weight, self.bias, self.groups, self.eps,
-                                                       x.shape[0], x.numel() // (x.shape[0] * x.shape[-1]),
-                                                       part2=part2 if x2 is not None else None)
-        else:
-            sc, sh = self.stats(x, x2)
+        sc, sh = self.scale_shift(x, x2, part, part2)
         return ops.groupnorm_apply(x, sc, sh, silu, x2=x2)
 
 

@@ -5,9 +5,11 @@ runs (cuDNN/Inductor on GPU, NEFF on Inferentia).  MI355X-first design:
 
 * Every 3x3/1x1 conv is the implicit-GEMM MFMA kernel; the time-embedding bias
   and the residual/skip add are fused into the conv epilogue, Upsample2D's
-  nearest-2x is fused into the gather.  GroupNorm+SiLU is a statistics pass
-  plus one vectorised apply pass (the conv kernel can also normalise inside
-  its gather, but for 3x3 convs that repeats the transform per tap and N-tile).
+  nearest-2x is fused into the gather.  A ResNet's GroupNorm+SiLU is the
+  prologue of its 3x3 conv: statistics from the producer's epilogue partials,
+  applied once per staged element in LDS by the halo-tiled conv
+  (csrc/kernels/conv_halo.hip; normalising inside a per-tap gather would repeat
+  the transform 9x per N-tile).
 * Transformer blocks: fused QKV GEMM -> flash attention reading strided views
   -> out-proj GEMM with the residual in its epilogue; GEGLU fused into the FF
   GEMM epilogue.
@@ -31,6 +33,9 @@ from .layers import Conv2d, GLULinear, GroupNorm, LayerNorm, Linear, timestep_em
 # GroupNorm partials / LayerNorm moments handed from the producing GEMM epilogue to the next norm (and LayerNorms
 # folded into their consumer projections); SHAI_NORM_HANDOFF=0 restores the standalone norm passes (A/B)
 NORM_HANDOFF = os.environ.get("SHAI_NORM_HANDOFF", "1") != "0"
+# ResNet GroupNorm + SiLU applied by the consuming 3x3 conv (ops.conv2d(norm=...): the halo-tiled conv normalises each
+# staged input element once in LDS); SHAI_FUSED_GN_CONV=0 restores the separate apply pass (A/B)
+FUSED_GN_CONV = os.environ.get("SHAI_FUSED_GN_CONV", "1") != "0"
 
 
 @dataclass
@@ -78,21 +83,27 @@ class ResnetBlock2D(nn.Module):
         """forward with the GroupNorm hand-off: ``xp`` / ``x2p`` are GroupNorm partials of x / x2 written by their
         producers' epilogues (they replace the statistics pass of norm1); with ``stats`` conv1 and conv2 write
         the partials of their outputs (norm2's input, and the next norm's).  Returns (out, partials or None)."""
-        # GroupNorm+SiLU as one memory-bound pass (normalising inside the 3x3 gather would
-        # redo the transform 9x per N-tile: VALU-bound, measured 5x slower).
-        n1 = self.norm1(x, silu=True, x2=x2, part=xp, part2=x2p)
-        if stats:
-            h, hp = self.conv1(n1, temb=temb_proj, stats="gn")
+        st = {"stats": "gn"} if stats else {}
+        if FUSED_GN_CONV and x.shape[-1] % 8 == 0 and (x2 is None or x2.shape[-1] % 8 == 0):
+            # GroupNorm + SiLU as the convs' prologue: (scale, shift) from the producers' partials, applied once per
+            # staged element inside the halo-tiled conv (one apply pass + the tuned conv where it does not fit)
+            sc, sh = self.norm1.scale_shift(x, x2, part=xp, part2=x2p)
+            out1 = self.conv1(x, x2=x2, norm=(sc, sh, "silu"), temb=temb_proj, **st)
         else:
-            h, hp = self.conv1(n1, temb=temb_proj), None
+            # the separate pass: GroupNorm + SiLU written out, then the conv
+            n1 = self.norm1(x, silu=True, x2=x2, part=xp, part2=x2p)
+            out1 = self.conv1(n1, temb=temb_proj, **st)
+        h, hp = out1 if stats else (out1, None)
         if self.conv_shortcut is not None:
             skip = self.conv_shortcut(x, x2=x2) if x2 is not None else self.conv_shortcut(x)
         else:
             skip = x if x2 is None else torch.cat([x, x2], dim=-1)
-        n2 = self.norm2(h, silu=True, part=hp)
-        if stats:
-            return self.conv2(n2, residual=skip, stats="gn")
-        return self.conv2(n2, residual=skip), None
+        if FUSED_GN_CONV and h.shape[-1] % 8 == 0:
+            sc, sh = self.norm2.scale_shift(h, part=hp)
+            out = self.conv2(h, norm=(sc, sh, "silu"), residual=skip, **st)
+        else:
+            out = self.conv2(self.norm2(h, silu=True, part=hp), residual=skip, **st)
+        return out if stats else (out, None)
 
 
 class GEGLU(nn.Module):

@@ -90,6 +90,13 @@ def _gn_tickets(x: torch.Tensor, n: int) -> Optional[torch.Tensor]:
     return t
 
 
+def _scale_shift_pair(n: int, c: int, device):
+    """GroupNorm (scale, shift) [n, c] fp32 as the two halves of ONE allocation (shift = scale + n c): the layout
+    the halo-tiled conv's scale / shift DMA reads (csrc/kernels/conv_halo.hip)."""
+    ss = torch.empty(2, n, c, dtype=torch.float32, device=device)
+    return ss[0], ss[1]
+
+
 def groupnorm_stats(x: torch.Tensor, gamma, beta, groups: int, eps: float, x2: Optional[torch.Tensor] = None):
     """Channels-last GroupNorm statistics. x [N, ..., C] -> (scale, shift) fp32 [N, C].
     With ``x2`` the statistics are those of ``cat([x, x2], -1)`` without materialising it."""
@@ -101,8 +108,7 @@ def groupnorm_stats(x: torch.Tensor, gamma, beta, groups: int, eps: float, x2: O
         xx = torch.cat([x3, x23], -1) if x23 is not None else x3
         return ref.groupnorm_stats(xx, gamma, beta, groups, eps)
     part = torch.empty(N * 256 * groups * 2, dtype=torch.float32, device=x.device)
-    scale = torch.empty(N, C, dtype=torch.float32, device=x.device)
-    shift = torch.empty(N, C, dtype=torch.float32, device=x.device)
+    scale, shift = _scale_shift_pair(N, C, x.device)
     _K().groupnorm_stats(x3, x23, gamma, beta, part, scale, shift, _gn_tickets(x, N), int(groups), float(eps))
     return scale, shift
 
@@ -346,8 +352,7 @@ def groupnorm_stats_from_partials(part: torch.Tensor, gamma, beta, groups: int, 
     C2 = part2.shape[-2] if part2 is not None else 0
     if not part.is_cuda:
         return ref.groupnorm_from_partials(part, part2, C1, C2, nimg, hw, gamma, beta, groups, eps)
-    scale = torch.empty(nimg, C1 + C2, dtype=torch.float32, device=part.device)
-    shift = torch.empty_like(scale)
+    scale, shift = _scale_shift_pair(nimg, C1 + C2, part.device)
     _K().groupnorm_from_partials(part, part2, C1, C2, nimg, hw, gamma, beta, scale, shift, int(groups), float(eps))
     return scale, shift
 
@@ -409,6 +414,13 @@ def bmm(a: torch.Tensor, w: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
     return y
 
 
+def set_halo_conv(mode: int = -1, waves: int = -1) -> int:
+    """Routing of the halo-tiled conv (csrc/kernels/conv_halo.hip): mode 0 off, 1 GroupNorm-fused convs (default,
+    SHAI_HALO_CONV), 2 also plain 3x3 convs; waves 4 / 8 pins its wave layout (0: default).  -1 keeps a setting.
+    Returns the previous mode (A/B in one process)."""
+    return int(_K().set_halo_conv(int(mode), int(waves)))
+
+
 def conv2d(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], kh: int, kw: int, stride: int = 1,
            pad: int = 0, upsample: bool = False, x2: Optional[torch.Tensor] = None, norm=None,
            temb: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None, act=None,
@@ -416,7 +428,9 @@ def conv2d(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor]
     """NHWC implicit-GEMM convolution with fused prologue/epilogue.
 
     norm = (scale [N,Cin] f32, shift [N,Cin] f32, act) applies GroupNorm(+act) to
-    the gathered input; x2 is concatenated on channels; upsample reads a
+    the input: on the GPU the halo-tiled conv normalises each staged element once in LDS (3x3 stride-1 convs of the
+    supported geometries, scale / shift from ``groupnorm_stats*``), other shapes get one vectorised apply pass and
+    the tuned conv; x2 is concatenated on channels; upsample reads a
     nearest-2x view; temb [N, Cout] is a per-image bias; residual is added last.
     stats="gn" / "ln": also return statistics of the output for the next norm, as ``linear_stats`` -- (out, st);
     st is None when the output shape cannot carry them (``stats_supported``).
