@@ -158,9 +158,11 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_halo_kernel(const GemmArgs
 #pragma unroll
     for (int u = 0; u < WJ; ++u) {
       const int q = wid + WAVES * u;
+      // (the offset is computed into a variable: a conditional expression as the builtin's argument silently
+      // drops the host-side kernel stub -- the .o then references an undefined __device_stub__)
+      const uint32_t off = woff[u] == HC_OOB ? HC_OOB : woff[u] + koff;
       if (q < BN / 8)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (hc_lds_void*)(base + q * 8 * HC_BK), 16,
-                                                 woff[u] == HC_OOB ? HC_OOB : woff[u] + koff, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (hc_lds_void*)(base + q * 8 * HC_BK), 16, off, 0, 0, 0);
     }
   };
 
