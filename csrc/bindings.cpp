@@ -1647,7 +1647,6 @@ TORCH_LIBRARY(shai, m) {
   m.def("layernorm_mod(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, int rows_per_mod, float eps) -> ()");
   m.def("qk_norm_rope(Tensor(a!) x, Tensor? q_w, Tensor? k_w, Tensor? cos, Tensor? sin, int H, int D, int S, float eps) -> ()");
   m.def("conv2d(Tensor x, Tensor? x2, Tensor w, Tensor(a!) out, Tensor? bias, Tensor? bias2d, Tensor? residual, Tensor? in_scale, Tensor? in_shift, int in_act, int kh, int kw, int stride, int pad, bool upsample, int act, float res_alpha, Tensor? ln_mr=None, Tensor? ln_s=None, Tensor(b!)? gn_part=None, Tensor(c!)? ln_stats=None, float ln_eps=1e-5) -> ()");
-  m.def("set_halo_conv(int mode, int waves=-1) -> int");
   m.def("flash_attn(Tensor q, Tensor k, Tensor v, Tensor(a!) o, float scale, bool causal, int causal_offset, Tensor? kv_lens, Tensor? q_lens, Tensor? bias, Tensor? block_table) -> ()");
   m.def("paged_attn_varlen(Tensor q, Tensor k_cache, Tensor v_cache, Tensor(a!) o, Tensor block_table, Tensor kv_lens, Tensor q_lens, Tensor q_start, int max_q, float scale, bool causal) -> ()");
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor(a!) o, Tensor block_table, Tensor ctx_lens, Tensor(b!) ws, int num_splits, float scale) -> ()");
@@ -1671,6 +1670,7 @@ TORCH_LIBRARY(shai, m) {
   m.def("gemm_tuning() -> str[]", &gemm_tuning);
   m.def("gemm_tuning_export() -> str[]", &gemm_tuning_export);
   m.def("gemm_tuning_import(str[] entries) -> int", &gemm_tuning_import);
+  m.def("set_halo_conv(int mode, int waves=-1) -> int", &set_halo_conv);
 }
 
 TORCH_LIBRARY_IMPL(shai, CUDA, m) {
@@ -1689,7 +1689,6 @@ TORCH_LIBRARY_IMPL(shai, CUDA, m) {
   m.impl("layernorm_mod", &layernorm_mod);
   m.impl("qk_norm_rope", &qk_norm_rope);
   m.impl("conv2d", &conv2d);
-  m.impl("set_halo_conv", &set_halo_conv);
   m.impl("flash_attn", &flash_attn);
   m.impl("paged_attn_varlen", &paged_attn_varlen);
   m.impl("decode_attn", &decode_attn);

@@ -29,6 +29,11 @@ CSRC = os.path.join(ROOT, "csrc")
 PKG = os.path.join(ROOT, "scalable-hw-agnostic-inference_amd")
 OUT = os.path.join(PKG, "_native")
 BUILD = os.path.join(ROOT, "build", "native")
+# device debug flavour (--debug / build(debug=True)): -DSHAI_KERNEL_DEBUG (device bounds asserts on DMA offsets, LDS
+# indices and slot ids in the hand-scheduled kernels; hazard-safe waits: counted vmcnt -> vmcnt(0), wider s_nop
+# margins), built into its own directories; SHAI_KERNEL_DEBUG=1 makes shai_amd.native load it
+OUT_DEBUG = os.path.join(PKG, "_native_debug")
+BUILD_DEBUG = os.path.join(ROOT, "build", "native_debug")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -57,10 +62,12 @@ def torch_paths():
     return inc, lib, abi
 
 
-def write_ninja(path: str) -> dict:
+def write_ninja(path: str, out: str = OUT, build_dir: str = BUILD, debug: bool = False) -> dict:
     inc, tlib, abi = torch_paths()
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     kflags = f"--offload-arch={ARCH} -O3 -std=c++17 -fPIC -ffp-contract=fast -Wno-unused-result -I{CSRC}"
+    if debug:
+        kflags += " -DSHAI_KERNEL_DEBUG"
     incs = " ".join(f"-isystem {p}" for p in inc)
     bflags = (f"-O2 -std=c++17 -fPIC -D_GLIBCXX_USE_CXX11_ABI={abi} -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 "
               f"-I{CSRC} {incs} -isystem {ROCM}/include -Wno-deprecated-declarations")
@@ -105,7 +112,7 @@ def write_ninja(path: str) -> dict:
         for s in srcs:
             if not os.path.exists(os.path.join(CSRC, s)):
                 continue
-            o = os.path.join(BUILD, s.replace("/", "_") + ".o")
+            o = os.path.join(build_dir, s.replace("/", "_") + ".o")
             lines.append(f"build {o}: {rule} {os.path.join(CSRC, s)} | {os.path.join(CSRC, 'kernels', 'common.h')} "
                          f"{os.path.join(CSRC, 'kernels', 'launchers.h')}")
             if s in EXTRA_KFLAGS:
@@ -114,15 +121,15 @@ def write_ninja(path: str) -> dict:
         return out
 
     k = objs(KERNEL_SRCS, "hip") + objs(BINDING_SRCS, "cxx")
-    targets["kernels"] = os.path.join(OUT, "libshai_kernels.so")
+    targets["kernels"] = os.path.join(out, "libshai_kernels.so")
     lines.append(f"build {targets['kernels']}: link_kernels {' '.join(k)}")
     r = objs(RUNTIME_SRCS, "rcxx")
     if r:
-        targets["runtime"] = os.path.join(OUT, "libshai_runtime.so")
+        targets["runtime"] = os.path.join(out, "libshai_runtime.so")
         lines.append(f"build {targets['runtime']}: link_cxx {' '.join(r)}")
     c = objs(COMM_SRCS, "hip")
     if c:
-        targets["comm"] = os.path.join(OUT, "libshai_comm.so")
+        targets["comm"] = os.path.join(out, "libshai_comm.so")
         lines.append(f"build {targets['comm']}: link_hip {' '.join(c)}")
     lines.append("default " + " ".join(targets.values()))
     with open(path, "w") as f:
@@ -133,13 +140,14 @@ def write_ninja(path: str) -> dict:
 LAST_BUILD: dict = {}
 
 
-def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -> dict:
-    if clean and os.path.isdir(BUILD):
-        shutil.rmtree(BUILD)
-    os.makedirs(BUILD, exist_ok=True)
-    os.makedirs(OUT, exist_ok=True)
-    ninja_file = os.path.join(BUILD, "build.ninja")
-    targets = write_ninja(ninja_file)
+def build(clean: bool = False, jobs: int | None = None, verbose: bool = False, debug: bool = False) -> dict:
+    out, bdir = (OUT_DEBUG, BUILD_DEBUG) if debug else (OUT, BUILD)
+    if clean and os.path.isdir(bdir):
+        shutil.rmtree(bdir)
+    os.makedirs(bdir, exist_ok=True)
+    os.makedirs(out, exist_ok=True)
+    ninja_file = os.path.join(bdir, "build.ninja")
+    targets = write_ninja(ninja_file, out, bdir, debug)
     ninja = shutil.which("ninja")
     if ninja is None:
         import ninja as _nj  # pip package ships the binary
@@ -149,7 +157,7 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
         cmd += ["-j", str(jobs)]
     if verbose:
         cmd.append("-v")
-    r = subprocess.run(cmd, cwd=BUILD, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    r = subprocess.run(cmd, cwd=bdir, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     sys.stdout.write(r.stdout)
     if r.returncode != 0:
         raise subprocess.CalledProcessError(r.returncode, cmd, r.stdout)
@@ -178,8 +186,9 @@ def main():
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("-j", type=int, default=min(16, os.cpu_count() or 8))
     ap.add_argument("-v", action="store_true")
+    ap.add_argument("--debug", action="store_true", help="device debug flavour into _native_debug/")
     a = ap.parse_args()
-    t = build(a.clean, a.j, a.v)
+    t = build(a.clean, a.j, a.v, a.debug)
     for k, v in t.items():
         print(f"{k}: {v}")
     print(summary())

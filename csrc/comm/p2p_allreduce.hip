@@ -26,6 +26,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "kernels/common.h"  // SHAI_DASSERT (device debug flavour)
+
 namespace {
 
 constexpr int kMaxRanks = 8;
@@ -129,6 +131,8 @@ template <bool STAGED>
 __global__ void __launch_bounds__(512) p2p_one_shot(Peers P, int rank, int world, const uint4* in,
                                                     uint4* out, long n16, Epi E, size_t off) {
   __shared__ uint32_t s_epoch;
+  // debug build: rank / world within the peer table, this block's epoch slot inside the signal area
+  SHAI_DASSERT(world >= 1 && world <= kMaxRanks && rank >= 0 && rank < world && blockIdx.x < (unsigned)kMaxBlocks);
   Layout* me = reinterpret_cast<Layout*>(P.base[rank]);
   if (threadIdx.x == 0) {
     const uint32_t e = me->epoch[blockIdx.x] + 1;
@@ -185,6 +189,8 @@ template <bool STAGED>
 __global__ void __launch_bounds__(512) p2p_two_shot(Peers P, int rank, int world, const uint4* in, uint4* out,
                                                     long n16, size_t slot_bytes, Epi E, size_t off) {
   __shared__ uint32_t s_epoch;
+  // debug build: rank / world within the peer table, this block's epoch slot inside the signal area
+  SHAI_DASSERT(world >= 1 && world <= kMaxRanks && rank >= 0 && rank < world && blockIdx.x < (unsigned)kMaxBlocks);
   Layout* me = reinterpret_cast<Layout*>(P.base[rank]);
   if (threadIdx.x == 0) {
     const uint32_t e = me->epoch[blockIdx.x] + 1;
@@ -196,6 +202,7 @@ __global__ void __launch_bounds__(512) p2p_two_shot(Peers P, int rank, int world
   const long seg = (n16 + world - 1) / world;
   const long stride = (long)gridDim.x * blockDim.x;
   const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  SHAI_DASSERT(off % 16 == 0 && off + (size_t)n16 * 16 <= slot_bytes);  // the message (slab) stays in slot A / B
   uint4* slotA = reinterpret_cast<uint4*>(P.base[rank] + kDataOff + off);
   uint4* slotB = reinterpret_cast<uint4*>(P.base[rank] + kDataOff + slot_bytes + off);
   if (!STAGED) {
@@ -241,6 +248,8 @@ __global__ void __launch_bounds__(512) p2p_two_shot(Peers P, int rank, int world
 __global__ void __launch_bounds__(512) p2p_all_gather(Peers P, int rank, int world, const uint4* in, uint4* out,
                                                       long n16) {
   __shared__ uint32_t s_epoch;
+  // debug build: rank / world within the peer table, this block's epoch slot inside the signal area
+  SHAI_DASSERT(world >= 1 && world <= kMaxRanks && rank >= 0 && rank < world && blockIdx.x < (unsigned)kMaxBlocks);
   Layout* me = reinterpret_cast<Layout*>(P.base[rank]);
   if (threadIdx.x == 0) {
     const uint32_t e = me->epoch[blockIdx.x] + 1;

@@ -71,6 +71,10 @@ __global__ void __launch_bounds__(256, OCC) flash64_dma_kernel(const AttnArgs p)
     const uint32_t ok0 = key < kv_len ? 0u : 0x80000000u, ok1 = key + 8 < kv_len ? 0u : 0x80000000u;
     const uint32_t r0 = (uint32_t)((long)key * p.k_ts * 2), r1 = (uint32_t)((long)(key + 8) * p.k_ts * 2);
     const uint32_t v0 = (uint32_t)((long)key * p.v_ts * 2), v1 = (uint32_t)((long)(key + 8) * p.v_ts * 2);
+    // debug: a valid key's byte offset fits the 31-bit buffer range (no wrap into the OOB sentinel), ring slot
+    SHAI_DASSERT(ok0 != 0u || ((long)key * p.k_ts * 2 + 128 < 0x80000000L && (long)key * p.v_ts * 2 + 128 < 0x80000000L));
+    SHAI_DASSERT(ok1 != 0u || ((long)(key + 8) * p.k_ts * 2 + 128 < 0x80000000L));
+    SHAI_DASSERT(stage == 0 || stage == 1);  // two K/V stages of LDS (launchers size 2 x 2 x 64 x 64)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (f3_lds_void*)(ks + (wid * 16) * D), 16, (r0 + kch0 * 16) | ok0, 0, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (f3_lds_void*)(ks + (wid * 16 + 8) * D), 16, (r1 + kch1 * 16) | ok1, 0, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (f3_lds_void*)(vs + (wid * 16) * D), 16, (v0 + vch0 * 16) | ok0, 0, 0, 0);
@@ -285,6 +289,10 @@ __global__ void __launch_bounds__(256, 2) flash64x2_kernel(const AttnArgs p) {
     const uint32_t ok0 = key < kv_len ? 0u : 0x80000000u, ok1 = key + 8 < kv_len ? 0u : 0x80000000u;
     const uint32_t r0 = (uint32_t)((long)key * p.k_ts * 2), r1 = (uint32_t)((long)(key + 8) * p.k_ts * 2);
     const uint32_t v0 = (uint32_t)((long)key * p.v_ts * 2), v1 = (uint32_t)((long)(key + 8) * p.v_ts * 2);
+    // debug: a valid key's byte offset fits the 31-bit buffer range (no wrap into the OOB sentinel), ring slot
+    SHAI_DASSERT(ok0 != 0u || ((long)key * p.k_ts * 2 + 128 < 0x80000000L && (long)key * p.v_ts * 2 + 128 < 0x80000000L));
+    SHAI_DASSERT(ok1 != 0u || ((long)(key + 8) * p.k_ts * 2 + 128 < 0x80000000L));
+    SHAI_DASSERT(stage == 0 || stage == 1);  // two K/V stages of LDS (launchers size 2 x 2 x 64 x 64)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (f3_lds_void*)(ks + (wid * 16) * D), 16, (r0 + kch0 * 16) | ok0, 0, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (f3_lds_void*)(ks + (wid * 16 + 8) * D), 16, (r1 + kch1 * 16) | ok1, 0, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (f3_lds_void*)(vs + (wid * 16) * D), 16, (v0 + vch0 * 16) | ok0, 0, 0, 0);

@@ -9,6 +9,19 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Device debug flavour (csrc/build.py --debug defines SHAI_KERNEL_DEBUG): SHAI_DASSERT bounds-checks DMA offsets,
+// LDS indices and ring slot ids in the hand-scheduled kernels (a failing check prints its condition and aborts the
+// kernel), and SHAI_DEBUG selects hazard-safe forms of hand-counted waits (vmcnt(0) for counted vmcnt(N), wider
+// s_nop margins after inline-asm MFMAs).  Both compile to nothing in the production build.
+#ifdef SHAI_KERNEL_DEBUG
+#include <cassert>
+#define SHAI_DASSERT(c) assert(c)
+#define SHAI_DEBUG 1
+#else
+#define SHAI_DASSERT(c) ((void)0)
+#define SHAI_DEBUG 0
+#endif
+
 namespace shai {
 
 constexpr int kWave = 64;
@@ -143,3 +156,8 @@ __device__ __forceinline__ float apply_act_rt(int act, float x) {
 }  // namespace shai
 
 #define SHAI_CHECK_LAUNCH() (void)hipGetLastError()
+
+// debug check of a 16-B buffer-DMA offset against its buffer: in range, or the out-of-bounds zero-fill sentinel
+// (any offset at or above the sentinel is out of the <= 2^31-byte buffer range: zero fill)
+#define SHAI_DASSERT_DMA(off, bytes, oob) \
+  SHAI_DASSERT((uint32_t)(off) >= (uint32_t)(oob) || (long)(off) + 16 <= (long)(bytes))

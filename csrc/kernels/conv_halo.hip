@@ -126,6 +126,8 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_halo_kernel(const GemmArgs
 #pragma unroll
     for (int j = 0; j < HJ; ++j) {
       const uint32_t off = hsrc[j] >= 0 ? ((uint32_t)hsrc[j] * cs + cb) * 2u : HC_OOB;
+      SHAI_DASSERT_DMA(off, src_pix * cs * 2, HC_OOB);
+      SHAI_DASSERT((wid * HJ + j + 1) * 8 <= HC_HPIX_MAX);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(second ? rA2 : rA, (hc_lds_void*)(base + j * 8 * HC_BK), 16, off, 0, 0,
                                                0);
     }
@@ -137,6 +139,7 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_halo_kernel(const GemmArgs
         uint32_t off = HC_OOB;
         if (lane < 32)
           off = (uint32_t)(((lane >= 16 ? p.Nimg * p.Cin : 0) + img * p.Cin + c * HC_BK + (lane & 15) * 4) * 4);
+        SHAI_DASSERT_DMA(off, (long)2 * p.Nimg * p.Cin * 4, HC_OOB);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rS, (hc_lds_void*)(ssb + sb * T::SS_FLOATS), 16, off, 0, 0, 0);
       }
     }
@@ -161,6 +164,8 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_halo_kernel(const GemmArgs
       // (the offset is computed into a variable: a conditional expression as the builtin's argument silently
       // drops the host-side kernel stub -- the .o then references an undefined __device_stub__)
       const uint32_t off = woff[u] == HC_OOB ? HC_OOB : woff[u] + koff;
+      SHAI_DASSERT_DMA(off, (long)p.N * p.ldw * 2, HC_OOB);
+      SHAI_DASSERT(t < nk && st >= 0 && st < 2);
       if (q < BN / 8)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (hc_lds_void*)(base + q * 8 * HC_BK), 16, off, 0, 0, 0);
     }
@@ -202,6 +207,7 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_halo_kernel(const GemmArgs
   }
   auto a_off = [&](int i, int ks, int tsh) {
     const int pp = hp0[i] + tsh;
+    SHAI_DASSERT(pp >= 0 && pp < g.HPIX && g.HPIX <= HC_HPIX_MAX);
     return pp * HC_BK + (((4 * ks + fq) ^ (pp & 7)) << 3);
   };
   auto w_off = [&](int j, int ks) { return (wc * WN + 16 * j + fr) * HC_BK + (((4 * ks + fq) ^ ((fr >> 1) & 7)) << 3); };

@@ -223,12 +223,15 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
     if ((g & 1) || g == 8) {
       uint32_t off = woff[j] + (uint32_t)k0 * 2;
       if (ktail && k0 + kchw[j] >= k_end) off = G4_OOB;
+      SHAI_DASSERT_DMA(off, (long)p.N * p.ldw * 2, G4_OOB);
+      SHAI_DASSERT(buf >= 0 && buf < 2);
       g4_glds(rW, sa + G4_BM * G4_BK + (wid * (BN / 8) + j * 8) * G4_BK, off);
       return;
     }
     if constexpr (CONV == 0) {
       uint32_t off = aoff[j] + (uint32_t)k0 * 2;
       if (ktail && k0 + kch[j] >= k_end) off = G4_OOB;
+      SHAI_DASSERT_DMA(off, (long)p.M * p.lda * 2, G4_OOB);
       g4_glds(rA, sa + (wid * 32 + j * 8) * G4_BK, off);
     } else {
       const bool second = p.A2 != nullptr && cp.c >= p.Cin1;
@@ -246,6 +249,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
         off = ok ? (uint32_t)(px * cs + cb) * 2 + aoff[j] : G4_OOB;
       }
       if (k0 >= k_end) off = G4_OOB;
+      SHAI_DASSERT_DMA(off, (long)p.Nimg * p.H * p.Wd * cs * 2, G4_OOB);
       g4_glds(second ? rA2 : rA, sa + (wid * 32 + j * 8) * G4_BK, off);
     }
   };

@@ -181,6 +181,8 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const GemmArgs p) {
     const bool oob_k = k0 + ((j & 1) ? kch1 : kch0) >= p.K;
     if (g >= AJ) {
       const uint32_t off = oob_k ? W4_OOB : woff[j] + (uint32_t)k0 * 2;
+      SHAI_DASSERT_DMA(off, (long)p.N * p.ldw * 2, W4_OOB);
+      SHAI_DASSERT(stage == 0 || stage == 1);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (w4_lds_void*)(base + (BM + wid * (BN / 4) + j * 8) * W4_BK), 16,
                                                off, 0, 0, 0);
       return;
@@ -188,6 +190,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const GemmArgs p) {
     bf16_t* dst = base + (wid * (BM / 4) + j * 8) * W4_BK;
     if constexpr (CONV == 0) {
       const uint32_t off = oob_k ? W4_OOB : aoff[j] + (uint32_t)k0 * 2;
+      SHAI_DASSERT_DMA(off, (long)p.M * p.lda * 2, W4_OOB);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (w4_lds_void*)dst, 16, off, 0, 0, 0);
     } else {
       // filter tap (kh, kw) and channel base c of this K-tile (wave-uniform; Cin % 64 == 0)
@@ -207,6 +210,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const GemmArgs p) {
         off = ok ? (uint32_t)(px * cs + cb) * 2 + aoff[j] : W4_OOB;
       }
       if (k0 >= p.K) off = W4_OOB;
+      SHAI_DASSERT_DMA(off, (long)p.Nimg * p.H * p.Wd * cs * 2, W4_OOB);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(second ? rA2 : rA, (w4_lds_void*)dst, 16, off, 0, 0, 0);
     }
   };

@@ -199,6 +199,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(const GemmArgs p, int s
 #pragma unroll
       for (int h = 0; h < AH; ++h) {
         const uint32_t off = arow[h] < rows ? (uint32_t)m0 * (uint32_t)(p.lda * 2) + aoff[h] + 128u * t : WS_OOB;
+        SHAI_DASSERT_DMA(off, (long)p.M * p.lda * 2, WS_OOB);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (ws_lds_void*)(st + t * BM * 128 + 8 * (wid * AH + h) * 128), 16,
                                                  off, 0, 0, 0);
       }
@@ -206,6 +207,7 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(const GemmArgs p, int s
 #pragma unroll
       for (int q = 0; q < T::R_DMA; ++q) {
         const uint32_t off = rrow[q] < rows ? (uint32_t)m0 * (uint32_t)(p.ldr * 2) + roff[q] : WS_OOB;
+        SHAI_DASSERT_DMA(off, (long)p.M * p.ldr * 2, WS_OOB);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rR, (ws_lds_void*)(rs + 1024 * (wid * T::R_DMA + q)), 16, off, 0, 0,
                                                  0);
       }
@@ -520,7 +522,8 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(const GemmArgs p, int s
   constexpr int NST = GLU ? RB + 1 : T::NST;   // store instructions per wave per full tile
   auto tile = [&](float4_ (&acc)[RB][WS_NB], const float4_ (&prev)[RB][WS_NB], int i) {
     // outstanding after tile i's DMA: tile i + 1's DMA and the stores of tiles i - 2 and i - 1
-    if (i >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T::DMA + 2 * NST) : "memory");
+    if constexpr (SHAI_DEBUG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // debug: hazard-safe drain
+    else if (i >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T::DMA + 2 * NST) : "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T::DMA) : "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slots restaged next are done
     __builtin_amdgcn_sched_barrier(0);
@@ -556,7 +559,8 @@ __global__ void __launch_bounds__(256, 1) gemm_ws_kernel(const GemmArgs p, int s
         else
           asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[rb][j]) : "a"(wf[j][s]), "v"(xc));
       }
-      asm volatile("s_nop 1" ::: "memory");  // WAR margin: a later read may land in this step's X registers
+      if constexpr (SHAI_DEBUG) asm volatile("s_nop 7" ::: "memory");  // debug: wide hazard margin
+      else asm volatile("s_nop 1" ::: "memory");  // WAR margin: a later read may land in this step's X registers
       // epilogue units of the previous tile, spread over the first half of the steps
       if constexpr (IL) {
 #pragma unroll

@@ -14,7 +14,9 @@ import threading
 
 import torch
 
-_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native")
+# SHAI_KERNEL_DEBUG=1: the device debug flavour (``python csrc/build.py --debug``: bounds asserts + hazard-safe waits)
+DEBUG = os.environ.get("SHAI_KERNEL_DEBUG", "0") == "1"
+_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native_debug" if DEBUG else "_native")
 KERNELS_LIB = os.path.join(_DIR, "libshai_kernels.so")
 RUNTIME_LIB = os.path.join(_DIR, "libshai_runtime.so")
 COMM_LIB = os.path.join(_DIR, "libshai_comm.so")
