@@ -47,7 +47,7 @@ EXTRA_KFLAGS = {"kernels/attention3.hip": "-mllvm -amdgpu-mfma-vgpr-form -fno-sl
                 "kernels/attention2.hip": "-mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize",
                 "kernels/gemm_w4.hip": "-mllvm -pragma-unroll-threshold=100000",
                 "kernels/gemm_ws.hip": "-mllvm -pragma-unroll-threshold=100000 -fno-slp-vectorize",
-                "kernels/conv_halo.hip": "-mllvm -pragma-unroll-threshold=100000"}
+                "kernels/conv_halo.hip": "-mllvm -pragma-unroll-threshold=100000 -fno-slp-vectorize"}
 BINDING_SRCS = ["bindings.cpp"]
 RUNTIME_SRCS = ["runtime/block_manager.cpp", "runtime/scheduler.cpp"]
 COMM_SRCS = ["comm/p2p_allreduce.hip"]

@@ -32,6 +32,8 @@
 // (y / 2, x / 2)), and with a two-source channel concat (A2 from channel Cin1, 64-aligned).
 #include "gemm_epilogue.h"
 
+#include <type_traits>
+
 namespace shai {
 
 typedef __bf16 hcbf16x8 __attribute__((ext_vector_type(8)));
@@ -171,8 +173,15 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_halo_kernel(const GemmArgs
     }
   };
 
-  // ---- normalisation of this lane's own halo slots (j0 .. j0 + NJ - 1) of buffer hb with scale / shift slot sb.
+  // ---- normalisation of this lane's own halo slots of buffer hb with the scale / shift of slot sb: branch-free
+  // (padding slots select 0, the DMA's zero fill; the whole step stays ONE basic block, so hipcc interleaves this
+  // VALU work with the step's MFMAs).  silu(y) = y / (1 + 2^(-y log2 e)), y = x sc + sh: fma, mul, v_exp, add,
+  // v_rcp, mul per element (per-chunk exp2 coefficients would save the mul but cost 16 registers: the 8-wave build
+  // sits at the 256-register cap).
   float sc[8], sh[8];
+  uint32_t hvalid = 0;   // bit j: this lane's halo slot j is a real pixel
+#pragma unroll
+  for (int j = 0; j < HJ; ++j) hvalid |= (hsrc[j] >= 0 ? 1u : 0u) << j;
   auto load_ss = [&](int sb) {
     const float* s = ssb + sb * T::SS_FLOATS;
     const float4_ a0 = *reinterpret_cast<const float4_*>(s + hcc * 8);
@@ -186,13 +195,17 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_halo_kernel(const GemmArgs
     }
   };
   auto norm_slot = [&](int hb, int j) {
-    if (hsrc[j] < 0) return;   // padding keeps the DMA's zero fill
     uint4_* q = reinterpret_cast<uint4_*>(halo + hb * T::HALO_ELEMS + ((wid * HJ + j) * 8) * HC_BK) + lane;
     const uint4_ v = *q;
     float f[8];
     unpack8(v, f);
+    const bool ok = (hvalid >> j) & 1u;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = silu_f(fmaf(f[e], sc[e], sh[e]));
+    for (int e = 0; e < 8; ++e) {
+      const float y = fmaf(f[e], sc[e], sh[e]);
+      const float ex = __builtin_amdgcn_exp2f(y * -1.4426950408889634f);
+      f[e] = ok ? y * rcp_f(1.0f + ex) : 0.f;
+    }
     *q = pack8(f);
   };
 
@@ -247,8 +260,10 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_halo_kernel(const GemmArgs
   __builtin_amdgcn_sched_barrier(0);
   read_frags(0, 0, x0, w0);
 
-  // normalisation slots of the next chunk done at tap `tap` of the current one (taps 1..7: the next chunk's DMA
-  // was issued at tap 0 and waited for at tap 1's vmcnt(0))
+  // The main loop walks the chunks with the 9 taps unrolled, so every per-tap decision is compile-time and a step is
+  // one basic block: the next chunk's normalisation slots (taps 1..7; its DMA was issued at tap 0 and waited for by
+  // tap 1's vmcnt(0)) interleave with the step's MFMAs.  Past the last chunk / tile the DMAs re-load the last valid
+  // chunk / tile and the normalisation runs over the idle halo buffer: harmless (never read), and no branch.
   constexpr int NPT = (HJ + 6) / 7;
   auto seg_a = [&](int t, bool first) {
     read_frags(t, 1, x1, w1);
@@ -259,7 +274,9 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_halo_kernel(const GemmArgs
       for (int j = 0; j < BNB; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[j], x0[i], first ? z : acc[i][j], 0, 0, 0);
   };
-  auto seg_bc = [&](int t) {
+  auto seg_bc = [&](int c, auto tap_c) {
+    constexpr int TAP = decltype(tap_c)::value;
+    const int t = 9 * c + TAP;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
@@ -269,27 +286,22 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_halo_kernel(const GemmArgs
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    const int c = t / 9, tap = t - 9 * c;
-    if (t + 2 < nk) dma_w(t + 2, t & 1);
-    const bool next_chunk = c + 1 < g.nchunks;
-    if (tap == 0 && next_chunk) {
-      dma_halo(c + 1, (c + 1) & 1);
-      dma_ss(c + 1, (c + 1) & 1);
+    const int cn = min(c + 1, g.nchunks - 1);   // the next chunk (the last one again past the end)
+    dma_w(min(t + 2, nk - 1), t & 1);
+    if constexpr (TAP == 0) {
+      dma_halo(cn, (c + 1) & 1);
+      dma_ss(cn, (c + 1) & 1);
     }
-    if (t + 1 < nk) read_frags(t + 1, 0, x0, w0);
+    read_frags(min(t + 1, nk - 1), 0, x0, w0);
+    if constexpr (MODE != 0 && TAP == 1) load_ss((c + 1) & 1);
 #pragma unroll
     for (int i = 0; i < BMB; ++i)
 #pragma unroll
       for (int j = 0; j < BNB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[j], x1[i], acc[i][j], 0, 0, 0);
-    if constexpr (MODE != 0) {
-      if (next_chunk && tap >= 1 && tap <= 7) {
-        if (tap == 1) load_ss((c + 1) & 1);
+    if constexpr (MODE != 0 && TAP >= 1 && TAP <= 7) {
 #pragma unroll
-        for (int u = 0; u < NPT; ++u) {
-          const int j = (tap - 1) * NPT + u;
-          if (j < HJ) norm_slot((c + 1) & 1, j);
-        }
-      }
+      for (int u = 0; u < NPT; ++u)
+        if ((TAP - 1) * NPT + u < HJ) norm_slot((c + 1) & 1, (TAP - 1) * NPT + u);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -297,13 +309,26 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_halo_kernel(const GemmArgs
 #pragma unroll
     for (int j = 0; j < BNB; ++j) asm volatile("" : "+v"(w0[j]));
   };
+  auto step = [&](int c, auto tap_c) {   // seg_bc(t) then seg_a(t + 1)
+    constexpr int TAP = decltype(tap_c)::value;
+    seg_bc(c, tap_c);
+    if (TAP < 8 || c + 1 < g.nchunks) seg_a(9 * c + TAP + 1, false);
+  };
 
   seg_a(0, true);
-  for (int t = 0; t + 1 < nk; ++t) {
-    seg_bc(t);
-    seg_a(t + 1, false);
+  for (int c = 0; c < g.nchunks; ++c) {
+    step(c, std::integral_constant<int, 0>{});
+    step(c, std::integral_constant<int, 1>{});
+    step(c, std::integral_constant<int, 2>{});
+    step(c, std::integral_constant<int, 3>{});
+    step(c, std::integral_constant<int, 4>{});
+    step(c, std::integral_constant<int, 5>{});
+    step(c, std::integral_constant<int, 6>{});
+    step(c, std::integral_constant<int, 7>{});
+    step(c, std::integral_constant<int, 8>{});
   }
-  seg_bc(nk - 1);
+  // every LDS-DMA (the re-loads past the end included) has landed before the epilogue reuses the LDS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // ---- epilogue (host: M % 256 == 0, N % BN == 0, 16-B aligned operands, ldc = ldr = N): lane owns pixel
   // m0 + 64 wr + 16 i + fr and columns n0 + wc WN + 16 j + 4 fq .. + 3

@@ -28,6 +28,14 @@ SHAPES = [  # (N, H, W, C1, C2, Cout, temb, residual)
 ]
 
 
+PLAIN = [  # (N, H, W, C, Cout, upsample)
+    (64, 32, 32, 640, 640, True),     # up block 2 -> 64x64 level
+    (64, 16, 16, 1280, 1280, True),   # up block 1 -> 32x32 level
+    (64, 64, 64, 320, 320, False),
+    (64, 32, 32, 640, 640, False),
+]
+
+
 def timeit(fn, n=20):
     for _ in range(3):
         fn()
@@ -81,6 +89,37 @@ def main():
         flop = 2.0 * N * H * W * Co * 9 * cin
         row = {"shape": f"{N}x{H}x{W} {C1}+{C2}->{Co}" + (" temb" if te else "") + (" res" if re else ""),
                "gflop": round(flop / 1e9, 1)}
+        for k, v in res.items():
+            us = min(v)
+            row[k + "_us"] = round(us, 1)
+            row[k + "_tfs"] = round(flop / us / 1e6, 1)
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    # plain 3x3 convs without a norm (upsample convs, conv2 of blocks whose input is not normalised): halo (mode 2)
+    # vs the tuned conv (mode 0)
+    for (N, H, W, C, Co, ups) in PLAIN[: args.shapes]:
+        torch.manual_seed(1)
+        x = torch.randn(N, H, W, C, device=dev).bfloat16()
+        cin = C
+        w = (torch.randn(Co, 9 * cin, device=dev) / (9 * cin) ** 0.5).bfloat16()
+        b = torch.zeros(Co, device=dev).bfloat16()
+
+        def plain():
+            return ops.conv2d(x, w, b, 3, 3, 1, 1, upsample=ups)
+
+        res = {}
+        ops.set_halo_conv(0, 0)
+        plain()
+        for _ in range(2):
+            ops.set_halo_conv(2, 8)
+            res.setdefault("halo8", []).append(timeit(plain))
+            ops.set_halo_conv(2, 4)
+            res.setdefault("halo4", []).append(timeit(plain))
+            ops.set_halo_conv(0, 0)
+            res.setdefault("conv", []).append(timeit(plain))
+        OH = 2 * H if ups else H
+        flop = 2.0 * N * OH * OH * Co * 9 * cin
+        row = {"shape": f"plain {N}x{H}x{W} {C}->{Co}" + (" up2x" if ups else ""), "gflop": round(flop / 1e9, 1)}
         for k, v in res.items():
             us = min(v)
             row[k + "_us"] = round(us, 1)
