@@ -26,15 +26,17 @@ namespace {
 
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
-// Halo-tiled conv routing (conv_halo.hip): 0 off, 1 GroupNorm-fused convs (default), 2 also plain 3x3 convs;
+// Halo-tiled conv routing (conv_halo.hip): 0 off (default), 1 GroupNorm-fused convs, 2 also plain 3x3 convs;
 // SHAI_HALO_CONV sets it, the set_halo_conv op changes it at run time (A/B in one process).  g_halo_waves: 0 = the
-// kernel's default wave layout (SHAI_HALO_WAVES), 4 / 8 pin one.
+// kernel's default wave layout (SHAI_HALO_WAVES), 4 / 8 pin one.  Off by default: at the SD2.1 batch-32 shapes the
+// in-LDS normalisation costs more than the apply pass it replaces (profiles/halo_conv_round6.md: e.g. 64x64x320
+// 561 us fused vs 497 us apply + tuned conv), so a norm= conv runs the apply pass + the tuned conv.
 int g_halo_mode = -1;
 int g_halo_waves = 0;
 int halo_conv_mode() {
   if (g_halo_mode < 0) {
     const char* e = getenv("SHAI_HALO_CONV");
-    g_halo_mode = e ? atoi(e) : 1;
+    g_halo_mode = e ? atoi(e) : 0;
   }
   return g_halo_mode;
 }
@@ -1019,8 +1021,8 @@ void conv2d(const Tensor& x, const optional<Tensor>& x2, const Tensor& w, const 
   }
   OutStats st;
   attach_norm_io(g, ln_mr, ln_s, gn_part, ln_stats, ln_eps, &st);
-  // Halo-tiled conv (conv_halo.hip): GroupNorm(+SiLU) convs (SHAI_HALO_CONV >= 1, default) and, at mode 2, every
-  // 3x3 stride-1 conv it supports; the output's GroupNorm partials come from its epilogue.
+  // Halo-tiled conv (conv_halo.hip): GroupNorm(+SiLU) convs (SHAI_HALO_CONV >= 1) and, at mode 2, every 3x3
+  // stride-1 conv it supports; the output's GroupNorm partials come from its epilogue.
   const int hmode = halo_conv_mode();
   if (hmode > 0 && g.row_mr == nullptr && st.ln_mr == nullptr && (g.in_scale != nullptr || hmode >= 2) &&
       shai::conv_halo_supported(g)) {

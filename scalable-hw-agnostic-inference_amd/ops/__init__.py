@@ -415,9 +415,9 @@ def bmm(a: torch.Tensor, w: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
 
 
 def set_halo_conv(mode: int = -1, waves: int = -1) -> int:
-    """Routing of the halo-tiled conv (csrc/kernels/conv_halo.hip): mode 0 off, 1 GroupNorm-fused convs (default,
-    SHAI_HALO_CONV), 2 also plain 3x3 convs; waves 4 / 8 pins its wave layout (0: default).  -1 keeps a setting.
-    Returns the previous mode (A/B in one process)."""
+    """Routing of the halo-tiled conv (csrc/kernels/conv_halo.hip): mode 0 off (default, SHAI_HALO_CONV), 1
+    GroupNorm-fused convs, 2 also plain 3x3 convs; waves 4 / 8 pins its wave layout (0: default).  -1 keeps a
+    setting.  Returns the previous mode (A/B in one process)."""
     return int(_K().set_halo_conv(int(mode), int(waves)))
 
 
@@ -428,9 +428,9 @@ def conv2d(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor]
     """NHWC implicit-GEMM convolution with fused prologue/epilogue.
 
     norm = (scale [N,Cin] f32, shift [N,Cin] f32, act) applies GroupNorm(+act) to
-    the input: on the GPU the halo-tiled conv normalises each staged element once in LDS (3x3 stride-1 convs of the
-    supported geometries, scale / shift from ``groupnorm_stats*``), other shapes get one vectorised apply pass and
-    the tuned conv; x2 is concatenated on channels; upsample reads a
+    the input: on the GPU one vectorised apply pass + the tuned conv inside the op (``set_halo_conv(1)``: the
+    halo-tiled conv normalises each staged element once in LDS instead -- measured slower at the SD2.1 shapes);
+    x2 is concatenated on channels; upsample reads a
     nearest-2x view; temb [N, Cout] is a per-image bias; residual is added last.
     stats="gn" / "ln": also return statistics of the output for the next norm, as ``linear_stats`` -- (out, st);
     st is None when the output shape cannot carry them (``stats_supported``).

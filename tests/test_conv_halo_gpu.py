@@ -46,6 +46,11 @@ def _restore_mode():
     ops.set_halo_conv(prev, 0)
 
 
+def test_default_mode_is_apply_pass(cuda):
+    """Off by default (profiles/halo_conv_round6.md): norm= convs take the apply pass + tuned conv."""
+    assert ops.set_halo_conv(-1, -1) == 0
+
+
 @pytest.mark.parametrize("waves", [8, 4])
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout", [
     (2, 64, 64, 320, 0, 320),     # UNet 64x64 level: 4 rows per tile, two 160-column N tiles
@@ -101,6 +106,7 @@ def test_padding_is_zero_after_the_norm(cuda):
     (a kernel that normalised the zero fill would shift every border output)."""
     ops.set_halo_conv(1, 0)
     x, _, w, b, _, _, sc, sh = _case(cuda, 1, 16, 16, 640, 0, 640, seed=3, temb=False, res=False)
+    assert ops.set_halo_conv(-1, -1) == 1
     sh = sh + 4.0
     ss = torch.stack([sc, sh]).contiguous()   # one allocation, as the kernel reads it
     y = ops.conv2d(x, w, b, 3, 3, 1, 1, norm=(ss[0], ss[1], "silu"))
