@@ -33,6 +33,7 @@
 #include "gemm_epilogue.h"
 
 #include <type_traits>
+#include <utility>
 
 namespace shai {
 
@@ -72,7 +73,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t hc_rsrc(const void* base, long
 }
 
 // MODE: 0 = the input as is, 2 = GroupNorm + SiLU in LDS.  UPS: nearest-2x upsampled input (MODE 0 only).
-template <int WAVES, int BNB, int MODE, bool UPS>
+// SGB (lab A/B): the normalisation hand-interleaved with the step's MFMAs, one 3-op phase per MFMA.
+template <int WAVES, int BNB, int MODE, bool UPS, bool SGB = false>
 __global__ void __launch_bounds__(64 * WAVES, 1) conv_halo_kernel(const GemmArgs p, const HaloGeo g) {
   using T = HcT<WAVES, BNB>;
   constexpr int BN = T::BN, WN = T::WN, HJ = T::HJ, WJ = T::WJ, BMB = T::BMB;
@@ -292,16 +294,60 @@ __global__ void __launch_bounds__(64 * WAVES, 1) conv_halo_kernel(const GemmArgs
       dma_halo(cn, (c + 1) & 1);
       dma_ss(cn, (c + 1) & 1);
     }
-    read_frags(min(t + 1, nk - 1), 0, x0, w0);
-    if constexpr (MODE != 0 && TAP == 1) load_ss((c + 1) & 1);
+    constexpr bool NORM_STEP = MODE != 0 && TAP >= 1 && TAP <= 7;
+    if constexpr (SGB && NORM_STEP) {
+      // hand-interleaved normalisation (lab variant): this step's NPT slots (16 elements each as two 3-op phases:
+      // y = fma, e = exp2(-y log2 e) | o = y / (1 + e)) one phase per MFMA, order pinned by sched_barrier; the raw
+      // slots are read BEFORE the next tile's fragments (LDS returns in order: their wait does not cover those)
+      if constexpr (TAP == 1) load_ss((c + 1) & 1);
+      const int hb = (c + 1) & 1;
+      uint4_* qs[NPT];
+      uint4_ raw[NPT];
 #pragma unroll
-    for (int i = 0; i < BMB; ++i)
+      for (int u = 0; u < NPT; ++u) {
+        const int j = min((TAP - 1) * NPT + u, HJ - 1);
+        qs[u] = reinterpret_cast<uint4_*>(halo + hb * T::HALO_ELEMS + ((wid * HJ + j) * 8) * HC_BK) + lane;
+        raw[u] = *qs[u];
+      }
+      read_frags(min(t + 1, nk - 1), 0, x0, w0);
+      float f[NPT][8], yv[NPT][8], ev[NPT][8];
+      constexpr int NSTG = 16 * NPT;
+      static_assert(NSTG <= BMB * BNB, "normalisation phases per step");
 #pragma unroll
-      for (int j = 0; j < BNB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[j], x1[i], acc[i][j], 0, 0, 0);
-    if constexpr (MODE != 0 && TAP >= 1 && TAP <= 7) {
+      for (int i = 0; i < BMB; ++i)
+#pragma unroll
+        for (int j = 0; j < BNB; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[j], x1[i], acc[i][j], 0, 0, 0);
+          const int k = i * BNB + j;
+          if (k < NSTG) {
+            const int u = k / 16, e = (k % 16) >> 1;
+            if ((k & 1) == 0) {
+              if (e == 0) unpack8(raw[u], f[u]);
+              yv[u][e] = fmaf(f[u][e], sc[e], sh[e]);
+              ev[u][e] = __builtin_amdgcn_exp2f(yv[u][e] * -1.4426950408889634f);
+            } else {
+              const int jj = (TAP - 1) * NPT + u;
+              const bool ok = jj < HJ && ((hvalid >> min(jj, HJ - 1)) & 1u);
+              f[u][e] = ok ? yv[u][e] * rcp_f(1.0f + ev[u][e]) : 0.f;
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
       for (int u = 0; u < NPT; ++u)
-        if ((TAP - 1) * NPT + u < HJ) norm_slot((c + 1) & 1, (TAP - 1) * NPT + u);
+        if ((TAP - 1) * NPT + u < HJ) *qs[u] = pack8(f[u]);
+    } else {
+      read_frags(min(t + 1, nk - 1), 0, x0, w0);
+      if constexpr (MODE != 0 && TAP == 1) load_ss((c + 1) & 1);
+#pragma unroll
+      for (int i = 0; i < BMB; ++i)
+#pragma unroll
+        for (int j = 0; j < BNB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[j], x1[i], acc[i][j], 0, 0, 0);
+      if constexpr (NORM_STEP) {
+#pragma unroll
+        for (int u = 0; u < NPT; ++u)
+          if ((TAP - 1) * NPT + u < HJ) norm_slot((c + 1) & 1, (TAP - 1) * NPT + u);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -460,15 +506,15 @@ bool conv_halo_supported(const GemmArgs& a) {
   return true;
 }
 
-template <int WAVES, int BNB, int MODE, bool UPS>
+template <int WAVES, int BNB, int MODE, bool UPS, bool SGB = false>
 static void hc_go(const GemmArgs& a, const HaloGeo& g, hipStream_t s) {
   using T = HcT<WAVES, BNB>;
-  conv_halo_kernel<WAVES, BNB, MODE, UPS><<<g.tiles_m * g.tiles_n, 64 * WAVES, T::LDS, s>>>(a, g);
+  conv_halo_kernel<WAVES, BNB, MODE, UPS, SGB><<<g.tiles_m * g.tiles_n, 64 * WAVES, T::LDS, s>>>(a, g);
 }
 
-template <int WAVES, int BNB>
+template <int WAVES, int BNB, bool SGB = false>
 static void hc_mode(const GemmArgs& a, const HaloGeo& g, hipStream_t s) {
-  if (a.in_scale) hc_go<WAVES, BNB, 2, false>(a, g, s);
+  if (a.in_scale) hc_go<WAVES, BNB, 2, false, SGB>(a, g, s);
   else if (a.upsample) hc_go<WAVES, BNB, 0, true>(a, g, s);
   else hc_go<WAVES, BNB, 0, false>(a, g, s);
 }
@@ -495,6 +541,9 @@ void launch_conv_halo(const GemmArgs& a, hipStream_t s, int waves) {
   if (waves == 4) {
     if (bn == 160) hc_mode<4, 10>(a, g, s);
     else hc_mode<4, 8>(a, g, s);
+  } else if (waves == 9) {  // lab: 8 waves with the normalisation hand-interleaved between the MFMAs
+    if (bn == 160) hc_mode<8, 5, true>(a, g, s);
+    else hc_mode<8, 4, true>(a, g, s);
   } else {
     if (bn == 160) hc_mode<8, 5>(a, g, s);
     else hc_mode<8, 4>(a, g, s);

@@ -83,6 +83,8 @@ def main():
             res.setdefault("halo8", []).append(timeit(fused))
             ops.set_halo_conv(1, 4)
             res.setdefault("halo4", []).append(timeit(fused))
+            ops.set_halo_conv(1, 9)
+            res.setdefault("halo8sgb", []).append(timeit(fused))
             ops.set_halo_conv(0, 0)
             res.setdefault("apply+conv", []).append(timeit(fused))
             res.setdefault("conv", []).append(timeit(bare))
