@@ -536,10 +536,29 @@ void launch_flash64(const AttnArgs& a, hipStream_t s) {
   else flash64_kernel<false><<<grid, 256, lds, s>>>(a);
 }
 
+// D = 128 routing: 1 = flash128x2 (default), 0 = flash2 (SHAI_FLASH128X2=0, or set_flash128x2 at run time for A/B)
+static int g_f128x2 = -1;
+int flash128x2_mode() {
+  if (g_f128x2 < 0) {
+    const char* e = getenv("SHAI_FLASH128X2");
+    g_f128x2 = (e == nullptr || atoi(e) != 0) ? 1 : 0;
+  }
+  return g_f128x2;
+}
+int set_flash128x2(int mode) {
+  const int prev = flash128x2_mode();
+  if (mode >= 0) g_f128x2 = mode;
+  return prev;
+}
+
 void launch_flash_attn(const AttnArgs& a, hipStream_t s) {
   static const bool v1_only = getenv("SHAI_FLASH_V1") != nullptr;  // A/B and tests: pin the v1 kernel
   if (!v1_only && flash64_supported(a)) {  // D = 64 (every SD2.1 / ViT / BERT attention)
     launch_flash64(a, s);
+    return;
+  }
+  if (!v1_only && flash128x2_mode() && flash128x2_supported(a) && a.Sq >= 512 && a.Skv >= 512) {
+    launch_flash128x2(a, s);
     return;
   }
   if (!v1_only && flash2_supported(a)) {  // 8-wave ping-pong kernel (attention2.hip)

@@ -500,6 +500,281 @@ void launch_flash64_x2(const AttnArgs& a, hipStream_t s) {
   else flash64x2_kernel<false><<<grid, 256, lds, s>>>(a);
 }
 
+// flash128x2: flash64x2's structure at D = 128 (Flux joint attention: 24 heads x 128 over 1056-4608 tokens; Llama /
+// Mistral prefill) -- the round-5 verdict's ask for the 8-wave ping-pong flash2<128> (40 % MFMA busy).  Four waves of
+// two 32-query groups each (256 queries per workgroup, ONE workgroup per CU: ~400 registers per lane).  Per 64-key
+// tile every K fragment (16 ds_read_b128) and every V^T fragment (32 transposed reads) is read ONCE and feeds both
+// groups' MFMAs; group B's score MFMAs and A's P.V MFMAs sit in the same basic block as the other group's branch-free
+// exponentials (one wave per SIMD interleaves its own MFMA and VALU streams).  Per tile and wave: 2 x (2 x 9 + 16) =
+// 68 32x32x16 MFMAs (~2.2k matrix cycles) vs ~0.9k cycles of softmax VALU.  K / V tiles (16 KB each) by LDS-DMA into a
+// 3-slot ring, two tiles ahead (vmcnt counted: tile t + 2's 8 DMAs per wave stay in flight), source-side XOR
+// swizzles as flash2<128> (K: chunk ^ (row & 15); V: chunk ^ ((row & 3) << 2)).
+__device__ __forceinline__ int f4_kswz(int row, int ch) { return row * 128 + ((ch ^ (row & 15)) << 3); }
+__device__ __forceinline__ int f4_vswz(int row, int ch) { return row * 128 + ((ch ^ ((row & 3) << 2)) << 3); }
+__device__ __forceinline__ void f4_glds(__amdgpu_buffer_rsrc_t r, bf16_t* lds, uint32_t off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (f3_lds_void*)lds, 16, off, 0, 0, 0);
+}
+
+template <bool CAUSAL>
+__global__ void __launch_bounds__(256, 1) flash128x2_kernel(const AttnArgs p) {
+  constexpr int D = 128, KT = 64, NS = 8, ND = 4, G = 2, NSLOT = 3;
+  constexpr int TILE = 2 * KT * D;   // ring slot: K tile then V tile (elements)
+  constexpr float kSumThr = 256.f;
+  constexpr float kL2e = 1.4426950408889634f;
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 31, fh = lane >> 5;
+  const int b = blockIdx.z, hq = blockIdx.y;
+  const int hk = hq / (p.Hq / p.Hkv);
+  const int q_len = p.q_lens ? p.q_lens[b] : p.Sq;
+  const int kv_len = p.kv_lens ? p.kv_lens[b] : p.Skv;
+  const int c_off = p.q_lens ? kv_len - q_len : p.causal_offset;
+  if ((int)blockIdx.x * 256 >= q_len) return;
+  const int q0 = blockIdx.x * 256;
+  int qi[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) qi[g] = q0 + wid * 64 + 32 * g + fr;
+  const float sl2 = p.scale * kL2e;
+
+  const bf16_t* kbase = p.k + (long)b * p.k_bs + (long)hk * D;
+  const bf16_t* vbase = p.v + (long)b * p.v_bs + (long)hk * D;
+  // descriptors sized to the valid keys: rows past kv_len read as zeros (never NaN garbage into P.V)
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(kbase), (short)0, (int)min((long)kv_len * p.k_ts * 2, 0x7fffffffL), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(vbase), (short)0, (int)min((long)kv_len * p.v_ts * 2, 0x7fffffffL), 0x00020000);
+  int kv_end = kv_len;
+  if (CAUSAL) kv_end = min(kv_end, q0 + 255 + c_off + 1);
+  const int ntiles = kv_end > 0 ? (kv_end + KT - 1) / KT : 0;
+  // DMA: wave wid stages K rows 16 wid + 4 j + (lane >> 4) and the same V rows (j < 4), 16 B chunk lane & 15
+  const int drow = wid * 16 + (lane >> 4), dch = lane & 15;
+  uint32_t koffs[4], voffs[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = drow + 4 * j;
+    koffs[j] = (uint32_t)(((long)row * p.k_ts + ((dch ^ (row & 15)) * 8)) * 2);
+    voffs[j] = (uint32_t)(((long)row * p.v_ts + ((dch ^ ((row & 3) << 2)) * 8)) * 2);
+  }
+  auto dma = [&](int slot, int t) {
+    bf16_t* ks = smem + slot * TILE;
+    bf16_t* vs = ks + KT * D;
+    const uint32_t tk = (uint32_t)((long)t * KT * p.k_ts * 2), tv = (uint32_t)((long)t * KT * p.v_ts * 2);
+    SHAI_DASSERT(slot >= 0 && slot < NSLOT);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f4_glds(rk, ks + (wid * 16 + 4 * j) * D, koffs[j] + tk);
+      f4_glds(rv, vs + (wid * 16 + 4 * j) * D, voffs[j] + tv);
+    }
+  };
+  // tiles 0 and 1 in flight (over-issued past the end: zero fill, never read)
+  dma(0, 0);
+  dma(1, 1);
+
+  f3bf16x8 qf[G][NS];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const bf16_t* qp = p.q + (p.q_start ? (long)p.q_start[b] * p.q_ts : (long)b * p.q_bs) +
+                        (long)min(qi[g], q_len - 1) * p.q_ts + (long)hq * D;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      uint4_ v = *reinterpret_cast<const uint4_*>(qp + 16 * s + 8 * fh);
+      if (qi[g] >= q_len) v = uint4_{0u, 0u, 0u, 0u};
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= sl2;
+      qf[g][s] = __builtin_bit_cast(f3bf16x8, pack8(f));
+    }
+  }
+
+  float16_ o[G][ND];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[g][d][r] = 0.f;
+  float m_run[G], l_run[G];
+  f3bf16x8 b_negm[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    m_run[g] = -INFINITY;
+    l_run[g] = 0.f;
+    b_negm[g] = __builtin_bit_cast(f3bf16x8, uint4_{0u, 0u, 0u, 0u});
+  }
+  const f3bf16x8 a_one = __builtin_bit_cast(f3bf16x8, uint4_{lane < 32 ? 0x3F80u : 0u, 0u, 0u, 0u});
+
+  const int g16 = lane >> 4, i16 = lane & 15;
+  const int tq = i16 >> 2, tp = i16 & 3;
+  int koff[NS], voff[ND];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) koff[s] = f4_kswz(fr, 2 * s + fh);
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    const int col = d * 32 + 16 * (g16 & 1) + 4 * tp;
+    voff[d] = f4_vswz(4 * fh + tq, col >> 3) + 4 * ((col >> 2) & 1);
+  }
+
+  float16_ sacc[G][2];
+  f3bf16x8 pf[G][2][2];
+  auto expo = [&](int g, float add, auto addt) {
+    constexpr bool ADD = decltype(addt)::value;
+    float ls4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          e[j] = __builtin_amdgcn_exp2f(ADD ? sacc[g][kb][8 * s + j] + add : sacc[g][kb][8 * s + j]);
+        f3bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ls4[j & 3] += e[j];
+          v[j] = (__bf16)e[j];
+        }
+        pf[g][kb][s] = v;
+      }
+    return (ls4[0] + ls4[1]) + (ls4[2] + ls4[3]);
+  };
+  // slow path of group g (masking, lazy-max rescale) after the branch-free fast path, as flash64x2
+  auto check = [&](int g, int key0, float ls_fast) {
+    const bool mask = (key0 + KT > kv_len) || (CAUSAL && key0 + KT - 1 > q0 + wid * 64 + 32 * g + c_off);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) asm volatile("" ::"v"(pf[g][kb][s2]));
+    asm volatile("" ::"v"(ls_fast));
+    const uint64_t slow_lanes = __ballot(m_run[g] == -INFINITY) | __ballot(!(ls_fast <= kSumThr));
+    float ls = ls_fast;
+    if (mask | (slow_lanes != 0)) {
+      if (mask) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = key0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+            const bool bad = key >= kv_len || (CAUSAL && key > qi[g] + c_off);
+            sacc[g][kb][r] = bad ? -INFINITY : sacc[g][kb][r];
+          }
+      }
+      float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) m4[r & 3] = fmaxf(m4[r & 3], sacc[g][kb][r]);
+      const float mb = m_run[g] == -INFINITY ? 0.f : m_run[g];
+      float mloc = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64)) + mb;
+      uint32_t u = __float_as_uint(fmaxf(m_run[g], mloc));
+      if ((u & 0xffffu) != 0u && u != 0xff800000u) u = (u & 0x80000000u) ? (u & 0xffff0000u) : ((u + 0x10000u) & 0xffff0000u);
+      const float m_new = __uint_as_float(u);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = __builtin_amdgcn_exp2f(m_run[g] - m_use);
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[g][d][r] *= alpha;
+      l_run[g] *= alpha;
+      const float shift = mb - m_use;
+      m_run[g] = m_new;
+      const uint32_t nb = __float_as_uint(-(m_run[g] == -INFINITY ? 0.f : m_run[g])) >> 16;
+      b_negm[g] = __builtin_bit_cast(f3bf16x8, uint4_{lane < 32 ? nb : 0u, 0u, 0u, 0u});
+      ls = expo(g, shift, std::true_type{});
+    }
+    l_run[g] += ls;
+  };
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t % NSLOT;
+    // tile t landed (this wave's 8 DMAs of tile t + 1 stay in flight), every wave past its reads of slot (t + 2) % 3
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    dma((t + 2) % NSLOT, t + 2);
+    const bf16_t* ks = smem + cur * TILE;
+    const bf16_t* vs = ks + KT * D;
+    const int key0 = t * KT;
+    // scores of both groups: every K fragment read once
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const float16_ z = {};
+#pragma unroll
+      for (int g = 0; g < G; ++g) sacc[g][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_one, b_negm[g], z, 0, 0, 0);
+#pragma unroll
+      for (int s2 = 0; s2 < NS; ++s2) {
+        const f3bf16x8 kf = *reinterpret_cast<const f3bf16x8*>(ks + koff[s2] + kb * 32 * D);
+#pragma unroll
+        for (int g = 0; g < G; ++g) sacc[g][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[g][s2], sacc[g][kb], 0, 0, 0);
+      }
+    }
+    const float ls0 = expo(0, 0.f, std::false_type{});
+    check(0, key0, ls0);
+    // P.V of group A beside group B's exponentials; each V^T fragment read once for both groups
+    f3bf16x8 vf[ND][2][2];
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16_t* a0 = vs + voff[d] + kb * 32 * D + s2 * 16 * D;
+          const f3s4v t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) f3s4v*)(a0));
+          const f3s4v t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) f3s4v*)(a0 + 8 * D));
+          vf[d][kb][s2] = __builtin_bit_cast(f3bf16x8, __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7));
+          o[0][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[d][kb][s2], pf[0][kb][s2], o[0][d], 0, 0, 0);
+        }
+    const float ls1 = expo(1, 0.f, std::false_type{});
+    check(1, key0, ls1);
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          o[1][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[d][kb][s2], pf[1][kb][s2], o[1][d], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the over-issued tail DMAs land before the workgroup exits
+
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const float l_tot = l_run[g] + __shfl_xor(l_run[g], 32, 64);
+    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+    if (qi[g] < q_len) {
+      bf16_t* op = p.o + (p.q_start ? (long)p.q_start[b] * p.o_ts : (long)b * p.o_bs) + (long)qi[g] * p.o_ts +
+                   (long)hq * D;
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          const int dd = d * 32 + 8 * gg + 4 * fh;
+          uint2_ w;
+          w[0] = pack2(o[g][d][4 * gg] * inv, o[g][d][4 * gg + 1] * inv);
+          w[1] = pack2(o[g][d][4 * gg + 2] * inv, o[g][d][4 * gg + 3] * inv);
+          *reinterpret_cast<uint2_*>(op + dd) = w;
+        }
+    }
+  }
+}
+
+// D = 128, no additive bias / paged K/V, 16-B aligned rows; causal (+ offset), per-batch q / kv lengths, packed
+// varlen q / o and GQA as flash2
+bool flash128x2_supported(const AttnArgs& a) {
+  return a.D == 128 && a.bias == nullptr && a.block_table == nullptr && ((a.k_ts | a.v_ts | a.q_ts) & 7) == 0 &&
+         (long)a.Skv * a.k_ts * 2 < 0x7fffffffL && (long)a.Skv * a.v_ts * 2 < 0x7fffffffL;
+}
+
+void launch_flash128x2(const AttnArgs& a, hipStream_t s) {
+  dim3 grid((a.Sq + 255) / 256, a.Hq, a.B);
+  const size_t lds = (size_t)3 * 2 * 64 * 128 * sizeof(bf16_t);   // 96 KB: 3 ring slots of K + V
+  if (a.causal) flash128x2_kernel<true><<<grid, 256, lds, s>>>(a);
+  else flash128x2_kernel<false><<<grid, 256, lds, s>>>(a);
+}
+
 // Same contract as flash64 (attention.hip): D = 64, causal (+ offset), per-batch q / kv lengths, packed varlen
 // q / o, GQA; K / V rows addressed through 32-bit buffer offsets.
 bool flash64_dma_supported(const AttnArgs& a) {

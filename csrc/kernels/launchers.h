@@ -249,6 +249,12 @@ void launch_flash64_dma(const AttnArgs& a, hipStream_t s);
 // the same pipeline with two 32-query groups per wave (256 queries per workgroup, flash64_dma_supported contract;
 // launch_flash64 picks it for grids of >= 1024 such workgroups)
 void launch_flash64_x2(const AttnArgs& a, hipStream_t s);
+// D = 128 with two 32-query groups per wave (attention3.hip; 256 queries per workgroup, one workgroup per CU): Flux
+// joint attention / LLM prefill; launch_flash_attn picks it over flash2 for D = 128 (SHAI_FLASH128X2=0 opts out)
+bool flash128x2_supported(const AttnArgs& a);
+void launch_flash128x2(const AttnArgs& a, hipStream_t s);
+int flash128x2_mode();
+int set_flash128x2(int mode);   // -1 keeps the mode; returns the previous one
 // D = 512 single-head fused attention (attention3.hip; the VAE mid-block)
 bool attn512_supported(const AttnArgs& a);
 void launch_attn512(const AttnArgs& a, hipStream_t s);

@@ -516,3 +516,31 @@ def test_gemm2_splitk_fixup(cuda, cfg, splits, M, N, K, glu):
     ops.gemm_into(x, w, out2, b, act=act, residual=r, glu=glu, force_cfg=force)
     close(out1, ref.linear(x, w, b, act, r, glu), 2e-2)
     assert torch.equal(out1, out2)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+def test_flash128_x2_spikes_varlen_gqa(cuda, causal):
+    """D = 128 two-group kernel (flash128x2, attention3.hip; the default for D = 128 at Sq, Skv >= 512): spikes in the
+    first tile and past the fast-path bound, a moderate max growth, per-batch lengths with partial query / key tiles,
+    GQA 4:1 -- against the fp32 reference, and against the flash2 kernel it replaced."""
+    torch.manual_seed(18)
+    B, S, Hq, Hkv, D = 3, 1100, 8, 2, 128
+    q, k, v = rnd(B, S, Hq, D), rnd(B, S, Hkv, D), rnd(B, S, Hkv, D)
+    k[:, 3] = q[:, 700, :Hkv] * 3
+    k[:, 900] = q[:, 10, :Hkv] * 5
+    k[:, 513] = q[:, 600, :Hkv] * 0.7
+    kl = torch.tensor([1100, 1030, 513], device="cuda", dtype=torch.int32)
+    ql = kl.clone() if causal else None
+    K = ops._K()
+    prev = K.set_flash128x2(1)
+    try:
+        o = ops.attention(q, k, v, causal=causal, kv_lens=kl, q_lens=ql)
+        K.set_flash128x2(0)
+        o2 = ops.attention(q, k, v, causal=causal, kv_lens=kl, q_lens=ql)
+    finally:
+        K.set_flash128x2(prev)
+    orf = ref.attention(q, k, v, 1 / math.sqrt(D), causal, 0, kl, ql)
+    for b in range(B):
+        n = int((ql if ql is not None else torch.full_like(kl, S))[b])
+        close(o[b, :n], orf[b, :n], 2e-2)
+        close(o[b, :n], o2[b, :n], 2e-2)
