@@ -536,12 +536,15 @@ void launch_flash64(const AttnArgs& a, hipStream_t s) {
   else flash64_kernel<false><<<grid, 256, lds, s>>>(a);
 }
 
-// D = 128 routing: 1 = flash128x2 (default), 0 = flash2 (SHAI_FLASH128X2=0, or set_flash128x2 at run time for A/B)
+// D = 128 routing: 0 = flash2 (default), 1 = flash128x2 (SHAI_FLASH128X2=1, or set_flash128x2 at run time for A/B).
+// flash2 stays the default: the two-group kernel measured 11-15 % slower at the Flux / prefill shapes
+// (profiles/flash128x2_ab_round6.json: Flux 1024^2 312 vs 278 us) -- at ~400 registers per lane one wave per SIMD
+// cannot hide its own softmax behind its MFMAs the way the 8-wave ping-pong's partner wave does.
 static int g_f128x2 = -1;
 int flash128x2_mode() {
   if (g_f128x2 < 0) {
     const char* e = getenv("SHAI_FLASH128X2");
-    g_f128x2 = (e == nullptr || atoi(e) != 0) ? 1 : 0;
+    g_f128x2 = (e != nullptr && atoi(e) != 0) ? 1 : 0;
   }
   return g_f128x2;
 }

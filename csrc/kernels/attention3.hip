@@ -509,6 +509,9 @@ void launch_flash64_x2(const AttnArgs& a, hipStream_t s) {
 // 68 32x32x16 MFMAs (~2.2k matrix cycles) vs ~0.9k cycles of softmax VALU.  K / V tiles (16 KB each) by LDS-DMA into a
 // 3-slot ring, two tiles ahead (vmcnt counted: tile t + 2's 8 DMAs per wave stay in flight), source-side XOR
 // swizzles as flash2<128> (K: chunk ^ (row & 15); V: chunk ^ ((row & 3) << 2)).
+// Measured (round 6, tools/bench_attn128.py): 11-15 % SLOWER than flash2<128> (Flux 1024^2 312 vs 278 us): the
+// kernel needs ~400 registers (256 VGPR + 144 AGPR, accumulators shuffled between the files) and one wave per SIMD
+// does not hide its own softmax; kept opt-in (SHAI_FLASH128X2=1) with its tests.
 __device__ __forceinline__ int f4_kswz(int row, int ch) { return row * 128 + ((ch ^ (row & 15)) << 3); }
 __device__ __forceinline__ int f4_vswz(int row, int ch) { return row * 128 + ((ch ^ ((row & 3) << 2)) << 3); }
 __device__ __forceinline__ void f4_glds(__amdgpu_buffer_rsrc_t r, bf16_t* lds, uint32_t off) {

@@ -250,7 +250,7 @@ void launch_flash64_dma(const AttnArgs& a, hipStream_t s);
 // launch_flash64 picks it for grids of >= 1024 such workgroups)
 void launch_flash64_x2(const AttnArgs& a, hipStream_t s);
 // D = 128 with two 32-query groups per wave (attention3.hip; 256 queries per workgroup, one workgroup per CU): Flux
-// joint attention / LLM prefill; launch_flash_attn picks it over flash2 for D = 128 (SHAI_FLASH128X2=0 opts out)
+// joint attention / LLM prefill; opt-in over flash2 for D = 128 (SHAI_FLASH128X2=1 / set_flash128x2: measured slower)
 bool flash128x2_supported(const AttnArgs& a);
 void launch_flash128x2(const AttnArgs& a, hipStream_t s);
 int flash128x2_mode();

@@ -520,7 +520,7 @@ def test_gemm2_splitk_fixup(cuda, cfg, splits, M, N, K, glu):
 
 @pytest.mark.parametrize("causal", [False, True])
 def test_flash128_x2_spikes_varlen_gqa(cuda, causal):
-    """D = 128 two-group kernel (flash128x2, attention3.hip; the default for D = 128 at Sq, Skv >= 512): spikes in the
+    """D = 128 two-group kernel (flash128x2, attention3.hip; opt-in for D = 128 at Sq, Skv >= 512): spikes in the
     first tile and past the fast-path bound, a moderate max growth, per-batch lengths with partial query / key tiles,
     GQA 4:1 -- against the fp32 reference, and against the flash2 kernel it replaced."""
     torch.manual_seed(18)
