@@ -299,12 +299,16 @@ class FluxSingleTransformerBlock(nn.Module):
         D = c.head_dim
         HD = Hl * D
         xn = ops.layernorm_mod(x, mod[:, d:2 * d], mod[:, :d], s_loc)
-        if sp:
-            xn = comm.all_gather_seq(xn)
-        S = xn.shape[1]
-        qkv = ops.linear(xn, self.attn.qkv.weight, self.attn.qkv.bias)          # [B, S, 3HD]
+        S = s_loc * tp().size if sp else s_loc
+        qkv = torch.empty(B, S, 3 * HD, dtype=x.dtype, device=x.device)
         cat = torch.empty(B, S, HD + self.proj_mlp.out_local, dtype=x.dtype, device=x.device)
-        ops.gemm_into(xn, self.proj_mlp.weight, cat[..., HD:], self.proj_mlp.bias, act="gelu_tanh")
+        specs = [(self.attn.qkv.weight, self.attn.qkv.bias, None, qkv),
+                 (self.proj_mlp.weight, self.proj_mlp.bias, "gelu_tanh", cat[..., HD:])]
+        if sp:   # the sequence all-gather forked beside this rank's own rows' GEMMs (comm.gather_seq_linears)
+            comm.gather_seq_linears(xn, specs)
+        else:
+            for w, b, act, out in specs:
+                ops.gemm_into(xn, w, out, b, act=act)
         ops.qk_norm_rope(qkv.view(B * S, 3 * HD), self.attn.norm_q, self.attn.norm_k, cos, sin, Hl, D, S)
         ops.attention(qkv[..., :HD].view(B, S, Hl, D), qkv[..., HD:2 * HD].view(B, S, Hl, D),
                       qkv[..., 2 * HD:].view(B, S, Hl, D), out=cat[..., :HD].view(B, S, Hl, D))

@@ -288,6 +288,46 @@ def all_gather_seq(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -
     return flat.view((n,) + tuple(x.shape)).transpose(0, 1).reshape((B, n * s) + tuple(x.shape[2:]))
 
 
+SP_GATHER_OVERLAP = os.environ.get("SHAI_SP_GATHER_OVERLAP", "1") != "0"
+
+
+def gather_seq_linears(x: torch.Tensor, specs, group: Optional[dist.ProcessGroup] = None) -> None:
+    """Sequence-parallel all-gather fused with the column-parallel GEMMs that consume it (fork / join):
+    ``out = act(gather_seq(x) @ w^T + b)`` for every ``(w, b, act, out)`` in ``specs``, ``out`` a [B, n*s, N] view.
+
+    The all-gather is issued asynchronously (RCCL runs it on its own stream; gloo on its worker thread) and this
+    rank's own s rows -- already local -- go through every GEMM while the other ranks' rows are in flight; after
+    the join, the rows of the ranks before and after this one run as one batched GEMM each per image ([r, s, d]
+    views of the rank-major gather buffer, no re-layout copy).  On xGMI's full mesh the gather is one direct
+    exchange with every peer, so the own-rows GEMMs are what it can hide behind.  Reference: the Flux single
+    blocks' column-parallel QKV / MLP after the sequence gather (app/src/transformer/model.py:303-322);
+    SHAI_SP_GATHER_OVERLAP=0 gathers first (A/B)."""
+    from .. import ops
+    st = tp()
+    g = group if group is not None else st.group
+    n = st.size if group is None else (dist.get_world_size(g) if dist.is_initialized() else 1)
+    if n == 1 or not SP_GATHER_OVERLAP:
+        xg = all_gather_seq(x, group) if n > 1 else x
+        for w, b, act, out in specs:
+            ops.gemm_into(xg, w, out, b, act=act)
+        return
+    r = dist.get_rank(g)
+    x = x.contiguous()
+    B, s = x.shape[0], x.shape[1]
+    flat = torch.empty((n * B,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    work = dist.all_gather_into_tensor(flat, x, group=g, async_op=True)   # rank-major along dim 0
+    for w, b, act, out in specs:                                           # own rows beside the exchange
+        ops.gemm_into(x, w, out[:, r * s:(r + 1) * s], b, act=act)
+    work.wait()
+    fv = flat.view((n, B) + tuple(x.shape[1:]))
+    for w, b, act, out in specs:
+        N = out.shape[-1]
+        for bi in range(B):
+            for j0, j1 in ((0, r), (r + 1, n)):
+                if j1 > j0:
+                    ops.gemm_into(fv[j0:j1, bi], w, out[bi, j0 * s:j1 * s].view(j1 - j0, s, N), b, act=act)
+
+
 def reduce_scatter_seq(x: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
     """Sequence-parallel reduce-scatter: partial sums [B, S, ...] -> this rank's reduced rows [B, S/n, ...].
     Replaces the all-reduce after a RowParallel layer (same bytes on the wire as the all-gather that feeds

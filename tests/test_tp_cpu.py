@@ -15,7 +15,7 @@ def _port():
 
 
 @pytest.mark.parametrize("which", ["llama", "t5", "flux", "flux_sp", "flux_ovl", "row_overlap", "row_gated_slabs",
-                                   "seq_comm", "mllama_vision"])
+                                   "seq_comm", "seq_gather_linears", "mllama_vision"])
 def test_tp2_matches_tp1(which):
     mp.spawn(tp_worker.run, args=(2, _port(), which), nprocs=2, join=True)
 
@@ -29,6 +29,12 @@ def test_tp_degrees_4_8_match_tp1(which, world):
     AND 10 teacher-forced decode steps, T5 with 1 head per rank at TP8, Flux with 24 heads (3 per rank at
     TP8) with and without sequence parallelism."""
     mp.spawn(tp_worker.run, args=(world, _port(), which), nprocs=world, join=True)
+
+
+def test_sp_gather_linears_middle_ranks():
+    """World 4: ranks 1 and 2 have rows both before and after their own (two batched GEMMs per image after the
+    join), ranks 0 / 3 only one side."""
+    mp.spawn(tp_worker.run, args=(4, _port(), "seq_gather_linears"), nprocs=4, join=True)
 
 
 def test_seq_major_layout_is_rank_chunks():

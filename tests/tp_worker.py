@@ -187,6 +187,38 @@ def run(rank, world, port, which):
         assert torch.equal(got, want)
         rs = comm.reduce_scatter_seq(full[rank].clone())
         assert torch.allclose(rs, sum(full)[:, rank * s:(rank + 1) * s], atol=1e-5)
+    elif which == "seq_gather_linears":
+        # the SP all-gather forked beside the own rows' GEMMs (comm.gather_seq_linears): every rank's output equals
+        # the dense GEMMs over the gathered sequence, at B = 1 and 2, into a strided column slice (the Flux single
+        # blocks' [attn | mlp] buffer), and the GEMM schedule is own rows first, then the rows before / after
+        from shai_amd import ops
+        from shai_amd.parallel import comm
+        init_distributed("gloo", tp_size=world)
+        g = torch.Generator().manual_seed(11)
+        d, s, N1, N2 = 32, 5, 24, 40
+        w1, b1 = torch.randn(N1, d, generator=g), torch.randn(N1, generator=g)
+        w2, b2 = torch.randn(N2, d, generator=g), torch.randn(N2, generator=g)
+        for B in (1, 2):
+            full = torch.randn(B, world * s, d, generator=g)
+            out1 = torch.full((B, world * s, N1), float("nan"))
+            cat = torch.full((B, world * s, 8 + N2), float("nan"))
+            calls = []
+            orig = ops.gemm_into
+
+            def spy(x, w, out, *a, **k):
+                calls.append(tuple(x.shape))
+                return orig(x, w, out, *a, **k)
+            ops.gemm_into = spy
+            try:
+                comm.gather_seq_linears(full[:, rank * s:(rank + 1) * s],
+                                        [(w1, b1, None, out1), (w2, b2, "gelu_tanh", cat[..., 8:])])
+            finally:
+                ops.gemm_into = orig
+            _close(out1, full @ w1.t() + b1, 1e-5)
+            _close(cat[..., 8:], torch.nn.functional.gelu(full @ w2.t() + b2, approximate="tanh"), 1e-5)
+            assert torch.isnan(cat[..., :8]).all()   # the columns left of the slice are untouched
+            others = sum(j1 > j0 for j0, j1 in ((0, rank), (rank + 1, world)))
+            assert calls[:2] == [(B, s, d)] * 2 and len(calls) == 2 * (1 + B * others), calls
     import torch.distributed as dist
     dist.barrier()
     dist.destroy_process_group()
