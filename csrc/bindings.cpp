@@ -1674,6 +1674,7 @@ TORCH_LIBRARY(shai, m) {
   m.def("gemm_tuning_import(str[] entries) -> int", &gemm_tuning_import);
   m.def("set_halo_conv(int mode, int waves=-1) -> int", &set_halo_conv);
   m.def("set_flash128x2(int mode) -> int", [](int64_t mode) -> int64_t { return shai::set_flash128x2((int)mode); });
+  m.def("set_decode_wb(int mode) -> int", [](int64_t mode) -> int64_t { return shai::set_decode_wb((int)mode); });
 }
 
 TORCH_LIBRARY_IMPL(shai, CUDA, m) {

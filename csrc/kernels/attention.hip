@@ -920,12 +920,329 @@ __global__ void decode_combine_kernel(const DecodeAttnArgs p) {
   }
 }
 
+// ----------------------------------------------------------------------------
+// Short-context decode attention, "wave per block" (D = 128, GQA group G = 4, one split).
+// The split kernel above walks a (sequence, KV head)'s 64-token blocks one after another with ONE block in flight
+// (two-slot ring), so at decode-batch contexts of a few hundred tokens its launch is mostly prologue and per-block
+// HBM latency (B 64 x ctx 192: 18 us for 50 MB, 2.8 TB/s; gpurun_out/r6f_decode.log).  Here the G waves of the
+// (sequence, KV head) workgroup each take their OWN blocks w, w + G, ... for ALL G query heads of the group (GQA:
+// each K / V block is read once for the four heads), so the workgroup has G blocks (128 KB) in flight from its
+// first instructions:
+//  * K block by LDS-DMA into the wave's own 16 KB slot (source-side XOR swizzle: conflict-free lane = key reads);
+//    V block straight into registers, 16 x buffer_load_dwordx4 (lane holds the 8-d chunk lane & 15 of the keys
+//    (lane >> 4) + 4 j); both range-checked by the buffer descriptor (zero fill past the context);
+//  * QK^T: lane = key, packed bf16 dot products against the G q rows (LDS broadcast reads);
+//  * online softmax per head over the wave's blocks; P (bf16, the denominator sums the rounded values) through a
+//    128-B LDS row per head, stored in the (key group, j) order the P.V step reads; P.V: v_perm key pairs + packed
+//    bf16 dot products, 8 d per lane; the next block's K DMA is issued as soon as QK^T has read the slot, its V
+//    loads as soon as P.V has consumed the registers;
+//  * merge: the G waves' (m, l, o) partials meet in LDS (aliasing the K slots) and wave h combines head h with this
+//    step's new token (roped k / v from the QKV rows or the QKV GEMM's split-K partials, attended from registers,
+//    written to the cache by wave 0) -- the split kernel's prologue / new-token semantics, bit for bit in q, k, v.
+// No wave waits for another before the merge: a wave's K slot and P rows are its own (its vmcnt / lgkmcnt cover
+// them).  SHAI_DECODE_WB=0 / set_decode_wb(0) routes these launches back to the split kernel (A/B).
+constexpr int kWbG = 4;
+constexpr size_t kWbLds = (size_t)kWbG * 64 * 128 * 2 + (size_t)kWbG * 128 * 2 + (size_t)kWbG * kWbG * 64 * 2;
+
+__global__ void __launch_bounds__(kWbG * 64, 2) decode_attn_wb_kernel(const DecodeAttnArgs p) {
+  constexpr int G = kWbG, D = 128, CPR = D / 8;
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  bf16_t* sK = reinterpret_cast<bf16_t*>(dsm);   // [G waves][64 keys][D], swizzled
+  bf16_t* sQb = sK + G * 64 * D;                 // [G heads][D]
+  bf16_t* sPb = sQb + G * D;                     // [G waves][G heads][4 key groups][16]
+  float* sM = reinterpret_cast<float*>(dsm);     // merge, aliasing the K slots: [G waves][G heads][2] (m, l)
+  float* sO = sM + G * G * 2;                    // [G waves][G heads][4 key groups][D]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.x / p.Hkv, hk = blockIdx.x - b * p.Hkv;
+  const int hq = hk * G + w;  // this wave's head in the prologue and in the merge
+  const bool fused = p.knew != nullptr;
+  const int ctx = p.ctx_lens[b] - (fused ? 1 : 0);  // tokens read from the cache
+  const int nblk = (ctx + 63) / 64;
+  const int nmine = nblk > w ? (nblk - w + G - 1) / G : 0;  // blocks w, w + G, ... of this wave
+  // physical ids of this wave's blocks, 64 per lane-distributed chunk (independent of ctx: issued beside its load)
+  const int* bt = p.block_table + (long)b * p.max_blocks;
+  int chunk0 = 0;
+  int my_phys = (w + G * lane < p.max_blocks) ? bt[w + G * lane] : 0;
+  auto phys_of = [&](int it) {
+    if (it - chunk0 >= 64) {
+      chunk0 += 64;
+      const int e = w + G * (chunk0 + lane);
+      my_phys = e < p.max_blocks ? bt[e] : 0;
+    }
+    return __builtin_amdgcn_readfirstlane(__shfl(my_phys, it - chunk0, 64));
+  };
+  const int lrow = lane >> 4, lpos = lane & 15;
+  bf16_t* slot = sK + w * 64 * D;
+  uint4_ vr[16];
+  // descriptor sized to the block's rows inside the context: rows past it read as zeros (the range check of the
+  // buffer instruction), so the offsets carry no per-lane select and fold into base + immediate / SGPR offsets
+  auto rsrc = [&](const bf16_t* cache, int phys, int bi) {
+    const int rows = min(64, ctx - bi * 64);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(cache + ((long)phys * p.Hkv + hk) * 64 * D),
+                                             (short)0, rows * D * 2, 0x00020000);
+  };
+  // K: instruction t fills rows 4t .. 4t + 3 lane-linearly; LDS position lpos of row r holds global chunk
+  // lpos ^ (r & 15), and (4t + lrow) & 15 repeats with t % 4
+  int koff[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int row = 4 * t + lrow;
+    koff[t] = (row * D + ((lpos ^ (row & (CPR - 1))) << 3)) * 2;
+  }
+  const int voff = (lrow * D + lpos * 8) * 2;  // V: row lrow + 4 j at voff + 1024 j
+  auto issue_k = [&](int bi, int phys) {
+    const __amdgpu_buffer_rsrc_t rk = rsrc(p.k_cache, phys, bi);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      SHAI_DASSERT_DMA(koff[t & 3] + (t >> 2) * 4096, 64 * D * 2, 0x80000000u);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (da_lds_void*)(slot + t * 512), 16, koff[t & 3], (t >> 2) * 4096,
+                                               0, 0);
+    }
+  };
+  auto issue_v = [&](int bi, int phys) {
+    const __amdgpu_buffer_rsrc_t rv = rsrc(p.v_cache, phys, bi);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      SHAI_DASSERT_DMA(voff + j * 1024, 64 * D * 2, 0x80000000u);
+      vr[j] = __builtin_bit_cast(
+          uint4_, __builtin_amdgcn_raw_buffer_load_b128(rv, voff + (j & 3) * 1024, (j >> 2) * 4096, 0));
+    }
+  };
+  if (nmine > 0) {
+    const int ph = phys_of(0);
+    issue_k(w, ph);
+    issue_v(w, ph);
+  }
+
+  // ---- prologue (as the split kernel): this wave's q head, roped, into sQb; the new token's k / v in registers
+  const int rpos = fused ? p.positions[b] : 0;
+  const bool new_tok = fused && p.slots[b] >= 0;
+  const bool part = p.qkv_ws != nullptr;
+  float pv[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (part) {
+    const long pslab = (long)p.B * p.qkv_n;
+    const int lq = lane & (D / 2 - 1), kcol = (p.Hq + hk) * D, vcol = (p.Hq + p.Hkv + hk) * D;
+    const int col[6] = {hq * D + lq, hq * D + lq + D / 2, kcol + lq, kcol + lq + D / 2, vcol + 2 * lane,
+                        vcol + 2 * lane + 1};
+    const float* row = p.qkv_ws + (long)b * p.qkv_n;
+    const float* ssr = p.qkv_ws + (long)p.qkv_kg * pslab + b;
+    for (int s0 = 0; s0 < p.qkv_kg; s0 += 4) {
+      float t[4][7];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int sl = min(s0 + u, p.qkv_kg - 1);
+#pragma unroll
+        for (int e = 0; e < 6; ++e) t[u][e] = row[(long)sl * pslab + col[e]];
+        t[u][6] = ssr[(long)sl * p.B];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (s0 + u < p.qkv_kg) {
+#pragma unroll
+          for (int e = 0; e < 7; ++e) pv[e] += t[u][e];
+        }
+    }
+    const float rstd = rsqrtf(pv[6] / p.qkv_k + p.qkv_eps);
+#pragma unroll
+    for (int e = 0; e < 6; ++e) pv[e] = bf2f(f2bf(pv[e] * rstd));
+  }
+  float kn0 = 0.f, kn1 = 0.f, kc0 = 0.f, ks0 = 0.f;
+  uint32_t vn_pair = 0u;
+  if (new_tok) {
+    const bf16_t* kn = p.knew + (long)b * p.new_bs + (long)hk * D;
+    const bf16_t* vn = p.vnew + (long)b * p.new_bs + (long)hk * D;
+    kn0 = part ? pv[2] : bf2f(kn[lane]);
+    kn1 = part ? pv[3] : bf2f(kn[lane + D / 2]);
+    kc0 = p.rope_cos[(long)rpos * (D / 2) + lane];
+    ks0 = p.rope_sin[(long)rpos * (D / 2) + lane];
+    vn_pair = part ? pack2(pv[4], pv[5]) : *reinterpret_cast<const uint32_t*>(vn + 2 * lane);
+  }
+  if (fused) {  // NeoX RoPE on q (f32 math, bf16 result), lane = rotation pair (D / 2 = 64)
+    const bf16_t* qs = p.q + (long)b * p.q_bs + (long)hq * D;
+    const float x0 = part ? pv[0] : bf2f(qs[lane]);
+    const float x1 = part ? pv[1] : bf2f(qs[lane + D / 2]);
+    const float c = p.rope_cos[(long)rpos * (D / 2) + lane], sn = p.rope_sin[(long)rpos * (D / 2) + lane];
+    sQb[w * D + lane] = f2bf(x0 * c - x1 * sn);
+    sQb[w * D + lane + D / 2] = f2bf(x1 * c + x0 * sn);
+  } else {
+    const bf16_t* qs = p.q + (long)b * p.q_bs + (long)hq * D;
+    *reinterpret_cast<uint32_t*>(sQb + w * D + 2 * lane) = *reinterpret_cast<const uint32_t*>(qs + 2 * lane);
+  }
+  // every wave reads all G q rows: raw barrier (a __syncthreads fence would drain the K / V loads in flight)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  const float sl2 = p.scale * kLog2e;
+  float m_run[G], l_run[G], o[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    m_run[h] = -INFINITY;
+    l_run[h] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[h][i] = 0.f;
+  }
+  bf16_t* sPw = sPb + w * G * 64;
+  for (int it = 0; it < nmine; ++it) {
+    const int bi = w + G * it;
+    // this block's K slot has landed (its V loads, issued behind it, may still be in flight)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    // ---- S = q K^T for the G heads, lane = key
+    float a0[G], a1[G];
+#pragma unroll
+    for (int h = 0; h < G; ++h) a0[h] = a1[h] = 0.f;
+#pragma unroll 2
+    for (int ch = 0; ch < CPR; ++ch) {
+      const bf16x8d kv =
+          __builtin_bit_cast(bf16x8d, *reinterpret_cast<const uint4_*>(slot + lane * D + ((ch ^ (lane & (CPR - 1))) << 3)));
+#pragma unroll
+      for (int h = 0; h < G; ++h) {
+        const bf16x8d qv = __builtin_bit_cast(bf16x8d, *reinterpret_cast<const uint4_*>(sQb + h * D + ch * 8));
+        a0[h] = __builtin_amdgcn_fdot2_f32_bf16(DA_PAIR(kv, 0), DA_PAIR(qv, 0), a0[h], false);
+        a1[h] = __builtin_amdgcn_fdot2_f32_bf16(DA_PAIR(kv, 1), DA_PAIR(qv, 1), a1[h], false);
+        a0[h] = __builtin_amdgcn_fdot2_f32_bf16(DA_PAIR(kv, 2), DA_PAIR(qv, 2), a0[h], false);
+        a1[h] = __builtin_amdgcn_fdot2_f32_bf16(DA_PAIR(kv, 3), DA_PAIR(qv, 3), a1[h], false);
+      }
+    }
+    // the K slot is read: the next block's K DMA goes out now (its phys id comes from the read-ahead chunk)
+    const bool more = it + 1 < nmine;
+    int ph_next = 0;
+    if (more) {
+      ph_next = phys_of(it + 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      issue_k(bi + G, ph_next);
+    }
+    // ---- online softmax per head; P row (bf16) in (key group, j) order: key = g + 4 j -> [g][j]
+    const int key = bi * 64 + lane;
+    const bool valid = key < ctx;
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      const float s = valid ? (a0[h] + a1[h]) * sl2 : -INFINITY;
+      const float m_new = fmaxf(m_run[h], wave_max(s));  // the block holds >= 1 valid key: finite
+      const float alpha = exp2f(m_run[h] - m_new);
+      const bf16_t eb = f2bf(valid ? exp2f(s - m_new) : 0.f);
+      l_run[h] = l_run[h] * alpha + wave_sum(bf2f(eb));
+      m_run[h] = m_new;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[h][i] *= alpha;
+      sPw[h * 64 + (lane & 3) * 16 + (lane >> 2)] = eb;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's P rows are written before they are read
+    // ---- O += P V: lane group g = lane >> 4 owns keys g + 4 j (j = 0..15), d = 8 lpos .. 8 lpos + 7
+    uint32_t pp[G][8];
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      const uint4_ pa = *reinterpret_cast<const uint4_*>(sPw + h * 64 + lrow * 16);
+      const uint4_ pb = *reinterpret_cast<const uint4_*>(sPw + h * 64 + lrow * 16 + 8);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pp[h][i] = pa[i];
+        pp[h][4 + i] = pb[i];
+      }
+    }
+#pragma unroll
+    for (int jp = 0; jp < 8; ++jp) {  // keys (2 jp, 2 jp + 1) of the group: P pair pp[h][jp]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t va = vr[2 * jp][i], vb = vr[2 * jp + 1][i];
+        const bf16x2d lo = __builtin_bit_cast(bf16x2d, __builtin_amdgcn_perm(vb, va, 0x05040100u));  // d = 2i
+        const bf16x2d hi = __builtin_bit_cast(bf16x2d, __builtin_amdgcn_perm(vb, va, 0x07060302u));  // d = 2i + 1
+#pragma unroll
+        for (int h = 0; h < G; ++h) {
+          const bf16x2d pk = __builtin_bit_cast(bf16x2d, pp[h][jp]);
+          o[h][2 * i] = __builtin_amdgcn_fdot2_f32_bf16(pk, lo, o[h][2 * i], false);
+          o[h][2 * i + 1] = __builtin_amdgcn_fdot2_f32_bf16(pk, hi, o[h][2 * i + 1], false);
+        }
+      }
+    }
+    // (no scheduling across: hoisting the next block's V loads above P.V would need a second 64-register set)
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) issue_v(bi + G, ph_next);
+  }
+
+  // ---- merge the G waves' partials (the buffers alias the K slots: every wave is past its last QK^T read)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      sM[(w * G + h) * 2] = m_run[h];
+      sM[(w * G + h) * 2 + 1] = l_run[h];
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    float* dst = sO + ((w * G + h) * 4 + lrow) * D + lpos * 8;
+    *reinterpret_cast<float4_*>(dst) = float4_{o[h][0], o[h][1], o[h][2], o[h][3]};
+    *reinterpret_cast<float4_*>(dst + 4) = float4_{o[h][4], o[h][5], o[h][6], o[h][7]};
+  }
+  __syncthreads();
+  // wave w: head hq; lane holds d = 2 lane, 2 lane + 1
+  float s_new = -INFINITY, kr0 = 0.f, kr1 = 0.f;
+  if (new_tok) {
+    kr0 = bf2f(f2bf(kn0 * kc0 - kn1 * ks0));  // roped k, rounded to bf16 as the cache stores it
+    kr1 = bf2f(f2bf(kn1 * kc0 + kn0 * ks0));
+    s_new = wave_sum(kr0 * bf2f(sQb[w * D + lane]) + kr1 * bf2f(sQb[w * D + lane + D / 2])) * sl2;
+  }
+  float M = s_new;
+#pragma unroll
+  for (int ww = 0; ww < G; ++ww) M = fmaxf(M, sM[(ww * G + w) * 2]);
+  float L = 0.f, o0 = 0.f, o1 = 0.f;
+#pragma unroll
+  for (int ww = 0; ww < G; ++ww) {
+    const float mw = sM[(ww * G + w) * 2];
+    const float f = mw == -INFINITY ? 0.f : exp2f(mw - M);
+    L += sM[(ww * G + w) * 2 + 1] * f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float2 v = *reinterpret_cast<const float2*>(sO + ((ww * G + w) * 4 + g) * D + 2 * lane);
+      o0 += v.x * f;
+      o1 += v.y * f;
+    }
+  }
+  if (new_tok) {
+    const float e = bf2f(f2bf(exp2f(s_new - M)));  // P is bf16 on the cache path too
+    L += e;
+    o0 += e * bf2f(vn_pair & 0xffff);
+    o1 += e * bf2f(vn_pair >> 16);
+    if (w == 0) {  // this step's k / v into the cache (no workgroup of this launch reads that row)
+      const int slot_new = p.slots[b];
+      const long dst = (((long)(slot_new >> 6) * p.Hkv + hk) * 64 + (slot_new & 63)) * D;
+      bf16_t* kc = const_cast<bf16_t*>(p.k_cache);
+      bf16_t* vc = const_cast<bf16_t*>(p.v_cache);
+      kc[dst + lane] = f2bf(kr0);
+      kc[dst + lane + D / 2] = f2bf(kr1);
+      *reinterpret_cast<uint32_t*>(vc + dst + 2 * lane) = vn_pair;
+    }
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  *reinterpret_cast<uint32_t*>(p.o + (long)b * p.o_bs + (long)hq * D + 2 * lane) = pack2(o0 * inv, o1 * inv);
+}
+
+static int g_decode_wb = -1;
+int decode_wb_mode() {
+  if (g_decode_wb < 0) {
+    const char* e = getenv("SHAI_DECODE_WB");
+    g_decode_wb = (e != nullptr && atoi(e) == 0) ? 0 : 1;
+  }
+  return g_decode_wb;
+}
+int set_decode_wb(int mode) {
+  const int prev = decode_wb_mode();
+  if (mode >= 0) g_decode_wb = mode;
+  return prev;
+}
+
 size_t decode_attn_workspace(int B, int Hq, int D, int num_splits) {
   return (size_t)B * Hq * num_splits * (D + 2) * sizeof(float);
 }
 
 void launch_decode_attn(const DecodeAttnArgs& a, hipStream_t s) {
   const int G = a.Hq / a.Hkv;
+  if (a.D == 128 && G == kWbG && a.num_splits == 1 && decode_wb_mode()) {  // wave-per-block short-context kernel
+    decode_attn_wb_kernel<<<dim3((unsigned)(a.B * a.Hkv)), kWbG * 64, kWbLds, s>>>(a);
+    return;
+  }
   static const int width = [] {  // two workgroups per CU (70 KB of LDS each)
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||

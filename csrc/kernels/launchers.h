@@ -288,6 +288,9 @@ struct DecodeAttnArgs {
   float qkv_eps;
 };
 void launch_decode_attn(const DecodeAttnArgs& a, hipStream_t s);
+// short-context decode routing (D 128, GQA 4, one split -> the wave-per-block kernel); SHAI_DECODE_WB=0 / mode 0: split kernel
+int decode_wb_mode();
+int set_decode_wb(int mode);   // -1 keeps the mode; returns the previous one
 size_t decode_attn_workspace(int B, int Hq, int D, int num_splits);
 
 // Write new K/V tokens into the paged cache.

@@ -25,7 +25,7 @@ __all__ = [
     "rmsnorm", "layernorm", "groupnorm_stats", "groupnorm_apply", "groupnorm", "linear", "conv2d", "attention",
     "paged_attention", "decode_attention", "kv_write", "rope", "rope_pairs", "gated_act", "bias_act", "sched_step",
     "softmax_", "embedding", "token_feedback", "decode_attention_rope", "decode_attention_rope_qkv", "gemm_partials", "quantize_fp8_rows", "dequant_fp8", "quant_rows_fp8", "gemm_f8", "pack_conv_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
-    "ACT_GELU_TANH", "ACT_QUICK_GELU", "ACT_RELU", "decode_splits",
+    "ACT_GELU_TANH", "ACT_QUICK_GELU", "ACT_RELU", "decode_splits", "set_decode_wb",
 ]
 
 
@@ -412,6 +412,12 @@ def bmm(a: torch.Tensor, w: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
     y = torch.empty(B, M, N, dtype=a.dtype, device=a.device)
     _K().gemm(a, w, y, None, None, 1, None, float(alpha), 1.0, ACT_NONE, False)
     return y
+
+
+def set_decode_wb(mode: int = -1) -> int:
+    """Decode attention routing at D 128 / GQA 4 / one split: 1 = the wave-per-block short-context kernel (default),
+    0 = the split kernel (``SHAI_DECODE_WB=0``); -1 keeps the mode.  Returns the previous mode (A/B in one process)."""
+    return int(_K().set_decode_wb(int(mode)))
 
 
 def set_halo_conv(mode: int = -1, waves: int = -1) -> int:

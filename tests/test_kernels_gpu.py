@@ -544,3 +544,53 @@ def test_flash128_x2_spikes_varlen_gqa(cuda, causal):
         n = int((ql if ql is not None else torch.full_like(kl, S))[b])
         close(o[b, :n], orf[b, :n], 2e-2)
         close(o[b, :n], o2[b, :n], 2e-2)
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_decode_attn_wave_per_block_matches_split_kernel(cuda, fused):
+    """The short-context wave-per-block decode kernel (D 128, GQA 4, one split; each wave walks its own 64-token
+    blocks for all four q heads) against the fp32 reference and the split kernel (set_decode_wb(0)): contexts of
+    1 / 63 / 64 / 65 / 256 / 257 tokens (waves with no block, a ragged last block, more than one block per wave) and
+    one of 17,000 (67 blocks per wave: the block-id read-ahead reloads its 64-entry chunk).  fused: RoPE + this
+    step's k / v from the QKV rows (written to the cache, attended from registers), padding row (slot -1) last."""
+    torch.manual_seed(31)
+    D, Hq, Hkv = 128, 32, 8
+    ctx = [1, 63, 64, 65, 256, 257, 17000, 5]
+    B = len(ctx)
+    kc, vc, bt = _paged_setup(B, Hkv, D, ctx, nblocks=sum((c + 63) // 64 for c in ctx) + 8)
+    lens = torch.tensor(ctx, dtype=torch.int32, device="cuda")
+    prev = ops.set_decode_wb(-1)
+    try:
+        if not fused:
+            q = rnd(B, Hq, D)
+            want = ref.decode_attention(q, kc, vc, bt, lens, 1 / math.sqrt(D))
+            ops.set_decode_wb(1)
+            o = ops.decode_attention(q, kc, vc, bt, lens, num_splits=1)
+            ops.set_decode_wb(0)
+            o_split = ops.decode_attention(q, kc, vc, bt, lens, num_splits=1)
+            close(o, want, 2e-2)
+            close(o, o_split, 2e-2)
+            return
+        qkv = rnd(B, (Hq + 2 * Hkv) * D)
+        ang = torch.rand(max(ctx) + 1, D // 2, device="cuda") * 3
+        cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
+        pos = lens - 1
+        slots = torch.stack([bt[b, (c - 1) // 64] * 64 + (c - 1) % 64 for b, c in enumerate(ctx)]).int()
+        slots[-1] = -1
+        outs, caches = [], []
+        for mode in (1, 0):
+            ops.set_decode_wb(mode)
+            k2, v2 = kc.clone(), vc.clone()
+            outs.append(ops.decode_attention_rope(qkv.clone(), k2, v2, bt, lens, pos, cos, sin, slots, Hq, Hkv,
+                                                  num_splits=1))
+            caches.append((k2, v2))
+        assert torch.equal(caches[0][0], caches[1][0]) and torch.equal(caches[0][1], caches[1][1])
+        close(outs[0][:-1], outs[1][:-1], 2e-2)
+        # fp32 reference over the updated cache (the new token is in it now)
+        q2 = qkv.clone()
+        k3, v3 = kc.clone(), vc.clone()
+        ops.rope_qkv_cache(q2, pos, cos, sin, k3, v3, slots, Hq, Hkv)
+        want = ref.decode_attention(q2[:, :Hq * D].reshape(B, Hq, D), k3, v3, bt, lens, 1 / math.sqrt(D))
+        close(outs[0][:-1], want.reshape(B, Hq * D)[:-1], 2e-2)
+    finally:
+        ops.set_decode_wb(prev)

@@ -31,6 +31,30 @@ def timeit(fn, iters=20, warmup=3):
     return s.elapsed_time(e) / iters * 1e-3
 
 
+def graph_time(fn, iters=32, reps=5):
+    """Seconds per call of fn with the host out of the loop: `iters` calls captured into one HIP graph, the
+    replay timed with events (best of `reps`).  For kernels shorter than the host's per-call launch cost."""
+    fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        fn()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(iters):
+                fn()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) / iters * 1e-3)
+    return best
+
+
 def rnd(*shape):
     return torch.randn(*shape, device="cuda").to(torch.bfloat16)
 
@@ -233,12 +257,24 @@ def bench_dattn(rows):
         qkv = rnd(B, (h + 2 * hk) * D)
         gb = B * hk * (ctx - 1) * D * 2 * 2 / 1e9
         r = dict(op="decode_attn", shape=f"B{B} ctx{ctx}")
+        prev = ops.set_decode_wb(0)
         for sp in (1, 2, 4, 8, 16):
             if sp > nblk:
                 continue
             t = timeit(lambda: ops.decode_attention_rope(qkv, kc, vc, bt, ctx_l, pos, cos, sin, slots, h, hk,
                                                          num_splits=sp), iters=48)
             r[f"s{sp}_us"] = t * 1e6
+        ops.set_decode_wb(1)  # one split -> the wave-per-block kernel
+        t = timeit(lambda: ops.decode_attention_rope(qkv, kc, vc, bt, ctx_l, pos, cos, sin, slots, h, hk,
+                                                     num_splits=1), iters=48)
+        r["wb_us"] = t * 1e6
+        # graph-replayed (host launch cost out of the loop): split kernel vs wave-per-block, one split
+        for mode, name in ((0, "g_s1_us"), (1, "g_wb_us")):
+            ops.set_decode_wb(mode)
+            o = torch.empty(B, h * D, device="cuda", dtype=torch.bfloat16)
+            r[name] = graph_time(lambda: ops.decode_attention_rope(qkv, kc, vc, bt, ctx_l, pos, cos, sin, slots, h,
+                                                                   hk, num_splits=1, out=o)) * 1e6
+        ops.set_decode_wb(prev)
         best = min(v for k, v in r.items() if k.endswith("_us"))
         r["best_GBps"] = gb / (best / 1e6)
         r["auto_splits"] = ops.decode_splits(B, hk, ctx)
