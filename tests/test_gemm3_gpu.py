@@ -181,3 +181,27 @@ rel = ((y.float().cpu() - yr.float()).norm() / yr.float().norm()).item()
 print("REL", rel)
 assert rel < 2e-2, rel
 """
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("glu", [False, True])
+def test_gemm2_every_tile_config_forced(cuda, cfg, splits, glu):
+    """Every v2 tile config (gemm_lds.hip: 0 = 256x320, 1 = 256x256, 2 = 256x128, 3 = 128x128, 4 = 128x64 -- 0 and 1
+    hold ~20 cached shapes with no other forced test) unsplit and split-K 3 (force 3000 + 100 splits + cfg), with
+    bias + activation + residual (or the GLU epilogue), ragged M / N / K tails, against fp32."""
+    torch.manual_seed(40 + cfg)
+    M, N, K = 700, 1288 if not glu else 1280, 1000
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    w = (torch.randn(N, K, device=cuda) / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device=cuda).bfloat16()
+    No = N // 2 if glu else N
+    r = torch.randn(M, No, device=cuda).bfloat16()
+    out = torch.empty(M, No, device=cuda, dtype=torch.bfloat16)
+    force = cfg if splits == 1 else 3000 + 100 * splits + cfg
+    act = "gelu" if glu else "silu"
+    ops.gemm_into(a, w, out, bias, act=act, residual=r, glu=glu, force_cfg=force)
+    y = a.float() @ w.float().t() + bias.float()
+    f = torch.nn.functional.gelu if glu else torch.nn.functional.silu
+    want = (y[:, 0::2] * f(y[:, 1::2]) if glu else f(y)) + r.float()
+    assert _rel(out, want) < 1e-2
