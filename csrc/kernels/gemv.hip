@@ -31,6 +31,7 @@
 //   in the reduction.  Half the weight bytes per token: decode is weight-bandwidth bound.
 #include "common.h"
 #include "launchers.h"
+#include "gemm_epilogue.h"
 
 #include <cstdlib>
 #include <map>
@@ -45,6 +46,7 @@ constexpr int SK_BN = 64;       // W rows per workgroup
 constexpr int SK_BK = 64;       // K per step
 constexpr int SK_WAVES = 4;
 constexpr uint32_t SK_OOB = 0x80000000u;
+constexpr int SK_RP4 = SK_BN + 4;  // floats per m row of the cross-wave reduction image (16 B of bank skew)
 
 // (An X-in-registers variant with an 8-deep W-only ring measured 10-25 % slower at M = 64 --
 // profiles/mistral7b_b64_async_decode_round2.md -- and was dropped: the X tile in LDS is not the limiter.)
@@ -55,10 +57,8 @@ struct SkGeom {
   static constexpr int W_ELEMS = F8 ? SK_BN * SK_BK / 2 : SK_BN * SK_BK;  // W tile in bf16 units
   static constexpr int STAGE_ELEMS = W_ELEMS + MB * SK_BK;  // W tile then X tile
   static constexpr int PER = (F8 ? 1 : 2) + XG;         // DMA instructions per wave per step
-  static constexpr int RP = MB + 1;                     // padded row of the reduction image
-  static constexpr size_t LDS = (size_t)STAGES * STAGE_ELEMS * 2 > (size_t)SK_WAVES * SK_BN * RP * 4
-                                    ? (size_t)STAGES * STAGE_ELEMS * 2
-                                    : (size_t)SK_WAVES * SK_BN * RP * 4;
+  static constexpr size_t RED = (size_t)SK_WAVES * MB * SK_RP4 * 4;  // reduction image red[w][m][n]
+  static constexpr size_t LDS = (size_t)STAGES * STAGE_ELEMS * 2 > RED ? (size_t)STAGES * STAGE_ELEMS * 2 : RED;
 };
 
 __device__ __forceinline__ int sk_swz(int row, int ch) { return row * SK_BK + ((ch ^ ((row >> 1) & 7)) << 3); }
@@ -73,6 +73,15 @@ __device__ __forceinline__ void sk_store_wt(__amdgpu_buffer_rsrc_t r, uint32_t o
 }
 __device__ __forceinline__ float sk_load_wt(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 16));
+}
+
+// the same, 16 B per lane (the slab of the in-launch split-K fixup, one float4 per thread and quad)
+__device__ __forceinline__ void sk_store_wt4(__amdgpu_buffer_rsrc_t r, uint32_t off, const float v[4]) {
+  const uint4_ u = uint4_{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+  __builtin_amdgcn_raw_buffer_store_b128(u, r, (int)off, 0, 16);
+}
+__device__ __forceinline__ float4_ sk_load_wt4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float4_, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16));
 }
 
 template <int PER, int N>
@@ -100,28 +109,6 @@ __device__ __forceinline__ void sk_store(const GemmArgs& p, int n, int m, float 
     float o = apply_act<ACT>(v0 * p.alpha + (p.bias ? bf2f(p.bias[n]) : 0.f));
     if (p.residual) o += bf2f(p.residual[(long)m * p.ldr + n]) * p.res_alpha;
     p.C[(long)m * p.ldc + n] = f2bf(o);
-  }
-}
-
-// Epilogue over a reduced 64 (n) x MB (m) tile held as get(nl, m).
-template <int MB, bool GLU, int ACT, typename Get>
-__device__ __forceinline__ void sk_epilogue(const GemmArgs& p, int n0, Get get) {
-  const int tid = threadIdx.x;
-  if constexpr (GLU) {
-    // 32 pairs x MB m, consecutive threads -> consecutive pairs
-#pragma unroll
-    for (int it = 0; it < 32 * MB / 256; ++it) {
-      const int idx = tid + it * 256;
-      const int m = idx >> 5, pr = idx & 31;
-      if (m < p.M) sk_store<GLU, ACT>(p, n0 + 2 * pr, m, get(2 * pr, m), get(2 * pr + 1, m));
-    }
-  } else {
-#pragma unroll
-    for (int it = 0; it < 64 * MB / 256; ++it) {
-      const int idx = tid + it * 256;
-      const int m = idx >> 6, nl = idx & 63;
-      if (m < p.M) sk_store<GLU, ACT>(p, n0 + nl, m, get(nl, m), 0.f);
-    }
   }
 }
 
@@ -269,20 +256,27 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
     for (int j = 0; j < XG; ++j) ss_red[w][64 * j + lane] = ss[j];
   }
 
-  // ---- cross-wave reduction: red[w][nl][m] (padded), reusing the stage ring
+  // ---- cross-wave reduction through LDS (the stage ring is dead), 16-byte granules: wave w stores its partial tile
+  // m-major, red[w][m][n] at a row pitch of SK_RP4 floats (16 B of bank skew per m row: conflict-free
+  // ds_write_b128 / ds_read_b128), each lane's 4 consecutive-n accumulators (registers 4q .. 4q + 3: n = 8q + 4fh
+  // + 0..3 of its 32-row half, m = 32j + fr) as ONE float4; a thread then owns output quads (m, 4 consecutive n) and
+  // sums the 4 waves' float4s in wave order -- 4x fewer LDS instructions than element-wise, the epilogue / partial
+  // stores 8-16 B per lane (gpurun_out/r6m_decode_lab2.log: the element-wise reduction + 4-B stores cost 2.4-3.9 us
+  // per launch over the streaming loop).
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   float* red = reinterpret_cast<float*>(sk_smem);
-  constexpr int RP = G::RP;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int nl = (i & 3) + 8 * (i >> 2) + 4 * fh;
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int j = 0; j < XG; ++j) {
-      red[(w * SK_BN + nl) * RP + 32 * j + fr] = acc[0][j][i];
-      red[(w * SK_BN + 32 + nl) * RP + 32 * j + fr] = acc[1][j][i];
-    }
-  }
+    for (int j = 0; j < XG; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = 32 * h + 8 * q + 4 * fh, m = 32 * j + fr;
+        SHAI_DASSERT((w * MB + m) * SK_RP4 + n + 4 <= (int)(G::LDS / 4));
+        *reinterpret_cast<float4_*>(red + (w * MB + m) * SK_RP4 + n) =
+            float4_{acc[h][j][4 * q], acc[h][j][4 * q + 1], acc[h][j][4 * q + 2], acc[h][j][4 * q + 3]};
+      }
   __syncthreads();
   auto row_ss = [&](int m) {
     const int j = m >> 5, r = m & 31;
@@ -295,37 +289,61 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
     if (KG == 1 && tid < MB) rstd_s[tid] = rsqrtf(row_ss(tid) / p.K + p.rms_eps);
     __syncthreads();
   }
-  auto wsum = [&](int nl, int m) {
-    float v = 0.f;
+  constexpr int QPT = MB * 16 / 256;  // output quads (m, 4 consecutive n) per thread
+  // quad it of this thread: qd = tid + 256 it, m = qd >> 4, n = 4 (qd & 15); v = sum over waves in wave order,
+  // times the fp8 row scale (per n) and, unsplit, the folded RMSNorm's rstd[m]
+  auto qsum = [&](int it, float v[4]) {
+    const int qd = tid + 256 * it, m = qd >> 4, n = 4 * (qd & 15);
+    float4_ a = float4_{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < SK_WAVES; ++q) v += red[(q * SK_BN + nl) * RP + m];
-    if constexpr (F8) v *= (n0 + nl < p.N) ? p.w_scale[n0 + nl] : 0.f;
-    if constexpr (RMS) {
-      if (KG == 1) v *= rstd_s[m];
+    for (int q = 0; q < SK_WAVES; ++q) a += *reinterpret_cast<const float4_*>(red + (q * MB + m) * SK_RP4 + n);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = a[e];
+      if constexpr (F8) v[e] *= (n0 + n + e < p.N) ? p.w_scale[n0 + n + e] : 0.f;
+      if constexpr (RMS) {
+        if (KG == 1) v[e] *= rstd_s[m];
+      }
     }
-    return v;
+  };
+  // fused epilogue of quad (m, n): 4 consecutive outputs (2 GLU pairs) with 8-B stores where the quad is whole
+  auto quad_out = [&](int m, int n, float v[4]) {
+    if (m >= p.M || n0 + n >= p.N) return;
+    if (n0 + n + 3 < p.N) {
+      epilogue4<GLU, ACT>(p, p.C, p.residual, m, n0 + n, v);
+    } else if constexpr (GLU) {
+      for (int e = 0; e < 4 && n0 + n + e + 1 < p.N; e += 2) sk_store<GLU, ACT>(p, n0 + n + e, m, v[e], v[e + 1]);
+    } else {
+      for (int e = 0; e < 4; ++e) sk_store<GLU, ACT>(p, n0 + n + e, m, v[e], 0.f);
+    }
   };
   if (KG == 1) {
-    sk_epilogue<MB, GLU, ACT>(p, n0, wsum);
+#pragma unroll
+    for (int it = 0; it < QPT; ++it) {
+      float v[4];
+      qsum(it, v);
+      const int qd = tid + 256 * it;
+      quad_out(qd >> 4, 4 * (qd & 15), v);
+    }
     return;
   }
   if (cnt != nullptr) {
     // ---- split-K fixed up in this launch (no reduce kernel): every K group writes its 64 x MB partial slab
-    // (+ MB row sums of squares) write-through (sc1), drains (vmcnt 0 in every wave), joins the workgroup
-    // barrier, then one lane takes a ticket (relaxed agent-scope atomic on this launch's own ticket slice,
-    // sk_tickets); the workgroup that draws KG-1 re-arms the ticket and reduces the KG slabs with sc1 loads
-    // before the fused epilogue.
+    // (+ MB row sums of squares) write-through (sc1, 16 B per lane), drains (vmcnt 0 in every wave), joins the
+    // workgroup barrier, then one lane takes a ticket (relaxed agent-scope atomic on this launch's own ticket
+    // slice, sk_tickets); the workgroup that draws KG-1 re-arms the ticket and reduces the KG slabs with sc1
+    // loads before the fused epilogue.
     // (MI355X_MICROARCH / hip guide "Projection GEMM at M = 256" item 2, write-through form.)
-    constexpr int SLAB = 64 * MB + MB, PT = 64 * MB / 256;
+    // Slab layout: element m * 64 + n, i.e. float4 qd of this thread at byte 16 qd.
+    constexpr int SLAB = 64 * MB + MB;
     const __amdgpu_buffer_rsrc_t rws = sk_rsrc(ws, 0x7fffffffu);
     const uint32_t tile_base = (uint32_t)((long)tile * KG * SLAB * 4);
     const uint32_t my_base = tile_base + (uint32_t)(kg * SLAB * 4);
-    float part[PT];  // element idx = tid + 256 it <-> (m = idx >> 6, nl = idx & 63), kept for the fixup
+    float part[QPT][4];
 #pragma unroll
-    for (int it = 0; it < PT; ++it) {
-      const int idx = tid + it * 256;
-      part[it] = wsum(idx & 63, idx >> 6);
-      sk_store_wt(rws, my_base + idx * 4, part[it]);
+    for (int it = 0; it < QPT; ++it) {
+      qsum(it, part[it]);
+      sk_store_wt4(rws, my_base + (tid + 256 * it) * 16, part[it]);
     }
     float ssv = 0.f;
     if constexpr (RMS) {
@@ -341,7 +359,7 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
       // The hand-off follows the write-through publish form (cdna_hip_programming.md Guideline 16, R1 with
       // sc1 consumer loads): every slab byte is stored sc1 by its writing wave, EVERY wave drains vmcnt(0)
       // before the workgroup barrier above, the signal is an agent-scope atomic, and the last arriver reads
-      // the slabs ONLY with sc1 loads into registers (sk_load_wt) -- no other load of this launch touches
+      // the slabs ONLY with sc1 loads into registers (sk_load_wt*) -- no other load of this launch touches
       // bytes another workgroup wrote.  So the ticket is relaxed and the acquire is a wavefront-scope fence
       // (no instruction: it only keeps the compiler from hoisting the slab loads above the ticket).  An
       // agent-scope acq_rel here (buffer_wbl2 + buffer_inv of the XCD's L2) measured -7 % Mistral decode.
@@ -355,21 +373,24 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
     // sum the KG slabs in K-group order (this group's own slab from registers), so the result does not
     // depend on which group arrived last: four slabs at a time with every load issued before the first add
     // (slots past KG, and this group's own slot, re-read this group's slab and substitute / drop it)
-    float own[PT], own_ss = ssv;
+    float own[QPT][4], sum[QPT][4], own_ss = ssv;
 #pragma unroll
-    for (int it = 0; it < PT; ++it) {
-      own[it] = part[it];
-      part[it] = 0.f;
-    }
+    for (int it = 0; it < QPT; ++it)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        own[it][e] = part[it][e];
+        sum[it][e] = 0.f;
+      }
     ssv = 0.f;
     for (int u0 = 0; u0 < KG; u0 += 4) {
-      float t[4][PT], ts[4];
+      float4_ t[4][QPT];
+      float ts[4];
 #pragma unroll
       for (int uu = 0; uu < 4; ++uu) {
         const int q = u0 + uu < KG ? u0 + uu : kg;
         const uint32_t b = tile_base + (uint32_t)(q * SLAB * 4);
 #pragma unroll
-        for (int it = 0; it < PT; ++it) t[uu][it] = sk_load_wt(rws, b + (tid + it * 256) * 4);
+        for (int it = 0; it < QPT; ++it) t[uu][it] = sk_load_wt4(rws, b + (tid + 256 * it) * 16);
         ts[uu] = 0.f;
         if constexpr (RMS) ts[uu] = sk_load_wt(rws, b + (64 * MB + (tid & (MB - 1))) * 4);
       }
@@ -379,36 +400,45 @@ __global__ void __launch_bounds__(SK_WAVES * 64) skinny_gemm_kernel(const GemmAr
         if (q < KG) {
           const bool mine = q == kg;
 #pragma unroll
-          for (int it = 0; it < PT; ++it) part[it] += mine ? own[it] : t[uu][it];
+          for (int it = 0; it < QPT; ++it)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sum[it][e] += mine ? own[it][e] : t[uu][it][e];
           ssv += mine ? own_ss : ts[uu];
         }
       }
     }
     if constexpr (RMS) {
       if (tid < MB) rstd_s[tid] = rsqrtf(ssv / p.K + p.rms_eps);
+      __syncthreads();
     }
-    float* sum = reinterpret_cast<float*>(sk_smem);  // the reduction image is dead past the ticket barrier
 #pragma unroll
-    for (int it = 0; it < PT; ++it) sum[tid + it * 256] = part[it];
-    __syncthreads();
-    auto fsum = [&](int nl, int m) {
-      float v = sum[m * 64 + nl];
-      if constexpr (RMS) v *= rstd_s[m];
-      return v;
-    };
-    sk_epilogue<MB, GLU, ACT>(p, n0, fsum);
+    for (int it = 0; it < QPT; ++it) {
+      const int qd = tid + 256 * it, m = qd >> 4;
+      if constexpr (RMS) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sum[it][e] *= rstd_s[m];
+      }
+      quad_out(m, 4 * (qd & 15), sum[it]);
+    }
     return;
   }
   if constexpr (RMS) {  // row sum-of-squares partials for the fold (one tile per K group writes them)
     if (tile == 0 && tid < p.M) ws[(long)KG * p.M * p.N + (long)kg * p.M + tid] = row_ss(tid);
   }
-  // ---- split-K over workgroups: fp32 partials [kg][M][N]; launch_splitk_epilogue folds them.
+  // ---- split-K over workgroups: fp32 partials [kg][M][N]; launch_splitk_epilogue (or the decode attention's QKV
+  // fold) folds them.  16 B per lane where the quad is whole and N keeps rows 16-B aligned.
   float* part = ws + (long)kg * p.M * p.N;
 #pragma unroll
-  for (int it = 0; it < 64 * MB / 256; ++it) {
-    const int idx = tid + it * 256;
-    const int m = idx >> 6, nl = idx & 63;
-    if (m < p.M && n0 + nl < p.N) part[(long)m * p.N + n0 + nl] = wsum(nl, m);
+  for (int it = 0; it < QPT; ++it) {
+    float v[4];
+    qsum(it, v);
+    const int qd = tid + 256 * it, m = qd >> 4, n = n0 + 4 * (qd & 15);
+    if (m >= p.M || n >= p.N) continue;
+    if (n + 3 < p.N && (p.N & 3) == 0) {
+      *reinterpret_cast<float4_*>(part + (long)m * p.N + n) = float4_{v[0], v[1], v[2], v[3]};
+    } else {
+      for (int e = 0; e < 4 && n + e < p.N; ++e) part[(long)m * p.N + n + e] = v[e];
+    }
   }
 }
 
