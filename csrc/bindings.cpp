@@ -165,6 +165,7 @@ bool lib_enabled() {  // off by default: every GEMM runs on the hand-written ker
 int max_splits_for(const shai::GemmArgs& g) {
   const int batch = g.batch > 0 ? g.batch : 1;
   if (batch != 1 || g.row_mr != nullptr) return 1;  // folded LayerNorm: applied by the unsplit v4 epilogue only
+  if (g.upsample == 2) return 1;                      // phase conv: the split-K fold would write GEMM rows
   const long kt = (g.K + 63) / 64;
   int s = 1;
   while (s < 16 && kt / (s * 2) >= 4) s *= 2;
@@ -940,7 +941,7 @@ void conv2d(const Tensor& x, const optional<Tensor>& x2, const Tensor& w, const 
             const optional<Tensor>& in_scale, const optional<Tensor>& in_shift, int64_t in_act, int64_t kh,
             int64_t kw, int64_t stride, int64_t pad, bool upsample, int64_t act, double res_alpha,
             const optional<Tensor>& ln_mr, const optional<Tensor>& ln_s, const optional<Tensor>& gn_part,
-            const optional<Tensor>& ln_stats, double ln_eps) {
+            const optional<Tensor>& ln_stats, double ln_eps, bool up_phases) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_bf16(out, "out");
@@ -977,11 +978,22 @@ void conv2d(const Tensor& x, const optional<Tensor>& x2, const Tensor& w, const 
   SHAI_CHECK(!upsample || stride == 1, "upsample requires stride 1");
   g.OH = (IH + 2 * pad - kh) / stride + 1;
   g.OW = (IW + 2 * pad - kw) / stride + 1;
+  if (up_phases) {
+    // nearest-2x upsample + 3x3 pad-1 conv as 4 phase 2x2 convs over the source (w: [4 Cout, 4 Cin] phase weights,
+    // ops.pack_up2_phase_weight); v4 kernel only (gemm_8ph.hip CONV 3)
+    SHAI_CHECK(upsample && kh == 2 && kw == 2 && stride == 1 && pad == 0 && !x2 && !in_scale && !residual,
+               "up_phases: phase weights of a plain upsample + 3x3 conv (kh = kw = 2, pad 0, no concat / norm / residual)");
+    g.upsample = 2;
+    g.OH = 2 * g.H;
+    g.OW = 2 * g.Wd;
+  }
   SHAI_CHECK(out.size(0) == g.Nimg && out.size(1) == g.OH && out.size(2) == g.OW, "conv2d out shape ", out.sizes(),
              " expected spatial ", g.OH, "x", g.OW);
   g.N = out.size(3);
   g.K = kh * kw * g.Cin;
-  SHAI_CHECK(w.size(0) == g.N && w.numel() == (long)g.N * g.K, "conv2d weight must be [Cout, KH*KW*Cin]");
+  const int wsets = up_phases ? 4 : 1;
+  SHAI_CHECK(w.size(0) == wsets * g.N && w.numel() == (long)wsets * g.N * g.K, "conv2d weight must be [Cout, KH*KW*Cin]",
+             up_phases ? " per phase" : "");
   g.M = g.Nimg * g.OH * g.OW;
   g.A = xcat.defined() ? cptr(xcat) : cptr(x);
   g.W = cptr(w);
@@ -1021,6 +1033,8 @@ void conv2d(const Tensor& x, const optional<Tensor>& x2, const Tensor& w, const 
   }
   OutStats st;
   attach_norm_io(g, ln_mr, ln_s, gn_part, ln_stats, ln_eps, &st);
+  SHAI_CHECK(g.upsample != 2 || (shai::gemm4_supported(g) && use_v2(g, x.numel() * 2, w.numel() * 2, 0)),
+             "up_phases: shape not supported by the phase conv (needs Cin % 64 == 0, H W % 256 == 0, v2 GEMM path)");
   // Halo-tiled conv (conv_halo.hip): GroupNorm(+SiLU) convs (SHAI_HALO_CONV >= 1) and, at mode 2, every 3x3
   // stride-1 conv it supports; the output's GroupNorm partials come from its epilogue.
   const int hmode = halo_conv_mode();
@@ -1648,7 +1662,7 @@ TORCH_LIBRARY(shai, m) {
   m.def("dequant_fp8(Tensor w8, Tensor scale, Tensor(a!) out) -> ()");
   m.def("layernorm_mod(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, int rows_per_mod, float eps) -> ()");
   m.def("qk_norm_rope(Tensor(a!) x, Tensor? q_w, Tensor? k_w, Tensor? cos, Tensor? sin, int H, int D, int S, float eps) -> ()");
-  m.def("conv2d(Tensor x, Tensor? x2, Tensor w, Tensor(a!) out, Tensor? bias, Tensor? bias2d, Tensor? residual, Tensor? in_scale, Tensor? in_shift, int in_act, int kh, int kw, int stride, int pad, bool upsample, int act, float res_alpha, Tensor? ln_mr=None, Tensor? ln_s=None, Tensor(b!)? gn_part=None, Tensor(c!)? ln_stats=None, float ln_eps=1e-5) -> ()");
+  m.def("conv2d(Tensor x, Tensor? x2, Tensor w, Tensor(a!) out, Tensor? bias, Tensor? bias2d, Tensor? residual, Tensor? in_scale, Tensor? in_shift, int in_act, int kh, int kw, int stride, int pad, bool upsample, int act, float res_alpha, Tensor? ln_mr=None, Tensor? ln_s=None, Tensor(b!)? gn_part=None, Tensor(c!)? ln_stats=None, float ln_eps=1e-5, bool up_phases=False) -> ()");
   m.def("flash_attn(Tensor q, Tensor k, Tensor v, Tensor(a!) o, float scale, bool causal, int causal_offset, Tensor? kv_lens, Tensor? q_lens, Tensor? bias, Tensor? block_table) -> ()");
   m.def("paged_attn_varlen(Tensor q, Tensor k_cache, Tensor v_cache, Tensor(a!) o, Tensor block_table, Tensor kv_lens, Tensor q_lens, Tensor q_start, int max_q, float scale, bool causal) -> ()");
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor(a!) o, Tensor block_table, Tensor ctx_lens, Tensor(b!) ws, int num_splits, float scale) -> ()");

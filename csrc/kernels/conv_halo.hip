@@ -492,6 +492,7 @@ bool conv_halo_supported(const GemmArgs& a) {
     if (a.in_act != ACT_SILU || a.upsample || a.in_shift != a.in_scale + (long)a.Nimg * a.Cin) return false;
     if (!hc_al16(a.in_scale) || a.Cin % 4 != 0) return false;
   }
+  if (a.upsample == 2) return false;  // phase-decomposed upsample conv: v4 only
   if (a.upsample && (a.OH != 2 * a.H || a.OW != 2 * a.Wd)) return false;
   if (!a.upsample && (a.OH != a.H || a.OW != a.Wd)) return false;
   if (a.ldw != a.K || a.ldc != a.N || (a.residual && a.ldr != a.N)) return false;

@@ -110,7 +110,14 @@ struct G4ConvPos {
   int kh, kw, c;
 };
 
-// CONV: 0 plain GEMM, 1 implicit-GEMM conv, 2 implicit-GEMM conv over a nearest-2x upsampled input.
+// CONV: 0 plain GEMM, 1 implicit-GEMM conv, 2 implicit-GEMM conv over a nearest-2x upsampled input,
+// 3 the same upsample + 3x3 conv decomposed by output phase (GemmArgs::upsample == 2): an output pixel
+// (2i + py, 2j + px) of the upsampled grid reads only 2 x 2 distinct source pixels (rows i - 1 + py + a, columns
+// j - 1 + px + b), so each of the 4 phases is a 2 x 2 conv over the LOW-resolution input with its own summed
+// weights ([4 phases][Cout][4 taps x Cin], ops.pack_up2_phase_weight): K = 4 Cin instead of 9 Cin, 2.25x fewer
+// FLOPs.  GEMM rows are ordered (image, phase, i, j), so a 256-row tile (H W % 256 == 0) has one image and one
+// phase (its weight slice), the GroupNorm partials' 128-row blocks stay inside one image, and the epilogue maps
+// each row to its output pixel.
 template <int CONV, bool GLU, int ACT, bool SPLITK, int VAR, int BN>
 __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __restrict__ ws, int k_per_split) {
   constexpr bool STAGGER = !(VAR & 1), STATIC_PRIO = (VAR & 2) != 0, PERSIST = (VAR & 8) != 0 && !SPLITK;
@@ -150,7 +157,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
 
   const bf16_t* A = p.A + (long)b * p.batch_a;
   const bf16_t* Wt = p.W + (long)b * p.batch_w;
-  const __amdgpu_buffer_rsrc_t rW = g4_rsrc(Wt, (long)p.N * p.ldw * 2);
+  const __amdgpu_buffer_rsrc_t rW = g4_rsrc(Wt, (long)p.N * p.ldw * 2 * (CONV == 3 ? 4 : 1));
   __amdgpu_buffer_rsrc_t rA, rA2;
   if constexpr (CONV != 0) {
     rA = g4_rsrc(A, (long)p.Nimg * p.H * p.Wd * (p.A2 ? p.Cin1 : p.Cin) * 2);
@@ -183,7 +190,9 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
     for (int j = 0; j < NWJ; ++j) {
       const int r = wid * (BN / 8) + j * 8 + lrow;  // LDS row
       const int n = n0 + (WIDE ? g4_wperm<BN>(r) : r);
-      woff[j] = n < p.N ? (uint32_t)(((long)n * p.ldw + kchw[j]) * 2) : G4_OOB;
+      // phase conv: the tile's phase selects its weight slice (rows ph N .. ph N + N - 1)
+      const long wrow = CONV == 3 ? (long)((m0 % (p.OH * p.OW)) / (p.H * p.Wd)) * p.N + n : (long)n;
+      woff[j] = n < p.N ? (uint32_t)((wrow * p.ldw + kchw[j]) * 2) : G4_OOB;
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -196,7 +205,17 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
         const int cn = mm / hw;
         const int rem = mm - cn * hw;
         const int coh = rem / p.OW, cow = rem - coh * p.OW;
-        if constexpr (CONV == 1) {
+        if constexpr (CONV == 3) {
+          // row (image cn, phase ph, i, j): 2 x 2 taps from source row i - 1 + py, column j - 1 + px
+          const int hwl = p.H * p.Wd;
+          const int ph = rem / hwl, r2 = rem - ph * hwl;
+          const int si = r2 / p.Wd, sj = r2 - si * p.Wd;
+          ih0[j] = m < p.M ? si - 1 + (ph >> 1) : -(1 << 24);
+          iw0[j] = sj - 1 + (ph & 1);
+          pix[j] = (cn * p.H + ih0[j]) * p.Wd + iw0[j];
+          (void)coh;
+          (void)cow;
+        } else if constexpr (CONV == 1) {
           ih0[j] = m < p.M ? coh * p.stride - p.pad : -(1 << 24);
           iw0[j] = cow * p.stride - p.pad;
           pix[j] = (cn * p.H + ih0[j]) * p.Wd + iw0[j];
@@ -223,7 +242,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
     if ((g & 1) || g == 8) {
       uint32_t off = woff[j] + (uint32_t)k0 * 2;
       if (ktail && k0 + kchw[j] >= k_end) off = G4_OOB;
-      SHAI_DASSERT_DMA(off, (long)p.N * p.ldw * 2, G4_OOB);
+      SHAI_DASSERT_DMA(off, (long)p.N * p.ldw * 2 * (CONV == 3 ? 4 : 1), G4_OOB);
       SHAI_DASSERT(buf >= 0 && buf < 2);
       g4_glds(rW, sa + G4_BM * G4_BK + (wid * (BN / 8) + j * 8) * G4_BK, off);
       return;
@@ -239,7 +258,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
       const int cb = second ? cp.c - p.Cin1 : cp.c;
       const int ih = ih0[j] + cp.kh, iw = iw0[j] + cp.kw;
       uint32_t off;
-      if constexpr (CONV == 1) {
+      if constexpr (CONV == 1 || CONV == 3) {
         const bool ok = ((unsigned)ih < (unsigned)p.H) & ((unsigned)iw < (unsigned)p.Wd);
         const int tapd = cp.kh * p.Wd + cp.kw;
         off = ok ? (uint32_t)((pix[j] + tapd) * cs + cb) * 2 + aoff[j] : G4_OOB;
@@ -405,6 +424,28 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
       } else {
         bf16_t* __restrict__ C = p.C + (long)b * p.batch_c;
         const bf16_t* __restrict__ R = p.residual ? p.residual + (long)b * p.batch_r : nullptr;
+        // output row of GEMM row m: itself, or (phase conv) its pixel on the upsampled grid.  The wave's 128 rows lie
+        // in one image and phase (H W % 256 == 0) and W is a power of two (host check), so a row costs shifts and
+        // adds only: a division per row bloats the unrolled epilogue until the accumulators leave registers.
+        const int mw = m0 + wm * 128;
+        long ob = 0;
+        int r2b = 0, lw = 0;
+        if constexpr (CONV == 3) {
+          const int hwl = p.H * p.Wd, ohw = p.OH * p.OW;
+          const int cn = mw / ohw, rem = mw - cn * ohw;
+          const int ph = rem / hwl;
+          r2b = rem - ph * hwl;
+          lw = __builtin_ctz((unsigned)p.Wd);
+          ob = (long)cn * ohw + (long)(ph >> 1) * p.OW + (ph & 1);
+        }
+        const auto orow = [&](int m) -> long {
+          if constexpr (CONV == 3) {
+            const int r2 = r2b + (m - mw);
+            return ob + (long)(r2 >> lw) * (2 * p.OW) + 2 * (r2 & (p.Wd - 1));
+          } else {
+            return m;
+          }
+        };
         if (p.row_mr != nullptr) {
           // LayerNorm folded in (host: batch 1, unsplit): acc <- rstd[m] * (acc - mean[m] * s[n]), i.e. the GEMM of
           // the normalised rows with the gain-folded W; the folded shift is in the bias
@@ -505,7 +546,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
 #pragma unroll
                 for (int ii = 0; ii < IG; ++ii) {
                   const int i = i0 + ii;
-                  bf16_t* crow = C + (long)(m0 + wm * 128 + i * 16 + fr) * p.ldc + n0 + wn * WC;
+                  bf16_t* crow = C + orow(m0 + wm * 128 + i * 16 + fr) * p.ldc + n0 + wn * WC;
                   // row statistics of this lane's columns, shifted by the row's first stored value in this
                   // slot (lane fq = 0, column 0): (mean, M2) per slot, combined exactly by the finalizer
                   float rs = 0.f, rq = 0.f, rk = 0.f;
@@ -709,7 +750,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
                   uint2_ o;
                   o[0] = pack2(v[0], v[1]);
                   o[1] = pack2(v[2], v[3]);
-                  *reinterpret_cast<uint2_*>(C + (long)m * p.ldc + n) = o;
+                  *reinterpret_cast<uint2_*>(C + orow(m) * p.ldc + n) = o;
                 }
               }
             }
@@ -754,7 +795,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
             const int n = n0 + wn * WC + g4_col<BN, WIDE>(j, fq);
             if (n >= p.N) continue;
             float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-            epilogue4<GLU, ACT>(p, C, R, m, n, v, b);
+            epilogue4<GLU, ACT>(p, CONV == 3 ? C + (orow(m) - m) * p.ldc : C, R, m, n, v, b);
           }
         }
       }
@@ -772,6 +813,12 @@ bool gemm4_supported(const GemmArgs& a) {
   if (a.conv) {
     if (a.Cin % 64 != 0) return false;
     if (a.A2 != nullptr && a.Cin1 % 64 != 0) return false;
+    if (a.upsample == 2) {  // phase conv: one image and phase per tile, output rows remapped (no residual / row stats)
+      if (a.KH != 2 || a.KW != 2 || a.OH != 2 * a.H || a.OW != 2 * a.Wd || (a.H * a.Wd) % G4_BM != 0) return false;
+      if ((a.Wd & (a.Wd - 1)) != 0) return false;  // epilogue row map by shifts
+      if (a.residual != nullptr || a.row_part != nullptr || a.row_mr != nullptr || a.gate != nullptr) return false;
+      if (a.batch > 1 || a.glu) return false;
+    }
   }
   return true;
 }
@@ -823,7 +870,7 @@ template <int VAR>
 static void g4_dispatch(const GemmArgs& a, float* ws, int splits, int kps, int bn, hipStream_t s);
 
 void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t s, bool persist) {
-  if (ws == nullptr) splits = 1;
+  if (ws == nullptr || a.upsample == 2) splits = 1;  // the split-K fold writes GEMM rows, not phase-conv pixels
   const long kt = (a.K + G4_BK - 1) / G4_BK;
   const int kps = (int)(((kt + splits - 1) / splits) * G4_BK);
   // wide epilogue (VAR bit 4) in production: +1-3 % on K >= 2048, +14-24 % on the K = 320 SD2.1 GEMMs
@@ -837,7 +884,10 @@ void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t 
 template <int VAR>
 static void g4_dispatch(const GemmArgs& a, float* ws, int splits, int kps, int bn, hipStream_t s) {
   if (a.conv) {
-    if (a.upsample) {
+    if (a.upsample == 2) {
+      if (a.act == ACT_SILU) g4_launch<3, false, ACT_SILU, VAR>(a, ws, splits, kps, bn, s);
+      else g4_launch<3, false, ACT_NONE, VAR>(a, ws, splits, kps, bn, s);
+    } else if (a.upsample) {
       if (a.act == ACT_SILU) g4_launch<2, false, ACT_SILU, VAR>(a, ws, splits, kps, bn, s);
       else g4_launch<2, false, ACT_NONE, VAR>(a, ws, splits, kps, bn, s);
     } else {

@@ -118,6 +118,21 @@ class Conv2d(nn.Module):
             state_dict[k] = self.pack(state_dict[k])
         super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
 
+    def _phase_weight(self) -> torch.Tensor:
+        """Phase weights of the upsample conv (ops.pack_up2_phase_weight), rebuilt when the weight changes."""
+        try:
+            ver = self.weight._version
+        except RuntimeError:  # inference tensors carry no version counter (weights frozen for serving)
+            ver = -1
+        key = (self.weight.data_ptr(), ver)
+        cached = getattr(self, "_w_up2", None)
+        if cached is None or cached[0] != key:
+            if torch.cuda.is_current_stream_capturing():  # never first-built inside a graph capture: plain path
+                return None
+            cached = (key, ops.pack_up2_phase_weight(self.weight.data, self.cin_p))
+            self._w_up2 = cached
+        return cached[1]
+
     def _pad_in(self, x):
         if x.shape[-1] != self.cin_p:
             x = torch.nn.functional.pad(x, (0, self.cin_p - x.shape[-1]))
@@ -129,6 +144,10 @@ class Conv2d(nn.Module):
         if x2 is None:
             x = self._pad_in(x)
         extra = {} if stats is None else {"stats": stats, "eps": eps}
+        if upsample and ops.up2_phases_ok(x, self.k, self.k, self.stride, self.padding, x2, norm, residual, self.cout):
+            w_up2 = self._phase_weight()
+            if w_up2 is not None:
+                extra["w_up2"] = w_up2
         return ops.conv2d(x, self.weight, self.bias, self.k, self.k, self.stride, self.padding, upsample=upsample,
                           x2=x2, norm=norm, temb=temb, residual=residual, act=act, **extra)
 

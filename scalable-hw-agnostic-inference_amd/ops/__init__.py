@@ -19,12 +19,12 @@ import torch
 from .. import native
 from . import reference as ref
 from .reference import (ACT_GELU, ACT_GELU_TANH, ACT_NONE, ACT_QUICK_GELU, ACT_RELU, ACT_SILU, act_id,
-                        pack_conv_weight, unpack_conv_weight)
+                        pack_conv_weight, pack_up2_phase_weight, unpack_conv_weight)
 
 __all__ = [
     "rmsnorm", "layernorm", "groupnorm_stats", "groupnorm_apply", "groupnorm", "linear", "conv2d", "attention",
     "paged_attention", "decode_attention", "kv_write", "rope", "rope_pairs", "gated_act", "bias_act", "sched_step",
-    "softmax_", "embedding", "token_feedback", "decode_attention_rope", "decode_attention_rope_qkv", "gemm_partials", "quantize_fp8_rows", "dequant_fp8", "quant_rows_fp8", "gemm_f8", "pack_conv_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
+    "softmax_", "embedding", "token_feedback", "decode_attention_rope", "decode_attention_rope_qkv", "gemm_partials", "quantize_fp8_rows", "dequant_fp8", "quant_rows_fp8", "gemm_f8", "pack_conv_weight", "pack_up2_phase_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
     "ACT_GELU_TANH", "ACT_QUICK_GELU", "ACT_RELU", "decode_splits", "set_decode_wb",
 ]
 
@@ -427,17 +427,36 @@ def set_halo_conv(mode: int = -1, waves: int = -1) -> int:
     return int(_K().set_halo_conv(int(mode), int(waves)))
 
 
+# upsample + 3x3 conv as 4 output-phase 2x2 convs over the source (2.25x fewer MACs; SHAI_UP2_PHASES=0: off)
+UP2_PHASES = os.environ.get("SHAI_UP2_PHASES", "1") != "0"
+
+
+def up2_phases_ok(x: torch.Tensor, kh: int, kw: int, stride: int, pad: int, x2=None, norm=None, residual=None,
+                  cout: int = 0) -> bool:
+    """Whether an upsample conv of this shape runs phase-decomposed (v4 kernel CONV 3): plain 3x3 pad-1 conv, 64-channel
+    multiples, H W % 256 == 0 (one image and phase per 256-row tile), W a power of two, and (cout given) at least 256
+    output tiles: the phase conv runs unsplit, so a small problem (SD2.1 at batch 1) keeps the 9-tap conv, whose
+    split-K fills the chip (measured: b32 +3.2 % img/s, b1 p50 +1.3 % slower with every shape phased)."""
+    N, H, W, C = x.shape
+    if cout and (4 * N * H * W // 256) * ((cout + 255) // 256) < 256:
+        return False
+    return (UP2_PHASES and x.is_cuda and kh == 3 and kw == 3 and stride == 1 and pad == 1 and x2 is None and norm is None
+            and residual is None and C % 64 == 0 and (H * W) % 256 == 0 and (W & (W - 1)) == 0)
+
+
 def conv2d(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], kh: int, kw: int, stride: int = 1,
            pad: int = 0, upsample: bool = False, x2: Optional[torch.Tensor] = None, norm=None,
            temb: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None, act=None,
-           res_alpha: float = 1.0, stats: Optional[str] = None, eps: float = 1e-5):
+           res_alpha: float = 1.0, stats: Optional[str] = None, eps: float = 1e-5,
+           w_up2: Optional[torch.Tensor] = None):
     """NHWC implicit-GEMM convolution with fused prologue/epilogue.
 
     norm = (scale [N,Cin] f32, shift [N,Cin] f32, act) applies GroupNorm(+act) to
     the input: on the GPU one vectorised apply pass + the tuned conv inside the op (``set_halo_conv(1)``: the
     halo-tiled conv normalises each staged element once in LDS instead -- measured slower at the SD2.1 shapes);
     x2 is concatenated on channels; upsample reads a
-    nearest-2x view; temb [N, Cout] is a per-image bias; residual is added last.
+    nearest-2x view; temb [N, Cout] is a per-image bias; residual is added last.  w_up2: the phase weights
+    (``pack_up2_phase_weight``) of an upsample conv -- used when ``up2_phases_ok``.
     stats="gn" / "ln": also return statistics of the output for the next norm, as ``linear_stats`` -- (out, st);
     st is None when the output shape cannot carry them (``stats_supported``).
     """
@@ -463,8 +482,12 @@ def conv2d(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor]
         want = stats
     gp = torch.empty(M // 128, cout, 2, dtype=torch.float32, device=x.device) if want == "gn" else None
     ls = torch.empty(M, 2, dtype=torch.float32, device=x.device) if want == "ln" else None
-    _K().conv2d(x, x2, w_packed, out, bias, temb, residual, sc, sh, act_id(nact), kh, kw, stride, pad, bool(upsample),
-                act_id(act), float(res_alpha), None, None, gp, ls, float(eps))
+    if upsample and w_up2 is not None and up2_phases_ok(x, kh, kw, stride, pad, x2, norm, residual):
+        _K().conv2d(x, None, w_up2, out, bias, temb, None, None, None, 0, 2, 2, 1, 0, True, act_id(act), 1.0, None,
+                    None, gp, ls, float(eps), True)
+    else:
+        _K().conv2d(x, x2, w_packed, out, bias, temb, residual, sc, sh, act_id(nact), kh, kw, stride, pad,
+                    bool(upsample), act_id(act), float(res_alpha), None, None, gp, ls, float(eps))
     if stats is None:
         return out
     return out, (gp if want == "gn" else ls)

@@ -199,6 +199,50 @@ def pack_conv_weight(w):
     return w.permute(0, 2, 3, 1).reshape(cout, -1).contiguous()
 
 
+# taps of a 3x3 kernel that land on source row (column) i - 1 + p + a of output phase p of a nearest-2x upsample:
+# phase 0 (even output rows 2i) reads rows i - 1 (kh 0) and i (kh 1, 2); phase 1 reads i (kh 0, 1) and i + 1 (kh 2)
+_UP2_TAPS = (((0,), (1, 2)), ((0, 1), (2,)))
+
+
+def pack_up2_phase_weight(w_packed, cin):
+    """Packed 3x3 weight [Cout, 9 Cin] of a conv over a nearest-2x upsampled input -> the 4 output phases' 2x2
+    weights [4 Cout, 4 Cin] (phase py * 2 + px, k ordered (a, b, c)): W_ph[a][b] = sum of the 3x3 taps that read the
+    same source pixel, accumulated in fp32 (csrc/kernels/gemm_8ph.hip CONV 3)."""
+    cout = w_packed.shape[0]
+    w = w_packed.float().reshape(cout, 3, 3, cin)
+    out = w.new_zeros(2, 2, cout, 2, 2, cin)
+    for py in range(2):
+        for px in range(2):
+            for a in range(2):
+                for b in range(2):
+                    for kh in _UP2_TAPS[py][a]:
+                        for kw in _UP2_TAPS[px][b]:
+                            out[py, px, :, a, b] += w[:, kh, kw]
+    return out.reshape(4 * cout, 4 * cin).to(w_packed.dtype)
+
+
+def conv2d_up2_phases(x, w_phase, bias=None, temb=None, act=None):
+    """Reference of the phase-decomposed upsample conv: out[n, 2i + py, 2j + px] = sum_{a, b} x[n, i - 1 + py + a,
+    j - 1 + px + b] W_ph (zero outside the source)."""
+    N, H, W, C = x.shape
+    cout = w_phase.shape[0] // 4
+    xp = F.pad(x.float(), (0, 0, 1, 1, 1, 1))
+    wp = w_phase.float().reshape(2, 2, cout, 2, 2, C)
+    y = x.new_zeros(N, 2 * H, 2 * W, cout, dtype=torch.float32)
+    for py in range(2):
+        for px in range(2):
+            acc = 0
+            for a in range(2):
+                for b in range(2):
+                    acc = acc + xp[:, py + a:py + a + H, px + b:px + b + W] @ wp[py, px, :, a, b].t()
+            y[:, py::2, px::2] = acc
+    if bias is not None:
+        y = y + bias.float()
+    if temb is not None:
+        y = y + temb.float()[:, None, None, :]
+    return apply_act(y, act).to(x.dtype)
+
+
 def conv2d(x, w_packed, bias, kh, kw, stride=1, pad=0, upsample=False, x2=None, norm=None, temb=None,
            residual=None, act=None, res_alpha=1.0):
     """x NHWC [N,H,W,C1] (+x2 [N,H,W,C2] concatenated on C) -> NHWC output."""

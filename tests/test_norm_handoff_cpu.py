@@ -91,3 +91,19 @@ def test_vit_norm_handoff_cpu():
     finally:
         vit.NORM_HANDOFF, ops.FOLD_MIN_TILES = old, old_min
     assert rel(y1, y0) < 1e-2
+
+
+def test_up2_phase_weights_match_upsample_conv():
+    """Upsample + 3x3 conv == 4 output-phase 2x2 convs over the source with summed weights (gemm_8ph.hip CONV 3)."""
+    torch.manual_seed(3)
+    for n, h, w, c, co in [(2, 4, 5, 8, 16), (1, 3, 3, 16, 8), (1, 1, 2, 8, 8)]:
+        x = torch.randn(n, h, w, c)
+        wp = ref.pack_conv_weight(torch.randn(co, c, 3, 3))
+        b, temb = torch.randn(co), torch.randn(n, co)
+        y0 = ref.conv2d(x, wp, b, 3, 3, 1, 1, True, temb=temb, act="silu")
+        y1 = ref.conv2d_up2_phases(x, ops.pack_up2_phase_weight(wp, c), b, temb=temb, act="silu")
+        assert y1.shape == (n, 2 * h, 2 * w, co)
+        torch.testing.assert_close(y1, y0, atol=1e-4, rtol=1e-4)
+    # bf16 packing: the fp32 sums round once
+    wb = ref.pack_conv_weight(torch.randn(8, 8, 3, 3)).to(torch.bfloat16)
+    assert ops.pack_up2_phase_weight(wb, 8).dtype == torch.bfloat16

@@ -244,7 +244,10 @@ def bench_dattn(rows):
     split count and context length; KV bytes read / time."""
     import math
     h, hk, D = 32, 8, 128
-    for B, ctx in [(64, 192), (64, 1024), (16, 4096), (1, 16384)]:
+    shapes = [(64, 192), (64, 1024), (16, 4096), (1, 16384)]
+    if os.environ.get("SHAI_DATTN_SHAPES"):  # e.g. "64x2,64x64,64x192": batch x context
+        shapes = [tuple(int(v) for v in t.split("x")) for t in os.environ["SHAI_DATTN_SHAPES"].split(",")]
+    for B, ctx in shapes:
         nblk = (ctx + 63) // 64
         pool = B * nblk + 8
         kc = rnd(pool, hk, 64, D)
