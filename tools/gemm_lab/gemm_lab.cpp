@@ -181,12 +181,20 @@ int main(int argc, char** argv) {
       conv("unet64_640to320", 64, 64, 640, 320, 3),
       conv("unet_up32_1280", 64, 16, 1280, 1280, 3, 1),
       conv("vae256_256", 4, 256, 256, 256, 3),
+      gemm("sd_geglu32_plain", 65536, 5120, 640),
+      gemm("sd_geglu16_plain", 16384, 10240, 1280),
   };
   if (quick) probs.resize(3);
   if (argc > 1 && !strcmp(argv[1], "--ws")) {  // the low-K problems of the W-stationary kernel only
     std::vector<Problem> q;
     for (auto& P : probs)
       if (!P.conv && P.K == 320) q.push_back(P);
+    probs = q;
+  }
+  if (argc > 1 && !strcmp(argv[1], "--glu")) {  // GEGLU problems beside the plain GEMM of the same shape
+    std::vector<Problem> q;
+    for (auto& P : probs)
+      if (!P.conv && !P.lnf && P.name.rfind("sd_geglu", 0) == 0) q.push_back(P);
     probs = q;
   }
   if (plain_only) {
