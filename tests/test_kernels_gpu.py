@@ -617,3 +617,24 @@ def test_decode_attn_wave_per_block_matches_split_kernel(cuda, fused):
         close(outs[0][:-1], want.reshape(B, Hq * D)[:-1], 2e-2)
     finally:
         ops.set_decode_wb(prev)
+
+
+def test_upsample2d_layer_takes_phase_conv_and_tracks_weight_updates(cuda):
+    """Upsample2D (UNet / VAE) on a shape with >= 256 output tiles runs the phase conv with cached phase weights,
+    matches the fp32 upsample + 3x3 conv, and rebuilds the phase weights after an in-place weight update."""
+    from shai_amd.models.unet2d import Upsample2D
+    torch.manual_seed(23)
+    C = 64
+    up = Upsample2D(C).to("cuda")
+    with torch.no_grad():
+        up.conv.weight.copy_(ops.pack_conv_weight(rnd(C, C, 3, 3, scale=1 / math.sqrt(C * 9))))
+        up.conv.bias.copy_(rnd(C))
+    x = rnd(16, 32, 32, C)
+    assert ops.up2_phases_ok(x, 3, 3, 1, 1, cout=C)
+    y = up(x)
+    assert getattr(up.conv, "_w_up2", None) is not None, "phase conv not taken"
+    close(y, ref.conv2d(x, up.conv.weight, up.conv.bias, 3, 3, 1, 1, upsample=True), 3e-2)
+    with torch.no_grad():
+        up.conv.weight.mul_(-0.5)
+    y2 = up(x)
+    close(y2, ref.conv2d(x, up.conv.weight, up.conv.bias, 3, 3, 1, 1, upsample=True), 3e-2)
