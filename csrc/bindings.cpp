@@ -165,7 +165,6 @@ bool lib_enabled() {  // off by default: every GEMM runs on the hand-written ker
 int max_splits_for(const shai::GemmArgs& g) {
   const int batch = g.batch > 0 ? g.batch : 1;
   if (batch != 1 || g.row_mr != nullptr) return 1;  // folded LayerNorm: applied by the unsplit v4 epilogue only
-  if (g.upsample == 2) return 1;                      // phase conv: the split-K fold would write GEMM rows
   const long kt = (g.K + 63) / 64;
   int s = 1;
   while (s < 16 && kt / (s * 2) >= 4) s *= 2;
@@ -446,8 +445,13 @@ void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_
     }
     return;
   }
+  static const int forced_splits = [] {  // with SHAI_GEMM_FORCE: split-K count (clamped to the problem's maximum)
+    const char* e = getenv("SHAI_GEMM_FORCE_SPLITS");
+    return e ? std::max(1, atoi(e)) : 1;
+  }();
   if (forced >= 0 && forced < shai::gemm2_num_cfgs() && shai::gemm2_cfg_supported(g, forced)) {
-    launch_final(g, like, Choice{forced, 1}, st);
+    const int sp = shai::gemm2_cfg_splittable(forced) ? std::min(forced_splits, max_splits_for(g)) : 1;
+    launch_final(g, like, Choice{forced, sp}, st);
     return;
   }
   const std::string key = gemm_key(g);

@@ -870,7 +870,7 @@ template <int VAR>
 static void g4_dispatch(const GemmArgs& a, float* ws, int splits, int kps, int bn, hipStream_t s);
 
 void launch_gemm4(const GemmArgs& a, float* ws, int splits, int bn, hipStream_t s, bool persist) {
-  if (ws == nullptr || a.upsample == 2) splits = 1;  // the split-K fold writes GEMM rows, not phase-conv pixels
+  if (ws == nullptr) splits = 1;  // (phase conv: the fold maps GEMM rows to output pixels, up2_out_row)
   const long kt = (a.K + G4_BK - 1) / G4_BK;
   const int kps = (int)(((kt + splits - 1) / splits) * G4_BK);
   // wide epilogue (VAR bit 4) in production: +1-3 % on K >= 2048, +14-24 % on the K = 320 SD2.1 GEMMs

@@ -5,6 +5,16 @@
 
 namespace shai {
 
+// Phase-decomposed upsample conv (GemmArgs::upsample == 2, gemm_8ph.hip CONV 3): the output pixel row of GEMM row m
+// (rows ordered image, phase, i, j over the low-resolution grid) -- the split-K fold's row map.
+__device__ __forceinline__ long up2_out_row(const GemmArgs& p, int m) {
+  const int hwl = p.H * p.Wd, ohw = p.OH * p.OW;
+  const int cn = m / ohw, rem = m - cn * ohw;
+  const int ph = rem / hwl, r2 = rem - ph * hwl;
+  const int si = r2 / p.Wd, sj = r2 - si * p.Wd;
+  return (long)cn * ohw + (long)(2 * si + (ph >> 1)) * p.OW + 2 * sj + (ph & 1);
+}
+
 // Apply the epilogue to 4 consecutive columns n..n+3 of row m and store.
 template <bool GLU, int ACT>
 __device__ __forceinline__ void epilogue4(const GemmArgs& p, bf16_t* C, const bf16_t* R, int m, int n, float v[4],

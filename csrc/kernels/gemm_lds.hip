@@ -437,7 +437,9 @@ __global__ void gemm_splitk_reduce(const GemmArgs p, const float* __restrict__ w
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] *= r;
     }
-    epilogue4<GLU, ACT>(p, p.C, p.residual, m, n, v);
+    // phase conv: row m's output pixel (no residual on that path)
+    bf16_t* C = p.upsample == 2 ? p.C + (up2_out_row(p, m) - m) * p.ldc : p.C;
+    epilogue4<GLU, ACT>(p, C, p.residual, m, n, v);
   }
 }
 

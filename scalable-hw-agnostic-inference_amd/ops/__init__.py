@@ -429,6 +429,8 @@ def set_halo_conv(mode: int = -1, waves: int = -1) -> int:
 
 # upsample + 3x3 conv as 4 output-phase 2x2 convs over the source (2.25x fewer MACs; SHAI_UP2_PHASES=0: off)
 UP2_PHASES = os.environ.get("SHAI_UP2_PHASES", "1") != "0"
+# models keep the 9-tap conv below this many 256 x 256 output tiles (``up2_phases_ok(..., cout=)``)
+UP2_MIN_TILES = int(os.environ.get("SHAI_UP2_MIN_TILES", "256"))
 
 
 def up2_phases_ok(x: torch.Tensor, kh: int, kw: int, stride: int, pad: int, x2=None, norm=None, residual=None,
@@ -438,7 +440,7 @@ def up2_phases_ok(x: torch.Tensor, kh: int, kw: int, stride: int, pad: int, x2=N
     output tiles: the phase conv runs unsplit, so a small problem (SD2.1 at batch 1) keeps the 9-tap conv, whose
     split-K fills the chip (measured: b32 +3.2 % img/s, b1 p50 +1.3 % slower with every shape phased)."""
     N, H, W, C = x.shape
-    if cout and (4 * N * H * W // 256) * ((cout + 255) // 256) < 256:
+    if cout and (4 * N * H * W // 256) * ((cout + 255) // 256) < UP2_MIN_TILES:
         return False
     return (UP2_PHASES and x.is_cuda and kh == 3 and kw == 3 and stride == 1 and pad == 1 and x2 is None and norm is None
             and residual is None and C % 64 == 0 and (H * W) % 256 == 0 and (W & (W - 1)) == 0)

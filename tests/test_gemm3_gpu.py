@@ -101,6 +101,39 @@ def test_gemm3_conv_forced(cuda, cfg):
 
 W4 = 13
 
+UP2_SCRIPT = r"""
+import math, sys, torch
+sys.path.insert(0, {root!r})
+import shai_amd.ops as ops
+from shai_amd.ops import reference as ref
+torch.manual_seed(5)
+worst = 0.0
+for (N, H, W, C, Co, act) in [(2, 16, 16, 1280, 1280, "silu"), (1, 32, 32, 640, 640, None), (4, 16, 32, 256, 512, None)]:
+    x = torch.randn(N, H, W, C, device="cuda").bfloat16()
+    w = ops.pack_conv_weight((torch.randn(Co, C, 3, 3, device="cuda") / math.sqrt(C * 9)).bfloat16())
+    b, temb = torch.randn(Co, device="cuda").bfloat16(), torch.randn(N, Co, device="cuda").bfloat16()
+    y, gp = ops.conv2d(x, w, b, 3, 3, 1, 1, upsample=True, temb=temb, act=act, stats="gn",
+                       w_up2=ops.pack_up2_phase_weight(w, C))
+    yr = ref.conv2d(x, w, b, 3, 3, 1, 1, upsample=True, temb=temb, act=act)
+    rel = ((y.float() - yr.float()).norm() / yr.float().norm()).item()
+    worst = max(worst, rel)
+    want = ref.col_partials(y.reshape(-1, Co)).reshape(N, -1, Co, 2).sum(1)
+    torch.testing.assert_close(gp.reshape(N, -1, Co, 2).sum(1), want, atol=2e-1, rtol=1e-3)
+print("WORST", worst)
+assert worst < 1e-2, worst
+"""
+
+
+@pytest.mark.parametrize("cfg,splits", [(9, 1), (10, 1), (9, 3), (10, 4), (11, 1), (12, 2)])
+def test_up2_phase_conv_forced(cuda, cfg, splits):
+    """Phase-decomposed upsample conv on each v4 config, unsplit and split-K (the fold maps GEMM rows to output
+    pixels), with per-image bias, SiLU and the output's GroupNorm partials (own process: SHAI_GEMM_FORCE /
+    SHAI_GEMM_FORCE_SPLITS are read once per process)."""
+    code = UP2_SCRIPT.format(root=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, SHAI_GEMM_FORCE=str(cfg), SHAI_GEMM_FORCE_SPLITS=str(splits))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+
 
 @pytest.mark.parametrize("act", ["gelu", "silu", "gelu_tanh"])
 def test_w4_glu_acts_ragged(cuda, act):
