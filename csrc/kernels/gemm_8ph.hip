@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
       const int r = wid * (BN / 8) + j * 8 + lrow;  // LDS row
       const int n = n0 + (WIDE ? g4_wperm<BN>(r) : r);
       // phase conv: the tile's phase selects its weight slice (rows ph N .. ph N + N - 1)
-      const long wrow = CONV == 3 ? (long)((m0 % (p.OH * p.OW)) / (p.H * p.Wd)) * p.N + n : (long)n;
+      const long wrow = CONV == 3 ? (long)up2_row(p, m0).ph * p.N + n : (long)n;
       woff[j] = n < p.N ? (uint32_t)((wrow * p.ldw + kchw[j]) * 2) : G4_OOB;
     }
 #pragma unroll
@@ -206,13 +206,12 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
         const int rem = mm - cn * hw;
         const int coh = rem / p.OW, cow = rem - coh * p.OW;
         if constexpr (CONV == 3) {
-          // row (image cn, phase ph, i, j): 2 x 2 taps from source row i - 1 + py, column j - 1 + px
-          const int hwl = p.H * p.Wd;
-          const int ph = rem / hwl, r2 = rem - ph * hwl;
-          const int si = r2 / p.Wd, sj = r2 - si * p.Wd;
-          ih0[j] = m < p.M ? si - 1 + (ph >> 1) : -(1 << 24);
-          iw0[j] = sj - 1 + (ph & 1);
-          pix[j] = (cn * p.H + ih0[j]) * p.Wd + iw0[j];
+          // row (image, phase, i, j): 2 x 2 taps from source row i - 1 + py, column j - 1 + px
+          const Up2Row q = up2_row(p, mm);
+          ih0[j] = m < p.M ? q.si - 1 + (q.ph >> 1) : -(1 << 24);
+          iw0[j] = q.sj - 1 + (q.ph & 1);
+          pix[j] = (q.img * p.H + ih0[j]) * p.Wd + iw0[j];
+          (void)cn;
           (void)coh;
           (void)cow;
         } else if constexpr (CONV == 1) {
@@ -424,27 +423,11 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
       } else {
         bf16_t* __restrict__ C = p.C + (long)b * p.batch_c;
         const bf16_t* __restrict__ R = p.residual ? p.residual + (long)b * p.batch_r : nullptr;
-        // output row of GEMM row m: itself, or (phase conv) its pixel on the upsampled grid.  The wave's 128 rows lie
-        // in one image and phase (H W % 256 == 0) and W is a power of two (host check), so a row costs shifts and
-        // adds only: a division per row bloats the unrolled epilogue until the accumulators leave registers.
-        const int mw = m0 + wm * 128;
-        long ob = 0;
-        int r2b = 0, lw = 0;
-        if constexpr (CONV == 3) {
-          const int hwl = p.H * p.Wd, ohw = p.OH * p.OW;
-          const int cn = mw / ohw, rem = mw - cn * ohw;
-          const int ph = rem / hwl;
-          r2b = rem - ph * hwl;
-          lw = __builtin_ctz((unsigned)p.Wd);
-          ob = (long)cn * ohw + (long)(ph >> 1) * p.OW + (ph & 1);
-        }
+        // output row of GEMM row m: itself, or (phase conv) its pixel on the upsampled grid -- shifts and masks only
+        // (up2_row): a division per row bloats the unrolled epilogue until the accumulators leave registers
         const auto orow = [&](int m) -> long {
-          if constexpr (CONV == 3) {
-            const int r2 = r2b + (m - mw);
-            return ob + (long)(r2 >> lw) * (2 * p.OW) + 2 * (r2 & (p.Wd - 1));
-          } else {
-            return m;
-          }
+          if constexpr (CONV == 3) return up2_out_row(p, m);
+          else return m;
         };
         if (p.row_mr != nullptr) {
           // LayerNorm folded in (host: batch 1, unsplit): acc <- rstd[m] * (acc - mean[m] * s[n]), i.e. the GEMM of
@@ -814,8 +797,10 @@ bool gemm4_supported(const GemmArgs& a) {
     if (a.Cin % 64 != 0) return false;
     if (a.A2 != nullptr && a.Cin1 % 64 != 0) return false;
     if (a.upsample == 2) {  // phase conv: one image and phase per tile, output rows remapped (no residual / row stats)
-      if (a.KH != 2 || a.KW != 2 || a.OH != 2 * a.H || a.OW != 2 * a.Wd || (a.H * a.Wd) % G4_BM != 0) return false;
-      if ((a.Wd & (a.Wd - 1)) != 0) return false;  // epilogue row map by shifts
+      if (a.KH != 2 || a.KW != 2 || a.OH != 2 * a.H || a.OW != 2 * a.Wd) return false;
+      if ((a.H & (a.H - 1)) != 0 || (a.Wd & (a.Wd - 1)) != 0) return false;  // rows map by shifts (up2_row)
+      const int hw = a.H * a.Wd;  // below 256: 256 / hw images per group (whole groups, no per-image bias)
+      if (hw < G4_BM && (a.Nimg % (G4_BM / hw) != 0 || a.bias2d != nullptr)) return false;
       if (a.residual != nullptr || a.row_part != nullptr || a.row_mr != nullptr || a.gate != nullptr) return false;
       if (a.batch > 1 || a.glu) return false;
     }
@@ -830,6 +815,9 @@ bool gemm4_stats_ok(const GemmArgs& a, int bn) {
   if (a.residual != nullptr && (a.ldr % 8 != 0 || !al16(a.residual))) return false;
   if (a.bias != nullptr && !al16(a.bias)) return false;
   if (a.bias2d != nullptr && (a.rows_per_bias2d % 128 != 0 || a.N % 8 != 0 || !al16(a.bias2d))) return false;
+  // phase conv over image groups (H W < 256): the GEMM's 128-row blocks interleave the group's images, and the partials'
+  // consumer maps block b to image b * 128 / (OH OW) -- statistics from a pass over the output instead
+  if (a.upsample == 2 && a.H * a.Wd < G4_BM) return false;
   return true;
 }
 

@@ -5,14 +5,28 @@
 
 namespace shai {
 
-// Phase-decomposed upsample conv (GemmArgs::upsample == 2, gemm_8ph.hip CONV 3): the output pixel row of GEMM row m
-// (rows ordered image, phase, i, j over the low-resolution grid) -- the split-K fold's row map.
+// Phase-decomposed upsample conv (GemmArgs::upsample == 2, gemm_8ph.hip CONV 3), row order: groups of
+// G = max(1, 256 / (H W)) images (H, W powers of two, host-checked); inside a group phase-major (ph = 2 py + px), then
+// image, then (i, j) of the low-resolution grid.  A 256-row tile so holds ONE phase (its weight slice); G = 1 is
+// image-major.  Shifts only: the epilogue evaluates this per stored row.
+struct Up2Row {
+  int img, ph, si, sj;
+};
+__device__ __forceinline__ Up2Row up2_row(const GemmArgs& p, int m) {
+  const int lw = __builtin_ctz((unsigned)p.Wd), lhw = lw + __builtin_ctz((unsigned)p.H);
+  const int lb = lhw >= 8 ? lhw : 8;  // log2 of one (group, phase) block's rows, G H W
+  const int r = m & ((1 << lb) - 1), r2 = r & ((1 << lhw) - 1);
+  Up2Row q;
+  q.ph = (m >> lb) & 3;
+  q.img = ((m >> (lb + 2)) << (lb - lhw)) + (r >> lhw);
+  q.si = r2 >> lw;
+  q.sj = r2 & (p.Wd - 1);
+  return q;
+}
+// the output pixel row of GEMM row m (epilogue and split-K fold)
 __device__ __forceinline__ long up2_out_row(const GemmArgs& p, int m) {
-  const int hwl = p.H * p.Wd, ohw = p.OH * p.OW;
-  const int cn = m / ohw, rem = m - cn * ohw;
-  const int ph = rem / hwl, r2 = rem - ph * hwl;
-  const int si = r2 / p.Wd, sj = r2 - si * p.Wd;
-  return (long)cn * ohw + (long)(2 * si + (ph >> 1)) * p.OW + 2 * sj + (ph & 1);
+  const Up2Row q = up2_row(p, m);
+  return ((long)q.img * p.OH + 2 * q.si + (q.ph >> 1)) * p.OW + 2 * q.sj + (q.ph & 1);
 }
 
 // Apply the epilogue to 4 consecutive columns n..n+3 of row m and store.

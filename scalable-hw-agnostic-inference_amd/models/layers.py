@@ -144,7 +144,8 @@ class Conv2d(nn.Module):
         if x2 is None:
             x = self._pad_in(x)
         extra = {} if stats is None else {"stats": stats, "eps": eps}
-        if upsample and ops.up2_phases_ok(x, self.k, self.k, self.stride, self.padding, x2, norm, residual, self.cout):
+        if upsample and ops.up2_phases_ok(x, self.k, self.k, self.stride, self.padding, x2, norm, residual, self.cout,
+                                          temb):
             w_up2 = self._phase_weight()
             if w_up2 is not None:
                 extra["w_up2"] = w_up2

@@ -434,16 +434,20 @@ UP2_MIN_TILES = int(os.environ.get("SHAI_UP2_MIN_TILES", "256"))
 
 
 def up2_phases_ok(x: torch.Tensor, kh: int, kw: int, stride: int, pad: int, x2=None, norm=None, residual=None,
-                  cout: int = 0) -> bool:
+                  cout: int = 0, temb=None) -> bool:
     """Whether an upsample conv of this shape runs phase-decomposed (v4 kernel CONV 3): plain 3x3 pad-1 conv, 64-channel
-    multiples, H W % 256 == 0 (one image and phase per 256-row tile), W a power of two, and (cout given) at least 256
-    output tiles: the phase conv runs unsplit, so a small problem (SD2.1 at batch 1) keeps the 9-tap conv, whose
-    split-K fills the chip (measured: b32 +3.2 % img/s, b1 p50 +1.3 % slower with every shape phased)."""
+    multiples, H and W powers of two; below H W = 256 the rows run over groups of 256 / (H W) images (N a multiple,
+    no per-image bias), so a 256-row tile still holds one phase.  With cout given, at least 256 output tiles: a small
+    problem (SD2.1 at batch 1) stays on the 9-tap conv (measured: b32 +3.2 % img/s; b1 p50 1-1.3 % slower with every
+    shape phased, split-K or not)."""
     N, H, W, C = x.shape
     if cout and (4 * N * H * W // 256) * ((cout + 255) // 256) < UP2_MIN_TILES:
         return False
+    pow2 = (H & (H - 1)) == 0 and (W & (W - 1)) == 0
+    grouped = H * W < 256
     return (UP2_PHASES and x.is_cuda and kh == 3 and kw == 3 and stride == 1 and pad == 1 and x2 is None and norm is None
-            and residual is None and C % 64 == 0 and (H * W) % 256 == 0 and (W & (W - 1)) == 0)
+            and residual is None and C % 64 == 0 and pow2
+            and (not grouped or (N % (256 // (H * W)) == 0 and temb is None)))
 
 
 def conv2d(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor], kh: int, kw: int, stride: int = 1,
@@ -484,7 +488,7 @@ def conv2d(x: torch.Tensor, w_packed: torch.Tensor, bias: Optional[torch.Tensor]
         want = stats
     gp = torch.empty(M // 128, cout, 2, dtype=torch.float32, device=x.device) if want == "gn" else None
     ls = torch.empty(M, 2, dtype=torch.float32, device=x.device) if want == "ln" else None
-    if upsample and w_up2 is not None and up2_phases_ok(x, kh, kw, stride, pad, x2, norm, residual):
+    if upsample and w_up2 is not None and up2_phases_ok(x, kh, kw, stride, pad, x2, norm, residual, temb=temb):
         _K().conv2d(x, None, w_up2, out, bias, temb, None, None, None, 0, 2, 2, 1, 0, True, act_id(act), 1.0, None,
                     None, gp, ls, float(eps), True)
     else:

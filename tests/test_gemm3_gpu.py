@@ -108,10 +108,14 @@ import shai_amd.ops as ops
 from shai_amd.ops import reference as ref
 torch.manual_seed(5)
 worst = 0.0
-for (N, H, W, C, Co, act) in [(2, 16, 16, 1280, 1280, "silu"), (1, 32, 32, 640, 640, None), (4, 16, 32, 256, 512, None)]:
+for (N, H, W, C, Co, act) in [(2, 16, 16, 1280, 1280, "silu"), (1, 32, 32, 640, 640, None), (4, 16, 32, 256, 512, None),
+                              (8, 8, 8, 1280, 1280, None), (6, 8, 16, 256, 320, "silu")]:
     x = torch.randn(N, H, W, C, device="cuda").bfloat16()
     w = ops.pack_conv_weight((torch.randn(Co, C, 3, 3, device="cuda") / math.sqrt(C * 9)).bfloat16())
-    b, temb = torch.randn(Co, device="cuda").bfloat16(), torch.randn(N, Co, device="cuda").bfloat16()
+    b = torch.randn(Co, device="cuda").bfloat16()
+    # image groups (H W < 256) take no per-image bias
+    temb = torch.randn(N, Co, device="cuda").bfloat16() if H * W >= 256 else None
+    assert ops.up2_phases_ok(x, 3, 3, 1, 1, temb=temb)
     y, gp = ops.conv2d(x, w, b, 3, 3, 1, 1, upsample=True, temb=temb, act=act, stats="gn",
                        w_up2=ops.pack_up2_phase_weight(w, C))
     yr = ref.conv2d(x, w, b, 3, 3, 1, 1, upsample=True, temb=temb, act=act)

@@ -179,15 +179,17 @@ def test_conv2d_fused(cuda):
 
 
 @pytest.mark.parametrize("N,H,W,C,Co,act", [(2, 16, 16, 1280, 1280, None), (3, 32, 32, 640, 640, "silu"),
-                                            (1, 16, 32, 320, 320, None), (2, 32, 16, 128, 512, None)])
+                                            (1, 16, 32, 320, 320, None), (2, 32, 16, 128, 512, None),
+                                            (8, 8, 8, 640, 640, "silu"), (4, 8, 16, 128, 256, None)])
 def test_conv2d_upsample_phases(cuda, N, H, W, C, Co, act):
     """Phase-decomposed upsample conv (v4 CONV 3, 2x2 phase weights over the source) vs the fp32 upsample + 3x3
     conv, incl. the per-image bias, activation and the output's GroupNorm partials (per-image sums)."""
     torch.manual_seed(17)
     x = rnd(N, H, W, C)
     w = ops.pack_conv_weight(rnd(Co, C, 3, 3, scale=1 / math.sqrt(C * 9)))
-    b, temb = rnd(Co), rnd(N, Co)
-    assert ops.up2_phases_ok(x, 3, 3, 1, 1)
+    b = rnd(Co)
+    temb = rnd(N, Co) if H * W >= 256 else None  # image groups (H W < 256) take no per-image bias
+    assert ops.up2_phases_ok(x, 3, 3, 1, 1, temb=temb)
     assert not ops.up2_phases_ok(x, 3, 3, 1, 1, cout=Co)  # too small to leave the split-K 9-tap conv in a model
     wph = ops.pack_up2_phase_weight(w, C)
     y, gp = ops.conv2d(x, w, b, 3, 3, 1, 1, upsample=True, temb=temb, act=act, stats="gn", w_up2=wph)
