@@ -70,6 +70,10 @@ def main():
     else:
         n = tp.follow(target, ch, leader_timeout_s=0)
         print(f"follower survived {n}", flush=True)
+    if case in ("mirrored", "subclass"):
+        # both ranks survive: neither tears its gloo connections down while the other still uses them (the leader
+        # leaving right after STOP aborted a loaded follower's exchange)
+        dist.barrier()
 
 
 if __name__ == "__main__":
