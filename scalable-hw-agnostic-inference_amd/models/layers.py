@@ -50,10 +50,14 @@ class Linear(nn.Module):
         return _folded(self, ln)
 
 
+def _wkey(t):
+    """Cache key of a derived weight: storage identity and version (inference-mode tensors carry no version counter:
+    their storage identity is the key)."""
+    return (t.data_ptr(), 0 if t.is_inference() else t._version) if t is not None else None
+
+
 def _folded(lin, ln):
-    # (inference-mode tensors carry no version counter: their storage identity is the key)
-    key = tuple((t.data_ptr(), 0 if t.is_inference() else t._version) if t is not None else None
-                for t in (lin.weight, lin.bias, ln.weight, ln.bias))
+    key = tuple(_wkey(t) for t in (lin.weight, lin.bias, ln.weight, ln.bias))
     cache = getattr(lin, "_ln_fold", None)
     if cache is None or cache[0] != key:
         cache = (key, ops.fold_layernorm(lin.weight, lin.bias, ln.weight, ln.bias))
@@ -120,11 +124,7 @@ class Conv2d(nn.Module):
 
     def _phase_weight(self) -> torch.Tensor:
         """Phase weights of the upsample conv (ops.pack_up2_phase_weight), rebuilt when the weight changes."""
-        try:
-            ver = self.weight._version
-        except RuntimeError:  # inference tensors carry no version counter (weights frozen for serving)
-            ver = -1
-        key = (self.weight.data_ptr(), ver)
+        key = _wkey(self.weight)
         cached = getattr(self, "_w_up2", None)
         if cached is None or cached[0] != key:
             if torch.cuda.is_current_stream_capturing():  # never first-built inside a graph capture: plain path

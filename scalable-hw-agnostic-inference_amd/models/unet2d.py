@@ -28,7 +28,10 @@ import torch.nn as nn
 
 from .. import ops
 from .attention import CrossAttention, FusedSelfAttention, merge_linear_keys
-from .layers import Conv2d, GLULinear, GroupNorm, LayerNorm, Linear, timestep_embedding
+from .layers import Conv2d, GLULinear, GroupNorm, LayerNorm, Linear, _wkey, timestep_embedding
+
+# the last transformer block's FF down projection merged into proj_out (Transformer2DModel._merged_out)
+MERGE_PROJ_OUT = os.environ.get("SHAI_MERGE_PROJ_OUT", "1") != "0"
 
 # GroupNorm partials / LayerNorm moments handed from the producing GEMM epilogue to the next norm (and LayerNorms
 # folded into their consumer projections); SHAI_NORM_HANDOFF=0 restores the standalone norm passes (A/B)
@@ -137,11 +140,13 @@ class BasicTransformerBlock(nn.Module):
         x = self.attn2(self.norm2(x), ctx_kv, residual=x)
         return self.ff(self.norm3(x), residual=x)
 
-    def forward_folded(self, x, ctx_kv, mr, next_eps=None):
+    def forward_folded(self, x, ctx_kv, mr, next_eps=None, defer_down: bool = False):
         """forward with every LayerNorm folded into the projection that consumes it: ``mr`` = (mean, rstd) [rows, 2]
         of x from its producer; each residual GEMM (attention out-projections, FF down) hands the next norm's
         (mean, rstd) over from its epilogue, so no normalised activation is ever written.  ``next_eps``: the
-        following block's norm1 eps (its statistics are returned), None for the last block."""
+        following block's norm1 eps (its statistics are returned), None for the last block.  ``defer_down``: return
+        (GEGLU output, residual stream) instead of applying the FF down projection (the caller merges it into
+        ``proj_out``)."""
         B, T, C = x.shape
         a1 = self.attn1
         w, b, s = a1.qkv.folded(self.norm1)
@@ -175,6 +180,8 @@ class BasicTransformerBlock(nn.Module):
             x, mr = a2.out.forward_stats(o.view(B, T, H * hd), residual=x, stats="ln", eps=self.norm3.eps)
             w, b, s = proj.folded(self.norm3)
             h = ops.linear(x, w, b, act=proj.act, glu=True, row_affine=(mr, s))
+        if defer_down:
+            return h, x
         down = self.ff.net[2]
         if next_eps is None:
             return down(h, residual=x), None
@@ -207,7 +214,11 @@ class Transformer2DModel(nn.Module):
             h = h.view(B, H * W, C)
             if mr is None:
                 mr = ops.row_moments(h, blocks[0].norm1.eps)
+            merged = self._merged_out(x.is_cuda)
             for i, blk in enumerate(blocks):
+                if i + 1 == len(blocks) and merged is not None:
+                    ffh, hx = blk.forward_folded(h, ctx_kv, mr, None, defer_down=True)
+                    return self._out_merged(ffh, hx, x, merged, stats)
                 h, mr = blk.forward_folded(h, ctx_kv, mr, blocks[i + 1].norm1.eps if i + 1 < len(blocks) else None)
         else:
             h = self.proj_in(self.norm(x, part=xp)).view(B, H * W, C)
@@ -218,6 +229,39 @@ class Transformer2DModel(nn.Module):
             out, op = self.proj_out.forward_stats(h, residual=res, stats="gn")
             return out.view(B, H, W, C), op
         return self.proj_out(h, residual=res).view(B, H, W, C), None
+
+    def _merged_out(self, cuda: bool = True):
+        """The last block's FF down projection merged into ``proj_out`` (both linear, adjacent: out = x + b_po +
+        (h + b_fo + f W_fo^T) W_po^T = x + b' + [f | h] [W_po W_fo | W_po]^T): ONE GEMM over the GEGLU output f and the
+        residual stream h, run as a 1x1 conv over the two sources -- the FF output h + ... is never written or
+        re-read.  Weights product and bias in fp32, cached until a weight changes; None when disabled
+        (SHAI_MERGE_PROJ_OUT=0) or first needed inside a graph capture."""
+        if not MERGE_PROJ_OUT:
+            return None
+        down, po = self.transformer_blocks[-1].ff.net[2], self.proj_out
+        if down.in_features % 64 or po.in_features % 64:
+            return None
+        key = tuple(_wkey(t) for t in (down.weight, down.bias, po.weight, po.bias))
+        cached = getattr(self, "_po_merged", None)
+        if cached is None or cached[0] != key:
+            if cuda and torch.cuda.is_current_stream_capturing():
+                return None
+            wpo = po.weight.float()
+            w = torch.cat([wpo @ down.weight.float(), wpo], 1).to(po.weight.dtype).contiguous()
+            b = po.bias.float() if po.bias is not None else torch.zeros(po.out_features, device=wpo.device)
+            if down.bias is not None:
+                b = b + wpo @ down.bias.float()
+            cached = (key, (w, b.to(po.weight.dtype)))
+            self._po_merged = cached
+        return cached[1]
+
+    def _out_merged(self, ffh, hx, x, merged, stats):
+        B, H, W, C = x.shape
+        w, b = merged
+        f = ffh.reshape(B, H, W, ffh.shape[-1])
+        kw = {"stats": "gn"} if stats and ops.stats_supported(B * H * W, C, "gn", H * W) else {}
+        r = ops.conv2d(f, w, b, 1, 1, x2=hx.reshape(B, H, W, C), residual=x, **kw)
+        return r if kw else (r, None)
 
 
 class Downsample2D(nn.Module):

@@ -71,6 +71,41 @@ def test_unet_norm_handoff_cpu():
     assert rel(y1, y0) < 1e-2
 
 
+def test_unet_merged_proj_out_cpu():
+    """The last transformer block's FF down projection merged into proj_out (one GEMM over [GEGLU out | residual
+    stream] with [W_po W_fo | W_po]) matches the two GEMMs, and the merged weights follow a weight update."""
+    from shai_amd.models import unet2d
+    from shai_amd.models.unet2d import UNet2DConditionModel, UNetConfig
+    torch.manual_seed(4)
+    cfg = UNetConfig.tiny()
+    m = UNet2DConditionModel(cfg).eval()
+    for p in m.parameters():
+        torch.nn.init.normal_(p, std=0.05)
+    x = torch.randn(2, 16, 16, 4).bfloat16()
+    t = torch.tensor([500.0])
+    kv = m.context_kv(torch.randn(2, 77, cfg.cross_attention_dim).bfloat16())
+    old, old_min, old_h = unet2d.MERGE_PROJ_OUT, ops.FOLD_MIN_TILES, unet2d.NORM_HANDOFF
+    try:
+        ops.FOLD_MIN_TILES = 0  # the folded (forward_parts) path at this small size too
+        unet2d.NORM_HANDOFF = True
+        unet2d.MERGE_PROJ_OUT = True
+        y1 = m(x, t, kv)
+        assert any(getattr(mod, "_po_merged", None) is not None for mod in m.modules()), "merged path not taken"
+        unet2d.MERGE_PROJ_OUT = False
+        y0 = m(x, t, kv)
+        assert rel(y1, y0) < 1e-2
+        tr = next(mod for mod in m.modules() if isinstance(mod, unet2d.Transformer2DModel))
+        with torch.no_grad():
+            tr.proj_out.weight.mul_(-1.5)
+        unet2d.MERGE_PROJ_OUT = True
+        y1 = m(x, t, kv)
+        unet2d.MERGE_PROJ_OUT = False
+        y0 = m(x, t, kv)
+        assert rel(y1, y0) < 1e-2
+    finally:
+        unet2d.MERGE_PROJ_OUT, ops.FOLD_MIN_TILES, unet2d.NORM_HANDOFF = old, old_min, old_h
+
+
 def test_vit_norm_handoff_cpu():
     from shai_amd.models import vit
     from shai_amd.models.vit import ViTConfig, ViTEncoderModel
