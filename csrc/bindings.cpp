@@ -70,7 +70,8 @@ std::mutex g_tune_mu;
 std::unordered_map<std::string, Choice> g_tuned;
 
 bool lib_supported(const shai::GemmArgs& g) {
-  return g.conv == 0 && !g.row_mr && g.batch <= 1 && !g.glu && g.act == 0 && !g.bias2d && !g.gate && !g.rms && !g.w_scale &&
+  return g.conv == 0 && !g.row_mr && g.batch <= 1 && !g.w_slice_rows && !g.glu && g.act == 0 && !g.bias2d && !g.gate &&
+         !g.rms && !g.w_scale &&
          !g.A2 && !g.in_scale && g.alpha == 1.f && !(g.bias && g.residual) &&
          (!g.residual || (g.res_alpha == 1.f && g.residual == g.C && g.ldr == g.ldc)) &&
          g.lda >= g.K && g.ldw >= g.K && g.ldc >= g.N;
@@ -84,6 +85,7 @@ std::string gemm_key(const shai::GemmArgs& g) {
   // not be reused by a same-shape problem with a fused epilogue (and vice versa): separate key class
   // a folded-LayerNorm GEMM (row_mr) runs only unsplit on v4: it tunes and caches apart from the plain problem
   return std::string(buf) + (g.rms ? "|rms" : "") + (g.w_scale ? "|fp8w" : "") + (g.row_mr ? "|ln" : "") +
+         (g.w_slice_rows ? "|wslice" + std::to_string(g.w_slice_rows) : "") +
          (lib_supported(g) && !g.residual ? "|lib" : "");
 }
 
@@ -433,6 +435,7 @@ void run_gemm(const shai::GemmArgs& g, const Tensor& like, long a_bytes, long w_
   if (!use_v2(g, a_bytes, w_bytes, a2_bytes)) {
     SHAI_CHECK(g.gate == nullptr, "gated GEMM epilogue needs the v2 kernel (operands < 2 GiB, SHAI_GEMM_V1 unset)");
     SHAI_CHECK(g.row_mr == nullptr, "folded LayerNorm needs the v4 kernel (operands < 2 GiB, SHAI_GEMM_V1 unset)");
+    SHAI_CHECK(g.w_slice_rows == 0, "weight slices need the v4 kernel (operands < 2 GiB, SHAI_GEMM_V1 unset)");
     if (g.conv) {  // the v1 conv instantiations: activation none / silu, silu only with 64-channel sources
       const bool fast = g.Cin % 64 == 0 && (g.A2 == nullptr || g.Cin1 % 64 == 0);
       SHAI_CHECK(!g.glu && (g.act == 0 || (g.act == 1 && fast)), "conv2d output activation ", g.act,
@@ -771,7 +774,7 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
           double res_alpha, int64_t act, bool glu, const optional<Tensor>& gate, int64_t rows_per_gate,
           int64_t force_cfg, double rms_eps, const optional<Tensor>& w_scale, const optional<Tensor>& ln_mr,
           const optional<Tensor>& ln_s, const optional<Tensor>& gn_part, const optional<Tensor>& ln_stats,
-          double ln_eps) {
+          double ln_eps, int64_t w_slice_rows) {
   check_rows(a, "a");
   if (w_scale.has_value()) {  // fp8 (e4m3) weights + fp32 per-row scale: skinny (decode-shaped) kernel only
     SHAI_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat8_e4m3fn && w.dim() == 2 && w.stride(1) == 1 &&
@@ -794,6 +797,13 @@ void gemm(const Tensor& a, const Tensor& w, const Tensor& c, const optional<Tens
   g.M = a.size(-2);
   g.K = a.size(-1);
   g.N = w.size(-2);
+  if (w_slice_rows > 0) {  // w: [M / w_slice_rows * N, K], slice s for rows [s w_slice_rows, (s + 1) w_slice_rows)
+    SHAI_CHECK(a.dim() == 2 && w.dim() == 2 && !glu && g.M % w_slice_rows == 0, "w_slice_rows: 2D, non-GLU, M % rows == 0");
+    const long slices = g.M / w_slice_rows;
+    SHAI_CHECK(w.size(0) % slices == 0, "w_slice_rows: w must hold M / w_slice_rows row slices");
+    g.N = w.size(0) / slices;
+    g.w_slice_rows = w_slice_rows;
+  }
   SHAI_CHECK(w.size(-1) == g.K, "gemm K mismatch: a ", a.sizes(), " w ", w.sizes());
   SHAI_CHECK(g.K % 8 == 0, "gemm K must be a multiple of 8");
   SHAI_CHECK(c.size(-2) == g.M && c.size(-1) == (glu ? g.N / 2 : g.N), "gemm output shape mismatch ", c.sizes());
@@ -1662,7 +1672,7 @@ TORCH_LIBRARY(shai, m) {
   m.def("groupnorm_from_partials(Tensor part1, Tensor? part2, int C1, int C2, int Nimg, int HW, Tensor? gamma, Tensor? beta, Tensor(a!) scale, Tensor(b!) shift, int G, float eps) -> ()");
   m.def("col_partials(Tensor x, Tensor(a!) part) -> ()");
   m.def("row_moments(Tensor x, Tensor(a!) mr, float eps) -> ()");
-  m.def("gemm(Tensor a, Tensor w, Tensor(a!) c, Tensor? bias, Tensor? bias2d, int rows_per_bias2d, Tensor? residual, float alpha, float res_alpha, int act, bool glu, Tensor? gate=None, int rows_per_gate=1, int force_cfg=-1, float rms_eps=-1.0, Tensor? w_scale=None, Tensor? ln_mr=None, Tensor? ln_s=None, Tensor(b!)? gn_part=None, Tensor(c!)? ln_stats=None, float ln_eps=1e-5) -> ()");
+  m.def("gemm(Tensor a, Tensor w, Tensor(a!) c, Tensor? bias, Tensor? bias2d, int rows_per_bias2d, Tensor? residual, float alpha, float res_alpha, int act, bool glu, Tensor? gate=None, int rows_per_gate=1, int force_cfg=-1, float rms_eps=-1.0, Tensor? w_scale=None, Tensor? ln_mr=None, Tensor? ln_s=None, Tensor(b!)? gn_part=None, Tensor(c!)? ln_stats=None, float ln_eps=1e-5, int w_slice_rows=0) -> ()");
   m.def("dequant_fp8(Tensor w8, Tensor scale, Tensor(a!) out) -> ()");
   m.def("layernorm_mod(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, int rows_per_mod, float eps) -> ()");
   m.def("qk_norm_rope(Tensor(a!) x, Tensor? q_w, Tensor? k_w, Tensor? cos, Tensor? sin, int H, int D, int S, float eps) -> ()");

@@ -157,7 +157,8 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
 
   const bf16_t* A = p.A + (long)b * p.batch_a;
   const bf16_t* Wt = p.W + (long)b * p.batch_w;
-  const __amdgpu_buffer_rsrc_t rW = g4_rsrc(Wt, (long)p.N * p.ldw * 2 * (CONV == 3 ? 4 : 1));
+  const long w_sets = CONV == 3 ? 4 : (p.w_slice_rows > 0 ? (p.M + p.w_slice_rows - 1) / p.w_slice_rows : 1);
+  const __amdgpu_buffer_rsrc_t rW = g4_rsrc(Wt, (long)p.N * p.ldw * 2 * w_sets);
   __amdgpu_buffer_rsrc_t rA, rA2;
   if constexpr (CONV != 0) {
     rA = g4_rsrc(A, (long)p.Nimg * p.H * p.Wd * (p.A2 ? p.Cin1 : p.Cin) * 2);
@@ -191,7 +192,9 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
       const int r = wid * (BN / 8) + j * 8 + lrow;  // LDS row
       const int n = n0 + (WIDE ? g4_wperm<BN>(r) : r);
       // phase conv: the tile's phase selects its weight slice (rows ph N .. ph N + N - 1)
-      const long wrow = CONV == 3 ? (long)up2_row(p, m0).ph * p.N + n : (long)n;
+      // phase conv: the tile's phase selects its weight slice; w_slice_rows: the tile's row block does
+      const long wrow = CONV == 3 ? (long)up2_row(p, m0).ph * p.N + n
+                                  : (p.w_slice_rows > 0 ? (long)(m0 / p.w_slice_rows) * p.N + n : (long)n);
       woff[j] = n < p.N ? (uint32_t)((wrow * p.ldw + kchw[j]) * 2) : G4_OOB;
     }
 #pragma unroll
@@ -241,7 +244,7 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
     if ((g & 1) || g == 8) {
       uint32_t off = woff[j] + (uint32_t)k0 * 2;
       if (ktail && k0 + kchw[j] >= k_end) off = G4_OOB;
-      SHAI_DASSERT_DMA(off, (long)p.N * p.ldw * 2 * (CONV == 3 ? 4 : 1), G4_OOB);
+      SHAI_DASSERT_DMA(off, (long)p.N * p.ldw * 2 * w_sets, G4_OOB);
       SHAI_DASSERT(buf >= 0 && buf < 2);
       g4_glds(rW, sa + G4_BM * G4_BK + (wid * (BN / 8) + j * 8) * G4_BK, off);
       return;
@@ -793,6 +796,9 @@ __global__ void __launch_bounds__(512) gemm4_kernel(const GemmArgs p, float* __r
 bool gemm4_supported(const GemmArgs& a) {
   if (a.in_scale != nullptr) return false;
   if (a.K % 8 != 0 || a.lda % 8 != 0 || a.ldw % 8 != 0) return false;  // 16-B source chunks
+  // weight slices: whole 256-row tiles per slice, plain batch-1 GEMM
+  if (a.w_slice_rows != 0 && (a.w_slice_rows % G4_BM != 0 || a.conv || a.batch > 1 || a.M % a.w_slice_rows != 0))
+    return false;
   if (a.conv) {
     if (a.Cin % 64 != 0) return false;
     if (a.A2 != nullptr && a.Cin1 % 64 != 0) return false;

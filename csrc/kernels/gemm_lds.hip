@@ -671,8 +671,9 @@ bool gemm2_cfg_splittable(int cfg) { return cfg != kW4Cfg && cfg != kW4Cfg + 1 &
 bool gemm2_cfg_supported(const GemmArgs& a, int cfg) {
   // an epilogue activation no tile kernel instantiates is never accepted (it would run as another one)
   if (!tile_act_supported(a)) return false;
-  // phase-decomposed upsample conv (upsample == 2): only the v4 kernel maps its rows to output pixels
-  if (a.upsample == 2) return cfg >= kV4Cfg && cfg < kV4Cfg + 4 && gemm4_supported(a);
+  // phase-decomposed upsample conv (upsample == 2) / weight slices: only the v4 kernel maps rows to output pixels
+  // and tiles to weight slices
+  if (a.upsample == 2 || a.w_slice_rows != 0) return cfg >= kV4Cfg && cfg < kV4Cfg + 4 && gemm4_supported(a);
   // folded LayerNorm (row_mr): only the v4 kernel's epilogue applies it, and only unsplit, batch 1
   if (a.row_mr != nullptr)
     return cfg == kWsCfg ? gemm_ws_supported(a) : cfg >= kV4Cfg && cfg < kV4Cfg + 4 && a.batch <= 1 && gemm4_supported(a);

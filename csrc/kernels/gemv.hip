@@ -472,7 +472,7 @@ void launch_dequant_fp8_rows(const uint8_t* w8, const float* scale, bf16_t* out,
 
 // ---------------------------------------------------------------------------- host side
 bool skinny_supported(const GemmArgs& a) {
-  return !a.conv && (a.batch <= 1) && a.M >= 1 && a.M <= 64 && a.K % 8 == 0 && a.N % 2 == 0 &&
+  return !a.conv && (a.batch <= 1) && a.w_slice_rows == 0 && a.M >= 1 && a.M <= 64 && a.K % 8 == 0 && a.N % 2 == 0 &&
          a.bias2d == nullptr && a.gate == nullptr && a.in_scale == nullptr && a.row_mr == nullptr && (a.lda % 8) == 0 &&
          (a.ldw % (a.w_scale ? 16 : 8)) == 0 && (long)a.N * a.ldw * 2 < 0x7fffffffL;
 }

@@ -293,7 +293,8 @@ __global__ void __launch_bounds__(256) skinny2_kernel(const GemmArgs p, float* _
 
 bool skinny2_supported(const GemmArgs& a) {
   // (QUICK_GELU is not instantiated by launch_skinny2: such problems stay on the other kernels)
-  return a.M >= 1 && a.M <= S2_MB && !a.conv && a.batch <= 1 && a.w_scale == nullptr && a.bias2d == nullptr &&
+  return a.M >= 1 && a.M <= S2_MB && !a.conv && a.batch <= 1 && a.w_slice_rows == 0 && a.w_scale == nullptr &&
+         a.bias2d == nullptr &&
          a.act != ACT_QUICK_GELU &&
          a.gate == nullptr && a.row_mr == nullptr && a.K % 8 == 0 && a.lda % 8 == 0 && a.ldw % 8 == 0 && (!a.glu || a.N % 2 == 0) &&
          (long)a.N * a.ldw * 2 < 0x7fffffffL && (long)a.M * a.lda * 2 < 0x7fffffffL;

@@ -142,6 +142,9 @@ struct GemmArgs {
   int row_part_slots;       //   by the row's first value -> LayerNorm (Chan's combine in row_moments_part_kernel
                             //   assumes equal column counts: every slot covers N / slots columns);
                             //   slots = 4 * column tiles
+  // > 0: rows [s w_slice_rows, (s + 1) w_slice_rows) multiply weight slice s (W is [M / w_slice_rows][N][ldw]; v4
+  // kernel only, w_slice_rows % 256 == 0): a per-image weight, e.g. a GroupNorm's per-image scale folded into W
+  int w_slice_rows;
 };
 // (conv, GLU, activation) epilogue variants the tile kernels (v2 / v4 / four-wave / W-stationary / halo conv)
 // instantiate: convolutions NONE / SILU, GLU SILU / GELU / GELU_TANH, plain GEMMs every activation.  Any other

@@ -32,6 +32,8 @@ from .layers import Conv2d, GLULinear, GroupNorm, LayerNorm, Linear, _wkey, time
 
 # the last transformer block's FF down projection merged into proj_out (Transformer2DModel._merged_out)
 MERGE_PROJ_OUT = os.environ.get("SHAI_MERGE_PROJ_OUT", "1") != "0"
+# the Transformer2D input GroupNorm folded into proj_in's weight per image (Transformer2DModel._proj_in_gn_folded)
+GN_FOLD_PROJ_IN = os.environ.get("SHAI_GN_FOLD_PROJ_IN", "1") != "0"
 
 # GroupNorm partials / LayerNorm moments handed from the producing GEMM epilogue to the next norm (and LayerNorms
 # folded into their consumer projections); SHAI_NORM_HANDOFF=0 restores the standalone norm passes (A/B)
@@ -210,7 +212,10 @@ class Transformer2DModel(nn.Module):
         B, H, W, C = x.shape
         blocks = list(self.transformer_blocks)
         if ops.fold_profitable(B * H * W, C):  # the Q projection (N = C) has the fewest tiles of the consumers
-            h, mr = self.proj_in(self.norm(x, part=xp), stats="ln", eps=blocks[0].norm1.eps)
+            if self._gn_fold_ok(x):
+                h, mr = self._proj_in_gn_folded(x, xp, blocks[0].norm1.eps)
+            else:
+                h, mr = self.proj_in(self.norm(x, part=xp), stats="ln", eps=blocks[0].norm1.eps)
             h = h.view(B, H * W, C)
             if mr is None:
                 mr = ops.row_moments(h, blocks[0].norm1.eps)
@@ -229,6 +234,24 @@ class Transformer2DModel(nn.Module):
             out, op = self.proj_out.forward_stats(h, residual=res, stats="gn")
             return out.view(B, H, W, C), op
         return self.proj_out(h, residual=res).view(B, H, W, C), None
+
+    def _gn_fold_ok(self, x) -> bool:
+        B, H, W, C = x.shape
+        # per-image weights (B C^2) well below the activation the apply pass moves (B H W C); 256-row slices
+        return (GN_FOLD_PROJ_IN and (H * W) % 256 == 0 and 2 * C <= H * W and self.proj_in.k == 1
+                and self.proj_in.cin_p == C)
+
+    def _proj_in_gn_folded(self, x, xp, eps):
+        """proj_in(GroupNorm(x)) without the normalised activation: GroupNorm is x s[n, c] + t[n, c] per image n,
+        so proj_in = x (W diag(s_n))^T + (t_n W^T + b): per-image weights (fp32 product, bf16) and a per-image bias,
+        ONE GEMM whose 256-row tiles pick their image's weight (``ops.linear_wslices``) -- the GroupNorm apply pass
+        (a read and a write of x) goes.  Returns (h [B H W, C], LayerNorm (mean, rstd) of h)."""
+        B, H, W, C = x.shape
+        sc, sh = self.norm.scale_shift(x, part=xp)
+        w, b = self.proj_in.weight, self.proj_in.bias
+        ws = (w.float()[None] * sc[:, None, :]).to(w.dtype)
+        b2 = ops.linear(sh.to(w.dtype), w, b)  # t_n W^T + b on the GEMM kernels
+        return ops.linear_wslices(x.view(B * H * W, C), ws, b2, H * W, stats="ln", eps=eps)
 
     def _merged_out(self, cuda: bool = True):
         """The last block's FF down projection merged into ``proj_out`` (both linear, adjacent: out = x + b_po +

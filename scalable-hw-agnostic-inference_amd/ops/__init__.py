@@ -24,7 +24,7 @@ from .reference import (ACT_GELU, ACT_GELU_TANH, ACT_NONE, ACT_QUICK_GELU, ACT_R
 __all__ = [
     "rmsnorm", "layernorm", "groupnorm_stats", "groupnorm_apply", "groupnorm", "linear", "conv2d", "attention",
     "paged_attention", "decode_attention", "kv_write", "rope", "rope_pairs", "gated_act", "bias_act", "sched_step",
-    "softmax_", "embedding", "token_feedback", "decode_attention_rope", "decode_attention_rope_qkv", "gemm_partials", "quantize_fp8_rows", "dequant_fp8", "quant_rows_fp8", "gemm_f8", "pack_conv_weight", "pack_up2_phase_weight", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
+    "softmax_", "embedding", "token_feedback", "decode_attention_rope", "decode_attention_rope_qkv", "gemm_partials", "quantize_fp8_rows", "dequant_fp8", "quant_rows_fp8", "gemm_f8", "pack_conv_weight", "pack_up2_phase_weight", "linear_wslices", "unpack_conv_weight", "act_id", "ACT_NONE", "ACT_SILU", "ACT_GELU",
     "ACT_GELU_TANH", "ACT_QUICK_GELU", "ACT_RELU", "decode_splits", "set_decode_wb",
 ]
 
@@ -284,6 +284,32 @@ def linear_stats(x: torch.Tensor, w: torch.Tensor, bias=None, residual=None, act
         y2 = y.reshape(-1, y.shape[-1])
         return y, (ref.row_moments(y2, eps) if stats == "ln" else ref.col_partials(y2))
     return _linear_norm_io(x, w, bias, act, residual, False, 1.0, 1.0, row_affine, stats, eps, force_cfg)
+
+
+def linear_wslices(x: torch.Tensor, w_slices: torch.Tensor, bias2d: Optional[torch.Tensor], rows_per_slice: int,
+                   stats: Optional[str] = None, eps: float = 1e-5):
+    """y[rows of slice s] = x[rows] w_slices[s]^T + bias2d[s]: one GEMM whose row blocks of ``rows_per_slice`` rows
+    (multiples of 256) each take their own weight [N, K] -- e.g. a GroupNorm's per-image scale folded into the
+    following projection's weight (``Transformer2DModel``).  x [M, K], w_slices [M / rows_per_slice, N, K], bias2d
+    [M / rows_per_slice, N].  ``stats`` as ``linear_stats`` (returns (y, st) then)."""
+    S, N, K = w_slices.shape
+    M = x.shape[0]
+    if not _gpu(x):
+        y = torch.einsum("smk,snk->smn", x.float().view(S, M // S, K), w_slices.float())
+        if bias2d is not None:
+            y = y + bias2d.float()[:, None, :]
+        y = y.reshape(M, N).to(x.dtype)
+        if stats is None:
+            return y
+        return y, (ref.row_moments(y, eps) if stats == "ln" else ref.col_partials(y))
+    y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    gp = torch.empty(M // 128, N, 2, dtype=torch.float32, device=x.device) if stats == "gn" else None
+    ls = torch.empty(M, 2, dtype=torch.float32, device=x.device) if stats == "ln" else None
+    _K().gemm(x, w_slices.reshape(S * N, K), y, None, bias2d, int(rows_per_slice), None, 1.0, 1.0, ACT_NONE, False,
+              None, 1, -1, -1.0, None, None, None, gp, ls, float(eps), int(rows_per_slice))
+    if stats is None:
+        return y
+    return y, (gp if stats == "gn" else ls)
 
 
 def linear_lnout(x: torch.Tensor, w: torch.Tensor, bias, residual: torch.Tensor, gamma, beta, eps: float = 1e-5):

@@ -640,3 +640,15 @@ def test_upsample2d_layer_takes_phase_conv_and_tracks_weight_updates(cuda):
         up.conv.weight.mul_(-0.5)
     y2 = up(x)
     close(y2, ref.conv2d(x, up.conv.weight, up.conv.bias, 3, 3, 1, 1, upsample=True), 3e-2)
+
+
+@pytest.mark.parametrize("S,R,N,K", [(4, 256, 320, 320), (2, 1024, 640, 640), (8, 512, 256, 192)])
+def test_linear_weight_slices(cuda, S, R, N, K):
+    """One GEMM whose row blocks of R rows each take their own weight slice and bias row (v4 kernel, w_slice_rows),
+    with the output's LayerNorm (mean, rstd) from the epilogue."""
+    torch.manual_seed(31)
+    x, w, b2 = rnd(S * R, K), rnd(S, N, K, scale=1 / math.sqrt(K)), rnd(S, N)
+    y, st = ops.linear_wslices(x, w, b2, R, stats="ln", eps=1e-5)
+    want = torch.einsum("smk,snk->smn", x.float().view(S, R, K), w.float()) + b2.float()[:, None, :]
+    close(y, want.reshape(S * R, N), 2e-2)
+    torch.testing.assert_close(st, ref.row_moments(y, 1e-5), atol=2e-3, rtol=2e-3)

@@ -106,6 +106,38 @@ def test_unet_merged_proj_out_cpu():
         unet2d.MERGE_PROJ_OUT, ops.FOLD_MIN_TILES, unet2d.NORM_HANDOFF = old, old_min, old_h
 
 
+def test_unet_proj_in_groupnorm_fold_cpu():
+    """Transformer2D input GroupNorm folded into proj_in per image (per-image weight slices + per-image bias, no
+    normalised activation) matches GroupNorm apply + proj_in; ops.linear_wslices matches its definition."""
+    from shai_amd.models import unet2d
+    from shai_amd.models.unet2d import UNet2DConditionModel, UNetConfig
+    torch.manual_seed(5)
+    x, w, b2 = torch.randn(512, 32).bfloat16(), torch.randn(2, 48, 32).bfloat16(), torch.randn(2, 48).bfloat16()
+    y, st = ops.linear_wslices(x, w, b2, 256, stats="ln", eps=1e-5)
+    want = torch.cat([x[:256].float() @ w[0].float().t() + b2[0].float(), x[256:].float() @ w[1].float().t() + b2[1].float()])
+    assert rel(y, want) < 1e-2 and st.shape == (512, 2)
+    cfg = UNetConfig.tiny()
+    m = UNet2DConditionModel(cfg).eval()
+    for p in m.parameters():
+        torch.nn.init.normal_(p, std=0.05)
+    xs = torch.randn(2, 16, 16, 4).bfloat16()
+    t = torch.tensor([500.0])
+    kv = m.context_kv(torch.randn(2, 77, cfg.cross_attention_dim).bfloat16())
+    tr = next(mod for mod in m.modules() if isinstance(mod, unet2d.Transformer2DModel))
+    old, old_min, old_h = unet2d.GN_FOLD_PROJ_IN, ops.FOLD_MIN_TILES, unet2d.NORM_HANDOFF
+    try:
+        ops.FOLD_MIN_TILES = 0
+        unet2d.NORM_HANDOFF = True
+        unet2d.GN_FOLD_PROJ_IN = True
+        assert tr._gn_fold_ok(torch.empty(2, 16, 16, tr.proj_in.cin_p)), "fold not eligible at the tiny config"
+        y1 = m(xs, t, kv)
+        unet2d.GN_FOLD_PROJ_IN = False
+        y0 = m(xs, t, kv)
+    finally:
+        unet2d.GN_FOLD_PROJ_IN, ops.FOLD_MIN_TILES, unet2d.NORM_HANDOFF = old, old_min, old_h
+    assert rel(y1, y0) < 1e-2
+
+
 def test_vit_norm_handoff_cpu():
     from shai_amd.models import vit
     from shai_amd.models.vit import ViTConfig, ViTEncoderModel
