@@ -95,6 +95,24 @@ class ViTLayer(nn.Module):
             return self.output(h, residual=x), None
         return self.output.forward_stats(h, residual=x, stats="ln", eps=next_eps)
 
+    def forward_cls(self, x, mr=None, keep: int = 1, tail: bool = False):
+        """The last layer when only some tokens leave the encoder: the first ``keep`` (token 0, CLS: image
+        classification) or, with ``tail``, the last ``keep`` (YOLOS's detection tokens).  K / V of every token, the
+        rest -- attention queries, out-projection, MLP -- for the kept tokens only (M = B keep instead of B T).
+        ``mr``: x's LayerNorm moments for the folded QKV (None: the plain norm).  Returns [B, keep, d]."""
+        B, T, C = x.shape
+        sel = slice(T - keep, T) if tail else slice(0, keep)
+        a = self.attention
+        if mr is not None:
+            w, b, s = a.qkv.folded(self.layernorm_before)
+            qkv = ops.linear(x, w, b, row_affine=(mr, s))
+        else:
+            qkv = a.qkv(self.layernorm_before(x))
+        q, k, v = a.split(qkv)
+        o = ops.attention(q[:, sel], k, v).reshape(B, keep, a.heads * a.head_dim)
+        x0 = a.out(o, residual=x[:, sel].contiguous())
+        return self.output(self.intermediate(self.layernorm_after(x0), act=self.act), residual=x0)
+
 
 class ViTEncoderModel(nn.Module):
     def __init__(self, c: ViTConfig):
@@ -112,6 +130,9 @@ class ViTEncoderModel(nn.Module):
         self.layers = nn.ModuleList([ViTLayer(c) for _ in range(c.num_hidden_layers)])
         self.layernorm = LayerNorm(c.hidden_size, c.layer_norm_eps)
 
+    def _kept(self, cls_only: bool):
+        return (1, False) if cls_only else (self.cfg.num_detection_tokens, True)
+
     def pos_embed(self, gh: int, gw: int) -> torch.Tensor:
         """Position embeddings for a (gh, gw) patch grid (bicubic interpolation of the
         trained grid, YOLOS InterpolateInitialPositionEmbeddings semantics)."""
@@ -128,8 +149,10 @@ class ViTEncoderModel(nn.Module):
         patch = patch.flatten(2).transpose(1, 2).to(pe.dtype)
         return torch.cat([cls_pe, patch, det_pe], dim=1)
 
-    def forward(self, pixels: torch.Tensor) -> torch.Tensor:
-        """pixels NHWC [B, H, W, 3] normalised bf16 -> hidden states [B, T, d]."""
+    def forward(self, pixels: torch.Tensor, cls_only: bool = False, det_only: bool = False) -> torch.Tensor:
+        """pixels NHWC [B, H, W, 3] normalised bf16 -> hidden states [B, T, d]; ``cls_only``: [B, 1, d] of token 0,
+        ``det_only``: [B, nd, d] of the detection tokens -- the last layer then runs its query side for those tokens
+        only (``ViTLayer.forward_cls``)."""
         B, H, W, _ = pixels.shape
         x = self.patch(pixels)  # [B, gh, gw, d]
         gh, gw = x.shape[1], x.shape[2]
@@ -144,10 +167,14 @@ class ViTEncoderModel(nn.Module):
             layers = list(self.layers)
             mr = ops.row_moments(x, layers[0].layernorm_before.eps)
             for i, layer in enumerate(layers):
+                if (cls_only or det_only) and i + 1 == len(layers):
+                    return self.layernorm(layer.forward_cls(x, mr, *self._kept(cls_only)))
                 nxt = layers[i + 1].layernorm_before.eps if i + 1 < len(layers) else None
                 x, mr = layer.forward_folded(x, mr, nxt)
             return self.layernorm(x)
-        for layer in self.layers:
+        for i, layer in enumerate(self.layers):
+            if (cls_only or det_only) and i + 1 == len(self.layers):
+                return self.layernorm(layer.forward_cls(x, None, *self._kept(cls_only)))
             x = layer(x)
         return self.layernorm(x)
 
@@ -194,7 +221,7 @@ class ViTForImageClassification(nn.Module):
         self.classifier = Linear(self.cfg.hidden_size, self.cfg.num_labels)
 
     def forward(self, pixels):
-        h = self.vit(pixels)
+        h = self.vit(pixels, cls_only=True)  # the logits read token 0 only
         return self.classifier(h[:, 0].contiguous())
 
     def convert_hf_state_dict(self, sd: dict) -> dict:
@@ -232,8 +259,7 @@ class YolosForObjectDetection(nn.Module):
 
     def forward(self, pixels):
         """-> (logits [B, 100, num_labels+1], boxes [B, 100, 4] (cx, cy, w, h) in [0, 1])."""
-        h = self.vit(pixels)
-        det = h[:, -self.cfg.num_detection_tokens:].contiguous()
+        det = self.vit(pixels, det_only=True).contiguous()  # the heads read the detection tokens only
         logits = self.class_labels_classifier(det)
         boxes = torch.sigmoid(self.bbox_predictor(det).float())
         return logits, boxes

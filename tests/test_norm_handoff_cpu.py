@@ -160,6 +160,35 @@ def test_vit_norm_handoff_cpu():
     assert rel(y1, y0) < 1e-2
 
 
+def test_vit_cls_only_last_layer_cpu():
+    """Classification reads token 0 only: the last layer's query side for that token alone (folded and plain paths)
+    equals token 0 of the full encoder."""
+    from shai_amd.models import vit
+    from shai_amd.models.vit import ViTConfig, ViTEncoderModel
+    torch.manual_seed(6)
+    c = ViTConfig(image_size=(32, 32), patch_size=16, hidden_size=64, num_hidden_layers=2, num_attention_heads=2,
+                  intermediate_size=128)
+    m = ViTEncoderModel(c).eval()
+    for p in m.parameters():
+        torch.nn.init.normal_(p, std=0.05)
+    px = torch.randn(3, 32, 32, 3).bfloat16()
+    old, old_min = vit.NORM_HANDOFF, ops.FOLD_MIN_TILES
+    try:
+        for handoff in (True, False):
+            ops.FOLD_MIN_TILES = 0
+            vit.NORM_HANDOFF = handoff
+            full = m(px)
+            cls = m(px, cls_only=True)
+            assert cls.shape == (3, 1, 64)
+            assert rel(cls[:, 0], full[:, 0]) < 1e-2
+            m.cfg.num_detection_tokens = 2  # the tail form (YOLOS detection tokens), here the last two patch tokens
+            det = m(px, det_only=True)
+            m.cfg.num_detection_tokens = 0
+            assert det.shape == (3, 2, 64) and rel(det, full[:, -2:]) < 1e-2
+    finally:
+        vit.NORM_HANDOFF, ops.FOLD_MIN_TILES = old, old_min
+
+
 def test_up2_phase_weights_match_upsample_conv():
     """Upsample + 3x3 conv == 4 output-phase 2x2 convs over the source with summed weights (gemm_8ph.hip CONV 3)."""
     torch.manual_seed(3)
